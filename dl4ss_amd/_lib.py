@@ -1,0 +1,79 @@
+"""ctypes binding of ``libdl4ss_hip.so`` (the C ABI in ``include/dl4ss_hip.h``).
+
+The product path has no CPU fallback: if the library is missing or a call
+returns a non-zero ``hipError_t`` this raises ``RuntimeError`` with the HIP error
+string.  Tensors are passed as raw device pointers; every call is enqueued on
+torch's current HIP stream.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdl4ss_hip.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F = ctypes.c_float
+
+# name -> argtypes (all return int hipError_t)
+SIGNATURES = {
+    "dl4ss_stft_fwd": [P, LL, I, I, I, I, P, P, P],
+    "dl4ss_istft": [P, LL, I, I, I, I, P, P],
+    "dl4ss_mix_sources": [P, P, I, I, I, P, P, P],
+}
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"dl4ss HIP library not found at {LIB_PATH}; run `python -m dl4ss_amd.build` "
+            "(there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipGetErrorString.restype = ctypes.c_char_p
+    hip.hipGetErrorString.argtypes = [ctypes.c_int]
+    lib._hip = hip
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _load()
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("dl4ss HIP op received a CPU tensor (no CPU fallback)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def call(name, *args):
+    lb = _load()
+    rc = getattr(lb, name)(*args)
+    if rc != 0:
+        msg = lb._hip.hipGetErrorString(rc).decode()
+        raise RuntimeError(f"{name} failed: hipError {rc} ({msg})")
+    return rc

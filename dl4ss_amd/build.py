@@ -1,0 +1,64 @@
+"""In-tree build of ``libdl4ss_hip.so`` (gfx950 only) with plain hipcc.
+
+Every ``dl4ss_amd/csrc/*.hip`` is compiled to an object with
+``hipcc --offload-arch=gfx950 -O3 -fPIC`` (in parallel) and linked into one
+shared library next to this file.  The library exports the C ABI declared in
+``include/dl4ss_hip.h``.  Objects are rebuilt only when a source or header is
+newer than the object.
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "csrc", "_obj")
+LIB = os.path.join(HERE, "libdl4ss_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+         "-Wno-unused-result", "-fvisibility=hidden"]
+
+
+def _newer(src, dst, deps):
+    if not os.path.exists(dst):
+        return True
+    t = os.path.getmtime(dst)
+    return os.path.getmtime(src) > t or any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src, obj):
+    cmd = [HIPCC, *FLAGS, "-I", CSRC, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return obj
+
+
+def build(verbose=False, jobs=None):
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    objs, todo = [], []
+    for f in srcs:
+        src = os.path.join(CSRC, f)
+        obj = os.path.join(OBJ, f[:-4] + ".o")
+        objs.append(obj)
+        if _newer(src, obj, headers):
+            todo.append((src, obj))
+    jobs = jobs or min(8, max(1, len(todo)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        for obj in ex.map(lambda a: _compile(*a), todo):
+            if verbose:
+                print("compiled", os.path.basename(obj), file=sys.stderr)
+    if todo or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

@@ -1,0 +1,98 @@
+"""GPU parity of the STFT / iSTFT / mixing kernels against the CPU oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+from oracle import dsp
+from dl4ss_amd import ops, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _sig(n_sig, N, seed):
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal((n_sig, N)).astype(np.float32)
+
+
+@pytest.mark.parametrize("N", [32000, 40000, 2000, 300, 1000 * 3 + 77])
+def test_stft_matches_oracle(dev, N):
+    x = _sig(3, N, N)
+    X, mag = ops.stft(torch.from_numpy(x).to(dev))
+    T = dsp.n_frames(N)
+    assert X.shape == (3, T, 129, 2) and mag.shape == (3, T, 129)
+    X, mag = X.cpu().numpy(), mag.cpu().numpy()
+    for i in range(3):
+        S = dsp.stft_tf(x[i].astype(np.float64))
+        scale = np.abs(S).max()
+        assert np.abs(X[i, ..., 0] - S.real).max() < 2e-6 * scale
+        assert np.abs(X[i, ..., 1] - S.imag).max() < 2e-6 * scale
+        assert np.abs(mag[i] - np.abs(S)).max() < 2e-6 * scale
+
+
+def test_stft_golden_fixture(dev):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "stft_golden.npz"))
+    X, _ = ops.stft(torch.from_numpy(g["x"]).to(dev), mag_out=False)
+    X = X.cpu().numpy()
+    scale = np.sqrt(g["re"] ** 2 + g["im"] ** 2).max()
+    assert np.abs(X[..., 0] - g["re"]).max() < 2e-6 * scale
+    assert np.abs(X[..., 1] - g["im"]).max() < 2e-6 * scale
+
+
+def test_stft_logmag_and_conj(dev):
+    x = _sig(2, 4000, 5)
+    xt = torch.from_numpy(x).to(dev)
+    _, lm = ops.stft(xt, complex_out=False, log=True)
+    Xc, _ = ops.stft(xt, mag_out=False, conj=True)
+    for i in range(2):
+        np.testing.assert_allclose(lm[i].cpu().numpy(), dsp.log_magnitude(x[i]), atol=2e-4)
+        S = dsp.stft_tf(x[i].astype(np.float64), conj=True)
+        np.testing.assert_allclose(Xc[i, ..., 1].cpu().numpy(), S.imag, atol=2e-4)
+
+
+def test_stft_frame_indices_bit_exact(dev):
+    """An impulse at sample n must land exactly in the frames covering n."""
+    N = 4000
+    for n in [0, 1, 127, 128, 129, 2047, 3999]:
+        x = np.zeros((1, N), np.float32)
+        x[0, n] = 1.0
+        _, mag = ops.stft(torch.from_numpy(x).to(dev), complex_out=False)
+        m = mag[0].cpu().numpy()
+        ref = dsp.magnitude(x[0])
+        nz = np.nonzero(ref.max(axis=1) > 1e-6)[0].tolist()
+        got = np.nonzero(m.max(axis=1) > 1e-6)[0].tolist()
+        assert got == nz, (n, got, nz)
+
+
+@pytest.mark.parametrize("T", [251, 313, 17, 2])
+def test_istft_matches_oracle(dev, T):
+    rng = np.random.default_rng(T)
+    S = (rng.standard_normal((2, T, 129)) + 1j * rng.standard_normal((2, T, 129))).astype(np.complex64)
+    Sd = torch.from_numpy(np.stack([S.real, S.imag], -1).astype(np.float32)).to(dev)
+    y = ops.istft(Sd).cpu().numpy()
+    for i in range(2):
+        ref = dsp.istft(S[i].T)
+        assert y.shape[1] == ref.shape[0] == 128 * (T - 1)
+        np.testing.assert_allclose(y[i], ref, atol=2e-5 * np.abs(ref).max())
+
+
+def test_stft_istft_round_trip_full_size(dev):
+    x = torch.from_numpy(_sig(64, 32000, 9)).to(dev)
+    X, _ = ops.stft(x, mag_out=False)
+    y = ops.istft(X)
+    assert torch.allclose(y, x, atol=1e-4)
+
+
+def test_mix_sources_matches_oracle(dev):
+    gen = synth.SyntheticMixtures(n_samples=32000, k=2, seed=3)
+    src, spk, u = gen.batch(4)
+    g = synth.gains_for(u, 2)
+    out = ops.mix_sources(torch.from_numpy(src.astype(np.float32)).to(dev),
+                          torch.from_numpy(g.astype(np.float32)).to(dev)).cpu().numpy()
+    for b in range(4):
+        srcs = [dsp.normalise_source(src[b, k].astype(np.float32), 32000) for k in range(2)]
+        s, m = dsp.mix_sources(srcs, g[b])
+        np.testing.assert_allclose(out[b, :2], s, atol=1e-5)
+        np.testing.assert_allclose(out[b, 2], m, atol=2e-5)
