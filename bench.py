@@ -1,0 +1,225 @@
+"""Benchmark: mixtures/sec of the full separation training step on MI355X.
+
+Workload (BASELINE.json configs[1]): 2-speaker synthetic
+WSJ0-shaped mixtures, 8 kHz, 4 s (N = 32000 -> T = 251, F = 129), BiLSTM-4L
+(H = 300) mask net, Linear(600 -> 129*50) + tanh, embedding + ADDJUST queries,
+label-ordered MSE + 0.5 sum-to-one loss, backward, (DP all-reduce), Adam --
+32 mixtures per GPU per step (weak scaling).  Inputs (raw sources, gains,
+speaker ids) are resident in HBM before the timed region; the step starts at
+preprocessing + STFT.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|bf16]
+
+N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--mode", default="label", choices=["label", "pit"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, N, K):
+    """Reference CPU path (the oracle restatement, torch-CPU fp32 + numpy FFT) on a
+    bounded sample of the same workload: cpu_batch mixtures of the B=32 batch."""
+    from oracle import dsp, model as om
+    from dl4ss_amd import synth
+
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(cores)
+    torch.manual_seed(1)
+    ref = om.SepModel(cell="lstm", num_layers=4)
+    opt = om.make_adam(ref)
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1)
+    src, spk, u = gen.batch(args.cpu_batch)
+    gains = synth.gains_for(u, K)
+
+    def one_step():
+        feats, Y = [], []
+        for b in range(args.cpu_batch):
+            srcs = [dsp.normalise_source(src[b, k], N) for k in range(K)]
+            s, m = dsp.mix_sources(srcs, gains[b])
+            _ = dsp.stft_tf(m)  # mix_phase (reference computes it, predata_multiAims_dB.py:214)
+            feats.append(dsp.magnitude(m))
+            Y.append(np.stack([dsp.magnitude(s[k]) for k in range(K)]))
+        f = torch.from_numpy(np.array(feats))
+        om.train_step(ref, opt, f, f, torch.from_numpy(np.array(Y)), torch.from_numpy(spk))
+
+    one_step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        one_step()
+    dt = time.perf_counter() - t0
+    return {"value": args.cpu_batch * args.cpu_steps / dt, "unit": "mixtures/s", "cores": cores, "kind": "port",
+            "sample": f"{args.cpu_steps} step(s) of {args.cpu_batch} mixtures (of the B={args.batch} workload), "
+                      "oracle torch-CPU fp32 BiLSTM-4L fwd+bwd+Adam incl. numpy STFT features"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    from dl4ss_amd import engine, ops, synth
+
+    B, K, N = args.batch, 2, 32000
+    net = engine.SepNet(cell="lstm", num_layers=4, hidden=300, emb=50, num_labels=101, device=dev, seed=1)
+    if world > 1:  # identical initial weights on every rank
+        import torch.distributed as dist
+
+        dist.broadcast(net.flat, 0)
+    tr = engine.SepTrainer(net, B, K, N, mode=args.mode, precision=args.precision, process_group=pg)
+
+    # synthetic input pool, resident in HBM (seed 1 + 1000 * rank)
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1, rank=rank)
+    pool = []
+    for _ in range(4):
+        src, spk, u = gen.batch(B)
+        pool.append((torch.from_numpy(src.astype(np.float32)).to(dev),
+                     torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
+                     torch.from_numpy(spk.astype(np.int32)).to(dev)))
+
+    # per-phase HIP events on the stream the kernels run on (torch's current stream)
+    ev = {"stft": []}
+
+    def timed_step(i, record):
+        raw, gains, spk = pool[i % len(pool)]
+        if not record:
+            return tr.step(raw, gains, spk)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tr.spk.copy_(spk)
+        ops.mix_sources(raw, gains, out_src=tr.src, out_mix=tr.mix, stats_ws=tr.stats)
+        e0.record()  # the two STFT launches (mixtures, then sources) of engine.SepTrainer.features
+        ops.stft(tr.mix, complex_out=False, mag_out=True, out_mag=tr.mag_mix)
+        ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
+        e1.record()
+        ev["stft"].append((e0, e1))
+        tr.forward()
+        loss = tr.loss_and_grad()
+        tr.backward()
+        tr.allreduce()
+        tr.optimizer_step()
+        return loss
+
+    for i in range(args.warmup):
+        timed_step(i, False)
+    tr.check()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    s0.record()
+    for i in range(args.steps):
+        loss = timed_step(i, True)
+    s1.record()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    tr.check()
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_v = float(loss[0].item())
+    if not np.isfinite(loss_v):
+        raise RuntimeError("non-finite loss")
+
+    # ---- roofline of the two north-star kernels (STFT in-step events; input GEMM isolated), same stream
+    T, F = tr.T, tr.F
+    stft_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["stft"]]))
+    stft_bytes = B * (K + 1) * (4 * N + 4 * T * F)  # mag-only STFT of mixture + K sources
+    # input-projection GEMM of BiLSTM layer 1..3 (M = B*T, N = 2400, K = 600), timed in isolation
+    x = tr.out[0].view(B * T, -1)
+    wih = net.cat_view("weight_ih", 1)
+    bih = net.cat_view("bias_ih", 1)
+    for _ in range(3):
+        ops.gemm(x, wih, transB=True, bias=bih, out=tr.G, precision=args.precision)
+    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g0.record()
+    for _ in range(20):
+        ops.gemm(x, wih, transB=True, bias=bih, out=tr.G, precision=args.precision)
+    g1.record()
+    torch.cuda.synchronize()
+    gemm_ms = g0.elapsed_time(g1) / 20
+    gemm_flops = 2.0 * B * T * 600 * 2400
+
+    if rank == 0:
+        value = B * world * args.steps / elapsed
+        stft_gbs = stft_bytes / (stft_ms * 1e-3) / 1e9
+        gemm_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12
+        out = {
+            "metric": "mixtures/sec (8 kHz, 4 s, 2-spk WSJ0-shape) at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "mixtures/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.precision == "fp32" else "bf16",
+            "data": "synthetic speech-shaped sources (harmonic stack + AM + noise), seed 1+1000*rank, HBM-resident",
+            "config": {"workload": "C2: 2-spk label-ordered BiLSTM-4L magnitude mask, B=32/GPU, N=32000 (T=251,F=129),"
+                                   " full step: mix+STFT+fwd+loss+bwd+allreduce+Adam",
+                       "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                       "precision": args.precision, "loss": args.mode},
+            "loss": loss_v,
+            "roofline": {"bound": "hbm", "kernel": "stft_fwd (2 launches/step: 32 mixtures + 64 sources, mag)", "achieved": stft_gbs,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "launch_ms": stft_ms, "algorithmic_bytes": stft_bytes},
+            "roofline_mfma": {"bound": "mfma", "kernel": "gemm (BiLSTM input projection 8032x2400x600)",
+                              "achieved": gemm_tf, "peak": MFMA_PEAK[args.precision], "unit": "TFLOP/s",
+                              "frac": gemm_tf / MFMA_PEAK[args.precision], "launch_ms": gemm_ms},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args, N, K)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -22,8 +22,22 @@ F = ctypes.c_float
 SIGNATURES = {
     "dl4ss_stft_fwd": [P, LL, I, I, I, I, P, P, P],
     "dl4ss_istft": [P, LL, I, I, I, I, P, P],
-    "dl4ss_mix_sources": [P, P, I, I, I, P, P, P],
+    "dl4ss_mix_sources": [P, P, I, I, I, P, P, P, P],
+    "dl4ss_gemm": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, P],
+    "dl4ss_birnn_workspace_bytes": [I, I, I],
+    "dl4ss_birnn_fwd": [I, I, I, I, P, P, P, P, P, P, P, P, LL, P, P],
+    "dl4ss_birnn_bwd": [I, I, I, I, P, P, P, P, P, P, P, P, P, LL, P, P],
+    "dl4ss_attn_nblk": [I, I],
+    "dl4ss_mask_attn_loss": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, P, P, P, P],
+    "dl4ss_pit_select": [P, I, I, I, P, P],
+    "dl4ss_loss_finalize": [P, I, I, I, P, F, F, P, P, I, P, P],
+    "dl4ss_query_fwd": [P, I, I, I, P, P, P, I, I, P, P, P],
+    "dl4ss_query_bwd": [P, I, I, I, P, P, P, P, I, I, P, P, P, P],
+    "dl4ss_colsum": [P, LL, I, I, P, P],
+    "dl4ss_adam": [P, P, P, P, LL, F, F, F, F, I, P],
 }
+# entry points that return a value rather than a hipError_t
+RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int}
 
 _lib = None
 
@@ -40,7 +54,7 @@ def _load():
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_int
+        fn.restype = RESTYPES.get(name, ctypes.c_int)
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipGetErrorString.restype = ctypes.c_char_p
     hip.hipGetErrorString.argtypes = [ctypes.c_int]
@@ -68,6 +82,11 @@ def ptr(t):
     if not t.is_cuda:
         raise RuntimeError("dl4ss HIP op received a CPU tensor (no CPU fallback)")
     return ctypes.c_void_p(t.data_ptr())
+
+
+def query(name, *args):
+    """Call an entry point that returns a value (sizes), not an error code."""
+    return getattr(_load(), name)(*args)
 
 
 def call(name, *args):

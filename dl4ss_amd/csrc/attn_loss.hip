@@ -1,0 +1,419 @@
+// Fused speaker-query mask attention + separation loss + its backward.
+//
+// Replaces, for the magnitude path (TDAA_beta/main_run_sstune_EvalVer.py:615-666,
+// Torch_multi/main_run.py:478-506):
+//     V.expand(B,K,...).contiguous()          (414 MB copy at B=32)
+//     baddbmm(V, q) -> sigmoid                 mask (B,K,T,F)
+//     predict = mask * |X| ; MSE(predict, Y) + 0.5 * MSE(sum_k mask, 1)
+// and for the cRM path (main_run_sstune_cRM_EvalVer.py:259-271, 688, 720-743):
+//     Mc = 10 tanh(V.q_{re,im}); M = -1/0.1 log((10 - Mc)/(10 + Mc));
+//     P = M (x) X (complex product); MSE(P_re, Y_re) + MSE(P_im, Y_im)
+// together with the whole backward down to dPre = dL/d(h W^T + b) of the
+// Linear+tanh that produced V, and dq = dL/dq.
+//
+// One pass reads each V row (E floats) exactly once: a workgroup stages a 256-row
+// tile of V with coalesced 16-B loads into LDS, each lane owns one (b,t,f) row
+// (8-B LDS reads: conflict-free for E = 50), computes the K logits / masks /
+// costs, and in the GRAD pass writes the dPre row back into the same LDS tile
+// for a coalesced store.  Loss terms and dq are reduced per workgroup (wave
+// shuffles + LDS) into per-block partials that a finalize kernel sums in fixed
+// order (bitwise deterministic).  PIT: the COST pass produces the K x K pairwise
+// cost matrix per utterance, `pit_select` picks the lowest-index minimising
+// permutation, the GRAD pass uses it; label order (the reference) = identity.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int TILE = 256;  // rows per tile
+
+template <int K>
+struct Perms;
+template <>
+struct Perms<1> { static constexpr int N = 1; static constexpr int P[1][1] = {{0}}; };
+template <>
+struct Perms<2> { static constexpr int N = 2; static constexpr int P[2][2] = {{0, 1}, {1, 0}}; };
+template <>
+struct Perms<3> {
+  static constexpr int N = 6;
+  static constexpr int P[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+};
+
+struct AttnArgs {
+  int B, T, F, rows_per_b, nblk;  // rows_per_b = T*F ; nblk = blocks per utterance
+  const float* V;                 // (B, T*F, E)
+  const float* q;                 // (B, K, QW)
+  const float* X;                 // mag: (b*xs + row) ; cRM: (b*xs + row)*2
+  long long xs;
+  const float* Y;                 // target k of b: Y + b*ys + k*yks (+row, cRM *2)
+  long long ys, yks;
+  const int* perm;                // (B, K) target index per channel, null = identity
+  float s1, s2;                   // loss scales: MSE term, sum-to-one term
+  float* dPre;                    // (B, T*F, E) GRAD pass output
+  float* part_loss;               // (B, nblk, K*K + 1)
+  float* part_dq;                 // (B, nblk, K, QW)
+  float* mask_out;                // optional (B, K, T*F) [cRM: x2]
+  float* pred_out;                // optional (B, K, T*F) [cRM: x2]
+};
+
+template <int E, int K, bool CRM, bool GRAD>
+__global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
+  constexpr int QW = CRM ? 2 * E : E;
+  constexpr int NC = CRM ? 2 : 1;  // components per bin
+  __shared__ __attribute__((aligned(16))) float sv[TILE * E];
+  __shared__ float sq[K * QW];
+  __shared__ float sred[NT / 64][K * K + 1];
+
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < K * QW; i += NT) sq[i] = a.q[(long long)b * K * QW + i];
+
+  // this block's row range
+  const int per = (a.rows_per_b + a.nblk - 1) / a.nblk;
+  const int rbeg = blockIdx.x * per;
+  const int rend = min(a.rows_per_b, rbeg + per);
+
+  int pm[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) pm[k] = a.perm ? a.perm[b * K + k] : k;
+
+  float cost[K * K + 1];
+#pragma unroll
+  for (int i = 0; i < K * K + 1; ++i) cost[i] = 0.f;
+  __shared__ float sdl[GRAD ? TILE * K * NC : 1];  // dL/dlogit per tile row
+  float dqa[2] = {0.f, 0.f};  // dq[j] for j = tid, tid + 256 (j < K*QW)
+  const float* Vb = a.V + (long long)b * a.rows_per_b * E;
+  float* Db = GRAD ? a.dPre + (long long)b * a.rows_per_b * E : nullptr;
+
+  for (int r0 = rbeg; r0 < rend; r0 += TILE) {
+    const int nr = min(TILE, rend - r0);
+    __syncthreads();  // previous tile fully consumed (and sq visible on first pass)
+    // coalesced stage of nr rows (nr*E floats, 16-B aligned when r0*E*4 % 16 == 0)
+    {
+      const float* src = Vb + (long long)r0 * E;
+      const int n = nr * E;
+      if ((((long long)r0 * E) & 3) == 0) {
+        const int n4 = n >> 2;
+        for (int i = tid; i < n4; i += NT) reinterpret_cast<float4*>(sv)[i] = reinterpret_cast<const float4*>(src)[i];
+        for (int i = (n4 << 2) + tid; i < n; i += NT) sv[i] = src[i];
+      } else {
+        for (int i = tid; i < n; i += NT) sv[i] = src[i];
+      }
+    }
+    __syncthreads();
+    const int r = tid;
+    if (r < nr) {
+      const int row = r0 + r;
+      const float* v = sv + r * E;
+      float lg[K * NC];
+#pragma unroll
+      for (int i = 0; i < K * NC; ++i) lg[i] = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; e += 2) {
+        const float2 vv = *reinterpret_cast<const float2*>(v + e);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            lg[k * NC + c] = fmaf(vv.x, sq[k * QW + c * E + e], lg[k * NC + c]);
+            lg[k * NC + c] = fmaf(vv.y, sq[k * QW + c * E + e + 1], lg[k * NC + c]);
+          }
+      }
+      float dl[K * NC];  // dL/dlogit
+      if constexpr (!CRM) {
+        const float x = a.X[(long long)b * a.xs + row];
+        float m[K], y[K], msum = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          m[k] = sigmoidf_(lg[k]);
+          msum += m[k];
+          y[k] = a.Y[(long long)b * a.ys + (long long)k * a.yks + row];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const float dd = m[k] * x - y[j];
+            cost[k * K + j] = fmaf(dd, dd, cost[k * K + j]);
+          }
+        const float ds = msum - 1.0f;
+        cost[K * K] = fmaf(ds, ds, cost[K * K]);
+        if (a.mask_out || a.pred_out) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const long long o = ((long long)b * K + k) * a.rows_per_b + row;
+            if (a.mask_out) a.mask_out[o] = m[k];
+            if (a.pred_out) a.pred_out[o] = m[k] * x;
+          }
+        }
+        if constexpr (GRAD) {
+          float yp[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            yp[k] = y[0];
+#pragma unroll
+            for (int j = 1; j < K; ++j) yp[k] = pm[k] == j ? y[j] : yp[k];
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const float dm = 2.f * a.s1 * (m[k] * x - yp[k]) * x + 2.f * a.s2 * ds;
+            dl[k] = dm * m[k] * (1.f - m[k]);
+          }
+        }
+      } else {
+        const float2 x = *reinterpret_cast<const float2*>(a.X + 2 * ((long long)b * a.xs + row));
+        float2 p[K], y[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          // cRM_EvalVer.py:269 (10 tanh) and :688 (inverse compression), fp32 as the reference
+          const float mcr = 10.f * tanhf(lg[k * 2]);
+          const float mci = 10.f * tanhf(lg[k * 2 + 1]);
+          const float mr = -10.f * logf((10.f - mcr) / (10.f + mcr));
+          const float mi = -10.f * logf((10.f - mci) / (10.f + mci));
+          p[k] = make_float2(mr * x.x - mi * x.y, mr * x.y + mi * x.x);
+          y[k] = *reinterpret_cast<const float2*>(a.Y + 2 * ((long long)b * a.ys + (long long)k * a.yks + row));
+          if (a.mask_out) {
+            const long long o = 2 * (((long long)b * K + k) * a.rows_per_b + row);
+            a.mask_out[o] = mr;
+            a.mask_out[o + 1] = mi;
+          }
+          if (a.pred_out) {
+            const long long o = 2 * (((long long)b * K + k) * a.rows_per_b + row);
+            a.pred_out[o] = p[k].x;
+            a.pred_out[o + 1] = p[k].y;
+          }
+          if constexpr (GRAD) {
+            // d(M)/d(logit) through the same fp32 chain: dM/dMc * dMc/dl
+            const float dmc_r = 10.f * (1.f / (10.f - mcr) + 1.f / (10.f + mcr));
+            const float dmc_i = 10.f * (1.f / (10.f - mci) + 1.f / (10.f + mci));
+            dl[k * 2] = dmc_r * (10.f * (1.f - (mcr * 0.1f) * (mcr * 0.1f)));
+            dl[k * 2 + 1] = dmc_i * (10.f * (1.f - (mci * 0.1f) * (mci * 0.1f)));
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const float dr = p[k].x - y[j].x, di = p[k].y - y[j].y;
+            cost[k * K + j] = fmaf(dr, dr, fmaf(di, di, cost[k * K + j]));
+          }
+        if constexpr (GRAD) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            float2 yp = y[0];
+#pragma unroll
+            for (int j = 1; j < K; ++j) yp = pm[k] == j ? y[j] : yp;
+            const float gr = 2.f * a.s1 * (p[k].x - yp.x), gi = 2.f * a.s1 * (p[k].y - yp.y);
+            // P = M (x) X: dMr = gr xr + gi xi ; dMi = -gr xi + gi xr
+            const float dmr = gr * x.x + gi * x.y;
+            const float dmi = -gr * x.y + gi * x.x;
+            dl[k * 2] *= dmr;
+            dl[k * 2 + 1] *= dmi;
+          }
+        }
+      }
+      if constexpr (GRAD) {
+#pragma unroll
+        for (int i = 0; i < K * NC; ++i) sdl[r * K * NC + i] = dl[i];
+      }
+    } else if (GRAD) {
+#pragma unroll
+      for (int i = 0; i < K * NC; ++i) sdl[r * K * NC + i] = 0.f;
+    }
+    if constexpr (GRAD) {
+      __syncthreads();
+      // dq[k][c*E+e] += sum_r dl[r][k*NC+c] V[r][e]   (lanes along e: conflict-free)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = tid + NT * h;
+        if (j < K * QW) {
+          const int k = j / QW, ce = j % QW, c = ce / E, e = ce % E;
+          float acc = 0.f;
+          for (int rr = 0; rr < nr; ++rr) acc = fmaf(sdl[rr * K * NC + k * NC + c], sv[rr * E + e], acc);
+          dqa[h] += acc;
+        }
+      }
+      __syncthreads();
+      // dV[e] = sum_k dl_k q_k[e] ; dPre = dV (1 - V^2), written in place over the own row
+      if (r < nr) {
+        float* v = sv + r * E;
+        float dl[K * NC];
+#pragma unroll
+        for (int i = 0; i < K * NC; ++i) dl[i] = sdl[r * K * NC + i];
+#pragma unroll
+        for (int e = 0; e < E; e += 2) {
+          const float2 vv = *reinterpret_cast<const float2*>(v + e);
+          float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              const float d = dl[k * NC + c];
+              g0 = fmaf(d, sq[k * QW + c * E + e], g0);
+              g1 = fmaf(d, sq[k * QW + c * E + e + 1], g1);
+            }
+          *reinterpret_cast<float2*>(v + e) = make_float2(g0 * (1.f - vv.x * vv.x), g1 * (1.f - vv.y * vv.y));
+        }
+      }
+    }
+    if constexpr (GRAD) {
+      __syncthreads();
+      float* dst = Db + (long long)r0 * E;
+      const int n = nr * E;
+      if ((((long long)r0 * E) & 3) == 0) {
+        const int n4 = n >> 2;
+        for (int i = tid; i < n4; i += NT) reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(sv)[i];
+        for (int i = (n4 << 2) + tid; i < n; i += NT) dst[i] = sv[i];
+      } else {
+        for (int i = tid; i < n; i += NT) dst[i] = sv[i];
+      }
+    }
+  }
+
+  // ---- block reductions (fixed order: wave shuffle, then waves 0..3)
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < K * K + 1; ++i) {
+    const float s = wave_sum(cost[i]);
+    if (lane == 0) sred[wave][i] = s;
+  }
+  __syncthreads();
+  float* pl = a.part_loss + ((long long)b * a.nblk + blockIdx.x) * (K * K + 1);
+  if (tid < K * K + 1) pl[tid] = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
+  if constexpr (GRAD) {
+    float* pd = a.part_dq + ((long long)b * a.nblk + blockIdx.x) * K * QW;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (tid + NT * h < K * QW) pd[tid + NT * h] = dqa[h];
+  }
+}
+
+// PIT selection: per utterance, lowest-index permutation minimising sum_k C[k][perm k]
+template <int K>
+__global__ void pit_select_kernel(const float* __restrict__ part, int B, int nblk, int* __restrict__ perm) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float C[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) C[i] = 0.f;
+  for (int blk = 0; blk < nblk; ++blk)
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) C[i] += part[((long long)b * nblk + blk) * (K * K + 1) + i];
+  int best = 0;
+  float bc = 0.f;
+  for (int p = 0; p < Perms<K>::N; ++p) {
+    float c = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) c += C[k * K + Perms<K>::P[p][k]];
+    if (p == 0 || c < bc) { bc = c; best = p; }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) perm[b * K + k] = Perms<K>::P[best][k];
+}
+
+// loss = s1 * sum_b sum_k C[b][k][perm k] + s2 * S ; also dq = sum_blk part_dq (fixed order)
+template <int K>
+__global__ void finalize_kernel(const float* __restrict__ part, int B, int nblk, const int* __restrict__ perm,
+                                float s1, float s2, float* __restrict__ loss_out, const float* __restrict__ part_dq,
+                                int qw, float* __restrict__ dq) {
+  // block 0: loss (single thread, fixed order) ; other threads: dq
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 0) {
+    double l1 = 0.0, l2 = 0.0;
+    for (int b = 0; b < B; ++b) {
+      for (int blk = 0; blk < nblk; ++blk) {
+        const float* p = part + ((long long)b * nblk + blk) * (K * K + 1);
+#pragma unroll
+        for (int k = 0; k < K; ++k) l1 += p[k * K + (perm ? perm[b * K + k] : k)];
+        l2 += p[K * K];
+      }
+    }
+    loss_out[0] = (float)(s1 * l1 + s2 * l2);
+    loss_out[1] = (float)(s1 * l1);
+    loss_out[2] = (float)(s2 * l2);
+  }
+  if (dq) {
+    const int n = B * K * qw;
+    for (int i = tid; i < n; i += gridDim.x * blockDim.x) {
+      const int b = i / (K * qw), j = i % (K * qw);
+      float s = 0.f;
+      for (int blk = 0; blk < nblk; ++blk) s += part_dq[((long long)b * nblk + blk) * K * qw + j];
+      dq[i] = s;
+    }
+  }
+}
+
+template <int E, int K, bool CRM>
+int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
+  dim3 grid(a.nblk, a.B);
+  if (grad)
+    hipLaunchKernelGGL((attn_kernel<E, K, CRM, true>), grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((attn_kernel<E, K, CRM, false>), grid, dim3(NT), 0, st, a);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+int dispatch(int E, int K, int crm, bool grad, const AttnArgs& a, hipStream_t st) {
+  if (E != 50) return (int)hipErrorInvalidValue;
+  if (!crm) {
+    if (K == 1) return launch_attn<50, 1, false>(grad, a, st);
+    if (K == 2) return launch_attn<50, 2, false>(grad, a, st);
+    if (K == 3) return launch_attn<50, 3, false>(grad, a, st);
+  } else {
+    if (K == 1) return launch_attn<50, 1, true>(grad, a, st);
+    if (K == 2) return launch_attn<50, 2, true>(grad, a, st);
+    if (K == 3) return launch_attn<50, 3, true>(grad, a, st);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+DL4SS_API int dl4ss_attn_nblk(int T, int F) {
+  // ~4 tiles per block
+  const int rows = T * F;
+  int nblk = (rows + 4 * TILE - 1) / (4 * TILE);
+  return nblk < 1 ? 1 : nblk;
+}
+
+// pass: 0 = COST (costs / masks only), 1 = GRAD (costs + dPre + dq partials)
+DL4SS_API int dl4ss_mask_attn_loss(int pass, int crm, int B, int K, int T, int F, int E, const float* V,
+                                   const float* q, const float* X, long long x_bstride, const float* Y,
+                                   long long y_bstride, long long y_kstride, const int* perm, float s1, float s2,
+                                   float* dPre, float* part_loss, float* part_dq, float* mask_out,
+                                   float* pred_out, void* stream) {
+  DL4SS_REQUIRE(B > 0 && K >= 1 && K <= 3 && T > 0 && F > 0 && V && q && X && Y && part_loss);
+  DL4SS_REQUIRE(pass == 0 || (dPre && part_dq));
+  AttnArgs a{};
+  a.B = B; a.T = T; a.F = F; a.rows_per_b = T * F; a.nblk = dl4ss_attn_nblk(T, F);
+  a.V = V; a.q = q; a.X = X; a.xs = x_bstride; a.Y = Y; a.ys = y_bstride; a.yks = y_kstride;
+  a.perm = perm; a.s1 = s1; a.s2 = s2; a.dPre = dPre; a.part_loss = part_loss; a.part_dq = part_dq;
+  a.mask_out = mask_out; a.pred_out = pred_out;
+  return dispatch(E, K, crm, pass == 1, a, as_stream(stream));
+}
+
+DL4SS_API int dl4ss_pit_select(const float* part_loss, int B, int K, int nblk, int* perm, void* stream) {
+  DL4SS_REQUIRE(part_loss && perm && B > 0 && K >= 1 && K <= 3);
+  hipStream_t st = as_stream(stream);
+  dim3 grid(cdiv(B, 64)), blk(64);
+  if (K == 1) hipLaunchKernelGGL(pit_select_kernel<1>, grid, blk, 0, st, part_loss, B, nblk, perm);
+  if (K == 2) hipLaunchKernelGGL(pit_select_kernel<2>, grid, blk, 0, st, part_loss, B, nblk, perm);
+  if (K == 3) hipLaunchKernelGGL(pit_select_kernel<3>, grid, blk, 0, st, part_loss, B, nblk, perm);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+// loss_out[0] = total loss, [1] = MSE term, [2] = weighted sum-to-one term; dq (B,K,qw) = sum of partials
+DL4SS_API int dl4ss_loss_finalize(const float* part_loss, int B, int K, int nblk, const int* perm, float s1,
+                                  float s2, float* loss_out, const float* part_dq, int qw, float* dq,
+                                  void* stream) {
+  DL4SS_REQUIRE(part_loss && loss_out && B > 0 && K >= 1 && K <= 3);
+  hipStream_t st = as_stream(stream);
+  dim3 grid(cdiv((long long)B * K * (qw > 0 ? qw : 1), 256)), blk(256);
+  if (K == 1) hipLaunchKernelGGL(finalize_kernel<1>, grid, blk, 0, st, part_loss, B, nblk, perm, s1, s2, loss_out, part_dq, qw, dq);
+  if (K == 2) hipLaunchKernelGGL(finalize_kernel<2>, grid, blk, 0, st, part_loss, B, nblk, perm, s1, s2, loss_out, part_dq, qw, dq);
+  if (K == 3) hipLaunchKernelGGL(finalize_kernel<3>, grid, blk, 0, st, part_loss, B, nblk, perm, s1, s2, loss_out, part_dq, qw, dq);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}

@@ -7,9 +7,8 @@
 // float64 numpy; here the mean and peak are reduced in fp64/fp32 and the
 // scaled sources are stored fp32 (the STFT's input precision).
 //
-// Layout: raw (B, K, N) fp32 -> out (B, K+1, N) fp32 with the K scaled sources
-// followed by the mixture, so ONE strided STFT launch covers all signals of a
-// mixture (sources and mix share a row pitch).
+// Layout: raw (B, K, N) fp32 -> scaled sources (B, K, N) and mixture (B, N), each
+// contiguous so that one STFT launch covers all sources and one all mixtures.
 #include "common.h"
 
 namespace {
@@ -49,7 +48,7 @@ __global__ __launch_bounds__(256) void source_stats_kernel(const float* __restri
 // grid (ceil(N/1024), B): normalise, gain, write sources and their sum
 __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw, const float2* __restrict__ stats,
                                                   const float* __restrict__ gains, int K, int N,
-                                                  float* __restrict__ out) {
+                                                  float* __restrict__ out_src, float* __restrict__ out_mix) {
   const int b = blockIdx.y;
   const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= N) return;
@@ -59,7 +58,7 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
     const float2 st = stats[src];
     const float g = gains[src] * st.y;
     const float* x = raw + src * N;
-    float* o = out + ((long long)b * (K + 1) + k) * N;
+    float* o = out_src + ((long long)b * K + k) * N;
     if (i + 3 < N && ((N & 3) == 0)) {
       float4 v = *reinterpret_cast<const float4*>(x + i);
       v.x = (v.x - st.x) * g; v.y = (v.y - st.x) * g; v.z = (v.z - st.x) * g; v.w = (v.w - st.x) * g;
@@ -74,7 +73,7 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
       }
     }
   }
-  float* m = out + ((long long)b * (K + 1) + K) * N;
+  float* m = out_mix + (long long)b * N;
   if (i + 3 < N && ((N & 3) == 0)) {
     *reinterpret_cast<float4*>(m + i) = acc;
   } else {
@@ -86,14 +85,14 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
 }  // namespace
 
 DL4SS_API int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws,
-                                float* out, void* stream) {
-  DL4SS_REQUIRE(raw && gains && out && stats_ws && B >= 0 && K >= 1 && N > 0);
+                                float* out_src, float* out_mix, void* stream) {
+  DL4SS_REQUIRE(raw && gains && out_src && out_mix && stats_ws && B >= 0 && K >= 1 && N > 0);
   if (B == 0) return 0;
   hipLaunchKernelGGL(source_stats_kernel, dim3(B * K), dim3(256), 0, as_stream(stream), raw, N,
                      reinterpret_cast<float2*>(stats_ws));
   DL4SS_CHECK_LAUNCH();
   hipLaunchKernelGGL(mix_kernel, dim3(cdiv(N, 1024), B), dim3(256), 0, as_stream(stream), raw,
-                     reinterpret_cast<const float2*>(stats_ws), gains, K, N, out);
+                     reinterpret_cast<const float2*>(stats_ws), gains, K, N, out_src, out_mix);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

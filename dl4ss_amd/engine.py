@@ -1,0 +1,301 @@
+"""The separation training step on the HIP path (host orchestration).
+
+One step (``TDAA_beta/main_run_sstune_EvalVer.py:586-675``,
+``main_run_sstune_cRM_EvalVer.py:639-752``, ``Torch_multi/main_run.py:453-522``):
+
+    raw sources -> normalise/gain/mix (R1) -> STFT of mixture and sources (R2-R4)
+    -> stacked BiLSTM/BiGRU (R8/R9) -> Linear + tanh -> V (B,T,F,E)
+    -> speaker queries (embedding + ADDJUST, R7/R10)
+    -> fused mask attention + label-ordered / PIT / cRM loss + backward (R11-R14)
+    -> BPTT, weight gradients -> (optional DP all-reduce) -> Adam (R15)
+
+Every arithmetic step is a C-ABI call into ``libdl4ss_hip.so``; torch only owns
+device memory, streams and (for DP) the collective.  All parameters live in one
+flat fp32 buffer (views carry the reference ``state_dict`` key names, so a
+reference / oracle state dict loads directly) and all gradients in a second
+flat buffer: one all-reduce and one Adam launch per step.
+"""
+import math
+
+import torch
+
+from . import _lib, ops
+
+CELLS = {"lstm": 0, "gru": 1}
+
+
+def _ngate(cell):
+    return 4 if cell == "lstm" else 3
+
+
+class SepNet:
+    """Trainable parameters of the mask network, flat fp32 with named views."""
+
+    def __init__(self, cell="lstm", num_layers=4, hidden=300, emb=50, num_labels=101, input_fre=129, crm=False,
+                 adjust=True, device="cuda", seed=1):
+        self.cell, self.L, self.H, self.E = cell, num_layers, hidden, emb
+        self.F, self.num_labels, self.crm, self.adjust = input_fre, num_labels, crm, adjust
+        self.W = 2 * emb if crm else emb
+        NGH = _ngate(cell) * hidden
+        specs = []
+        for l in range(num_layers):
+            D = input_fre if l == 0 else 2 * hidden
+            for kind, shape in (("weight_ih", (NGH, D)), ("weight_hh", (NGH, hidden)), ("bias_ih", (NGH,)),
+                                ("bias_hh", (NGH,))):
+                specs.append((f"mix.layer.{kind}_l{l}", shape))
+                specs.append((f"mix.layer.{kind}_l{l}_reverse", shape))
+        specs += [("mix.Linear.weight", (input_fre * emb, 2 * hidden)), ("mix.Linear.bias", (input_fre * emb,)),
+                  ("emb.layer.weight", (num_labels, self.W))]
+        if adjust:
+            specs.append(("adj.layer.weight", (self.W, 2 * hidden + self.W)))
+        self.specs = specs
+        self.offsets = {}
+        off = 0
+        for name, shape in specs:
+            n = math.prod(shape)
+            self.offsets[name] = (off, shape)
+            off += (n + 3) // 4 * 4  # 16-B aligned views
+        self.numel = off
+        self.device = torch.device(device)
+        self.flat = torch.zeros(off, device=self.device, dtype=torch.float32)
+        self.grad = torch.zeros_like(self.flat)
+        self.reset_parameters(seed)
+
+    def view(self, name, buf=None):
+        off, shape = self.offsets[name]
+        return (self.flat if buf is None else buf)[off:off + math.prod(shape)].view(shape)
+
+    def cat_view(self, kind, l, buf=None):
+        """[fwd; reverse] concatenation (contiguous by construction)."""
+        a = self.view(f"mix.layer.{kind}_l{l}", buf)
+        off = self.offsets[f"mix.layer.{kind}_l{l}"][0]
+        n = a.numel()
+        base = self.flat if buf is None else buf
+        return base[off:off + 2 * n].view(2 * a.shape[0], *a.shape[1:]) if a.dim() == 2 else base[off:off + 2 * n]
+
+    def named_parameters(self):
+        return {name: self.view(name) for name, _ in self.specs}
+
+    def reset_parameters(self, seed=1):
+        """torch default initialisers (nn.LSTM/GRU, nn.Linear, nn.Embedding)."""
+        g = torch.Generator().manual_seed(seed)
+        for name, shape in self.specs:
+            if name.startswith("mix.layer."):
+                k = 1.0 / math.sqrt(self.H)
+                t = torch.empty(shape).uniform_(-k, k, generator=g)
+            elif name == "emb.layer.weight":
+                t = torch.randn(shape, generator=g)
+            elif name.endswith("bias"):
+                k = 1.0 / math.sqrt(2 * self.H)
+                t = torch.empty(shape).uniform_(-k, k, generator=g)
+            else:
+                k = 1.0 / math.sqrt(shape[1])
+                t = torch.empty(shape).uniform_(-k, k, generator=g)
+            self.view(name).copy_(t)
+
+    def load_state_dict(self, sd):
+        for name, _ in self.specs:
+            self.view(name).copy_(sd[name].to(torch.float32))
+
+    def state_dict(self):
+        return {name: self.view(name).detach().clone() for name, _ in self.specs}
+
+
+class SepTrainer:
+    """Buffers and the step schedule for one (B, K, N) workload."""
+
+    def __init__(self, net, batch, k, n_samples, mode="label", precision="fp32", lr=2e-4, sum_weight=0.5,
+                 loss_channels=None, betas=(0.9, 0.999), eps=1e-8, process_group=None):
+        if mode not in ("label", "pit", "crm"):
+            raise ValueError(mode)
+        if (mode == "crm") != net.crm:
+            raise ValueError("cRM mode needs a cRM net (query width 2E) and vice versa")
+        self.net, self.B, self.K, self.N = net, batch, k, n_samples
+        self.mode, self.precision = mode, precision
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.pg = process_group
+        self.T = ops.n_frames(n_samples)
+        self.F = net.F
+        dev = net.device
+        B, K, N, T, F, H = batch, k, n_samples, self.T, net.F, net.H
+        NGH = _ngate(net.cell) * H
+        BT = B * T
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.src = torch.empty(B, K, N, **f32)
+        self.mix = torch.empty(B, N, **f32)
+        self.stats = torch.empty(2 * B * K, **f32)
+        self.mag_mix = torch.empty(B, T, F, **f32)
+        if mode == "crm":
+            self.Xc_mix = torch.empty(B, T, F, 2, **f32)
+            self.Xc_src = torch.empty(B, K, T, F, 2, **f32)
+        else:
+            self.Xc_mix = None
+            self.mag_src = torch.empty(B, K, T, F, **f32)
+        self.out = [torch.empty(B, T, 2 * H, **f32) for _ in range(net.L)]
+        self.hprev = [torch.empty(B, T, 2 * H, **f32) for _ in range(net.L)]
+        self.act = [torch.empty(B, T, 2, 4 * H, **f32) for _ in range(net.L)]
+        self.cs = [torch.empty(B, T, 2, H, **f32) for _ in range(net.L)] if net.cell == "lstm" else None
+        self.G = torch.empty(BT, 2 * NGH, **f32)  # input projection, reused as dG
+        self.dGh = torch.empty(BT, 2 * NGH, **f32) if net.cell == "gru" else None
+        self.dH = [torch.empty(BT, 2 * H, **f32), torch.empty(BT, 2 * H, **f32)]
+        self.V = torch.empty(BT, F * net.E, **f32)  # tanh output; overwritten in place by dPre
+        W = net.W
+        self.q = torch.empty(B, K, W, **f32)
+        self.mean = torch.empty(B, 2 * H, **f32)
+        self.dq = torch.empty(B, K, W, **f32)
+        self.dh_bcast = torch.empty(B, 2 * H, **f32)
+        self.nblk = _lib.query("dl4ss_attn_nblk", T, F)
+        self.part_loss = torch.empty(B, self.nblk, K * K + 1, **f32)
+        self.part_dq = torch.empty(B, self.nblk, K, W, **f32)
+        self.perm = torch.empty(B, K, device=dev, dtype=torch.int32)
+        self.loss = torch.zeros(3, **f32)
+        ws = _lib.query("dl4ss_birnn_workspace_bytes", CELLS[net.cell], B, H)
+        if ws < 0:
+            raise RuntimeError("unsupported BiRNN configuration")
+        self.ws_bytes = ws
+        self.rnn_ws = torch.empty((ws + 7) // 8, device=dev, dtype=torch.int64)
+        self.status = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.m = torch.zeros_like(net.flat)
+        self.v = torch.zeros_like(net.flat)
+        self.step_count = 0
+        nch = loss_channels if loss_channels else K
+        self.s1 = 1.0 / (B * nch * T * F)
+        self.s2 = 0.0 if (mode == "crm" or loss_channels) else sum_weight / (B * T * F)
+        self.spk = torch.empty(B, K, device=dev, dtype=torch.int32)
+
+    # ------------------------------------------------------------------ features
+    def features(self, raw, gains):
+        ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
+        B, K, N = self.B, self.K, self.N
+        if self.mode == "crm":
+            ops.stft(self.mix, complex_out=True, mag_out=True, out_c=self.Xc_mix, out_mag=self.mag_mix)
+            ops.stft(self.src.view(B * K, N), complex_out=True, mag_out=False, out_c=self.Xc_src.view(B * K, self.T,
+                                                                                                     self.F, 2))
+        else:
+            ops.stft(self.mix, complex_out=False, mag_out=True, out_mag=self.mag_mix)
+            ops.stft(self.src.view(B * K, N), complex_out=False, mag_out=True,
+                     out_mag=self.mag_src.view(B * K, self.T, self.F))
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, feats=None):
+        net, B, T, H = self.net, self.B, self.T, self.net.H
+        BT = B * T
+        x = (self.mag_mix if feats is None else feats).reshape(BT, -1)
+        st = _lib.stream_ptr()
+        cell = CELLS[net.cell]
+        for l in range(net.L):
+            ops.gemm(x, net.cat_view("weight_ih", l), transB=True, bias=net.cat_view("bias_ih", l), out=self.G,
+                     precision=self.precision)
+            _lib.call("dl4ss_birnn_fwd", cell, B, T, H, _lib.ptr(self.G), _lib.ptr(net.cat_view("weight_hh", l)),
+                      _lib.ptr(net.cat_view("bias_hh", l)), _lib.ptr(self.out[l]), _lib.ptr(self.hprev[l]),
+                      _lib.ptr(self.act[l]), _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.rnn_ws),
+                      self.ws_bytes, _lib.ptr(self.status), st)
+            x = self.out[l].view(BT, 2 * H)
+        ops.gemm(x, net.view("mix.Linear.weight"), transB=True, bias=net.view("mix.Linear.bias"),
+                 epilogue=ops.EPI_TANH, out=self.V, precision=self.precision)
+        wadj = net.view("adj.layer.weight") if net.adjust else None
+        _lib.call("dl4ss_query_fwd", _lib.ptr(self.out[-1]), B, T, 2 * H, _lib.ptr(self.spk),
+                  _lib.ptr(net.view("emb.layer.weight")), _lib.ptr(wadj), self.K, net.W, _lib.ptr(self.q),
+                  _lib.ptr(self.mean), st)
+
+    def _attn_args(self):
+        B, K, T, F = self.B, self.K, self.T, self.F
+        TF = T * F
+        if self.mode == "crm":
+            return self.Xc_mix, TF, self.Xc_src, K * TF, TF
+        return self.mag_mix, TF, self.mag_src, K * TF, TF
+
+    def attn(self, pass_, perm=None, mask_out=None, pred_out=None):
+        X, xs, Y, ys, yks = self._attn_args()
+        _lib.call("dl4ss_mask_attn_loss", pass_, int(self.mode == "crm"), self.B, self.K, self.T, self.F, self.net.E,
+                  _lib.ptr(self.V), _lib.ptr(self.q), _lib.ptr(X), xs, _lib.ptr(Y), ys, yks, _lib.ptr(perm),
+                  self.s1, self.s2, _lib.ptr(self.V) if pass_ == 1 else None, _lib.ptr(self.part_loss),
+                  _lib.ptr(self.part_dq) if pass_ == 1 else None, _lib.ptr(mask_out), _lib.ptr(pred_out),
+                  _lib.stream_ptr())
+
+    def loss_and_grad(self):
+        """Fused attention + loss + dPre (in place over V) + dq; returns loss (device)."""
+        st = _lib.stream_ptr()
+        perm = None
+        if self.mode == "pit":
+            self.attn(0)
+            _lib.call("dl4ss_pit_select", _lib.ptr(self.part_loss), self.B, self.K, self.nblk, _lib.ptr(self.perm), st)
+            perm = self.perm
+        self.attn(1, perm)
+        _lib.call("dl4ss_loss_finalize", _lib.ptr(self.part_loss), self.B, self.K, self.nblk, _lib.ptr(perm),
+                  self.s1, self.s2, _lib.ptr(self.loss), _lib.ptr(self.part_dq), self.net.W, _lib.ptr(self.dq), st)
+        return self.loss
+
+    # ------------------------------------------------------------------ backward
+    def backward(self):
+        net, B, T, H = self.net, self.B, self.T, self.net.H
+        BT = B * T
+        NGH = _ngate(net.cell) * H
+        g = net.grad
+        st = _lib.stream_ptr()
+        cell = CELLS[net.cell]
+        g.zero_()
+        wadj = net.view("adj.layer.weight") if net.adjust else None
+        _lib.call("dl4ss_query_bwd", _lib.ptr(self.dq), B, T, 2 * H, _lib.ptr(self.spk),
+                  _lib.ptr(net.view("emb.layer.weight")), _lib.ptr(wadj), _lib.ptr(self.mean), self.K, net.W,
+                  _lib.ptr(net.view("emb.layer.weight", g)),
+                  _lib.ptr(net.view("adj.layer.weight", g)) if net.adjust else None,
+                  _lib.ptr(self.dh_bcast) if net.adjust else None, st)
+        dPre = self.V
+        hL = self.out[-1].view(BT, 2 * H)
+        ops.gemm(dPre, hL, transA=True, out=net.view("mix.Linear.weight", g), precision=self.precision)
+        ops.colsum(dPre, net.view("mix.Linear.bias", g))
+        dH = self.dH[0]
+        ops.gemm(dPre, net.view("mix.Linear.weight"), out=dH, precision=self.precision)
+        for l in range(net.L - 1, -1, -1):
+            dG = self.G
+            dGh = self.dGh if self.dGh is not None else dG
+            _lib.call("dl4ss_birnn_bwd", cell, B, T, H, _lib.ptr(dH),
+                      _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
+                      _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
+                      _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), _lib.ptr(dG),
+                      _lib.ptr(self.dGh) if self.dGh is not None else None, _lib.ptr(self.rnn_ws), self.ws_bytes,
+                      _lib.ptr(self.status), st)
+            xl = self.mag_mix.view(BT, -1) if l == 0 else self.out[l - 1].view(BT, 2 * H)
+            ops.gemm(dG, xl, transA=True, out=net.cat_view("weight_ih", l, g), splitk=4, beta=1.0,
+                     precision=self.precision)
+            ops.colsum(dG, net.cat_view("bias_ih", l, g))
+            whh_g = net.cat_view("weight_hh", l, g)
+            hp = self.hprev[l].view(BT, 2 * H)
+            for d in range(2):
+                ops.gemm(dGh[:, d * NGH:(d + 1) * NGH], hp[:, d * H:(d + 1) * H], transA=True,
+                         out=whh_g[d * NGH:(d + 1) * NGH], splitk=4, beta=1.0, precision=self.precision)
+            ops.colsum(dGh, net.cat_view("bias_hh", l, g))
+            if l > 0:
+                dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
+                ops.gemm(dG, net.cat_view("weight_ih", l), out=dH_next, precision=self.precision)
+                dH = dH_next
+
+    def allreduce(self):
+        if self.pg is None:
+            return
+        import torch.distributed as dist
+
+        dist.all_reduce(self.net.grad, op=dist.ReduceOp.SUM, group=self.pg)
+        self.net.grad.mul_(1.0 / dist.get_world_size(self.pg))
+
+    def optimizer_step(self):
+        self.step_count += 1
+        ops.adam_(self.net.flat, self.net.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
+
+    def step(self, raw, gains, spk_idx):
+        """One full training step on device-resident inputs; returns the loss tensor (not synced)."""
+        self.spk.copy_(spk_idx)
+        self.features(raw, gains)
+        self.forward()
+        loss = self.loss_and_grad()
+        self.backward()
+        self.allreduce()
+        self.optimizer_step()
+        return loss
+
+    def check(self):
+        torch.cuda.synchronize()
+        s = int(self.status.item())
+        if s:
+            raise RuntimeError(f"BiRNN hand-off timed out (status {s})")

@@ -61,18 +61,74 @@ def istft(S, conj=False, out=None):
     return out
 
 
-def mix_sources(raw, gains, out=None, stats_ws=None):
-    """raw (B, K, N) fp32 sources, gains (B, K) fp32 ->
-    (B, K+1, N): normalised+scaled sources then their mixture."""
+def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None):
+    """raw (B, K, N) fp32 sources, gains (B, K) fp32 -> (scaled sources (B, K, N),
+    mixture (B, N)) -- normalise, gain, sum."""
     _f32c(raw, "mix_sources")
     _f32c(gains, "mix_sources(gains)")
     B, K, N = raw.shape
-    if gains.shape != (B, K):
+    if tuple(gains.shape) != (B, K):
         raise RuntimeError("mix_sources: gains must be (B, K)")
-    if out is None:
-        out = torch.empty(B, K + 1, N, device=raw.device, dtype=torch.float32)
+    if out_src is None:
+        out_src = torch.empty(B, K, N, device=raw.device, dtype=torch.float32)
+    if out_mix is None:
+        out_mix = torch.empty(B, N, device=raw.device, dtype=torch.float32)
     if stats_ws is None:
         stats_ws = torch.empty(B * K * 2, device=raw.device, dtype=torch.float32)
-    _lib.call("dl4ss_mix_sources", _lib.ptr(raw), _lib.ptr(gains), B, K, N, _lib.ptr(stats_ws), _lib.ptr(out),
+    _lib.call("dl4ss_mix_sources", _lib.ptr(raw), _lib.ptr(gains), B, K, N, _lib.ptr(stats_ws), _lib.ptr(out_src),
+              _lib.ptr(out_mix), _lib.stream_ptr())
+    return out_src, out_mix
+
+
+# ---------------------------------------------------------------------------
+# dense contractions
+# ---------------------------------------------------------------------------
+PREC = {"fp32": 0, "bf16": 1}
+EPI_NONE, EPI_TANH = 0, 1
+
+
+def _mat(t, name):
+    if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1):
+        raise RuntimeError(f"{name}: expected a 2-D row-major float32 CUDA matrix (unit inner stride)")
+    return t
+
+
+def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.0, out=None, precision="fp32",
+         splitk=1):
+    """out = op(A) @ op(B) (+ bias) (tanh) (+ beta*out).  op(A) = A.T if transA.
+
+    A is stored (M, K) or (K, M) if transA; B is stored (K, N) or (N, K) if transB.
+    """
+    _mat(A, "gemm(A)")
+    _mat(B, "gemm(B)")
+    M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
+    Kb, N = (B.shape[1], B.shape[0]) if transB else (B.shape[0], B.shape[1])
+    if K != Kb:
+        raise RuntimeError(f"gemm: inner dims differ ({K} vs {Kb})")
+    if out is None:
+        if beta != 0.0 or splitk > 1:
+            raise RuntimeError("gemm: accumulation needs an output tensor")
+        out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    _mat(out, "gemm(out)")
+    if tuple(out.shape) != (M, N):
+        raise RuntimeError(f"gemm: out shape {tuple(out.shape)} != {(M, N)}")
+    if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
+        raise RuntimeError("gemm: bias must be contiguous with N elements")
+    _lib.call("dl4ss_gemm", int(transA), int(transB), M, N, K, _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0),
+              _lib.ptr(out), out.stride(0), _lib.ptr(bias), epilogue, float(beta), PREC[precision], int(splitk),
               _lib.stream_ptr())
     return out
+
+
+def colsum(A, out):
+    """out += A.sum(0) for a row-major matrix view A (M, N)."""
+    _mat(A, "colsum")
+    _lib.call("dl4ss_colsum", _lib.ptr(A), A.stride(0), A.shape[0], A.shape[1], _lib.ptr(out), _lib.stream_ptr())
+    return out
+
+
+def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8):
+    for t in (p, g, m, v):
+        _f32c(t, "adam")
+    _lib.call("dl4ss_adam", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(), float(lr), float(betas[0]),
+              float(betas[1]), float(eps), int(step), _lib.stream_ptr())

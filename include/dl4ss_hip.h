@@ -46,12 +46,80 @@ int dl4ss_istft(const float* S_c64, long long n_sig, int T, int n_fft, int hop, 
                 void* stream);
 
 /* ---- R1 preprocessing / mixing ----------------------------------------- */
-/* raw (B, K, N) -> out (B, K+1, N): each source x -> (x - mean) / max|x - mean| * gain,
- * then their sum as channel K.  stats_ws: 2*B*K floats of workspace.
+/* raw (B, K, N) -> out_src (B, K, N): each source x -> (x - mean) / max|x - mean| * gain;
+ * out_mix (B, N): their sum.  stats_ws: 2*B*K floats of workspace.
  * Replaces Torch_multi/predata_multiAims_dB.py:156-197 (and the _3dB /
  * fromList_cRM_123 gain variants: gains are computed by the caller). */
-int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws, float* out,
-                      void* stream);
+int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws, float* out_src,
+                      float* out_mix, void* stream);
+
+/* ---- dense contractions (MFMA) ------------------------------------------ */
+enum { DL4SS_EPI_NONE = 0, DL4SS_EPI_TANH = 1 };
+enum { DL4SS_PREC_F32 = 0, DL4SS_PREC_BF16 = 1 };
+/* C = op(A) op(B) (+ bias[N]) (tanh) (+ beta C); row-major, leading dims in elements.
+ * transA: A stored K x M (else M x K); transB: B stored N x K (else K x N).
+ * splitk > 1: C += op(A) op(B) with fp32 atomics (epilogue none, beta 1).
+ * Replaces the cuDNN input projection inside nn.LSTM/nn.GRU (EvalVer.py:282-293),
+ * nn.Linear(600, 6450) + tanh (EvalVer.py:290,298-299) and their autograd GEMMs. */
+int dl4ss_gemm(int transA, int transB, int M, int N, int K, const float* A, long long lda, const float* B,
+               long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta, int precision,
+               int splitk, void* stream);
+
+/* ---- persistent bidirectional LSTM / GRU recurrence ---------------------- */
+enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
+/* Granule workspace (bytes) needed by dl4ss_birnn_fwd / _bwd for (cell, B, H); -1 if unsupported. */
+long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
+/* One layer, both directions: G (B,T,2,NG*H) = X W_ih^T + b_ih (NG = 4 LSTM / 3 GRU),
+ * W_hh (2, NG*H, H), b_hh (2, NG*H) -> out (B,T,2H) [fwd | reverse], hprev (B,T,2H)
+ * (h_{t-1} per step), act (B,T,2,4H) gate activations, cs (B,T,2,H) LSTM cells.
+ * *status != 0 after the call means a hand-off timed out (results invalid).
+ * Replaces the cuDNN recurrence of nn.LSTM / nn.GRU(batch_first, bidirectional)
+ * at TDAA_beta/main_run_sstune_EvalVer.py:282-293, Torch_multi/main_run.py:263-273. */
+int dl4ss_birnn_fwd(int cell, int B, int T, int H, const float* G, const float* W_hh, const float* b_hh, float* out,
+                    float* hprev, float* act, float* cs, void* workspace, long long ws_bytes, int* status,
+                    void* stream);
+/* BPTT of one layer: dOut (B,T,2H) (+ dOut_bcast (B,2H) at every t, may be NULL) ->
+ * dG (B,T,2,NG*H) grad of the input projection (pre-activation) and, for GRU, dGh
+ * grad of W_hh h + b_hh (for LSTM they coincide; dGh may be NULL). */
+int dl4ss_birnn_bwd(int cell, int B, int T, int H, const float* dOut, const float* dOut_bcast, const float* W_hh,
+                    const float* act, const float* cs, const float* hprev, float* dG, float* dGh, void* workspace,
+                    long long ws_bytes, int* status, void* stream);
+
+/* ---- speaker-query mask attention + loss (fused forward/backward) -------- */
+/* Blocks per utterance used by the partial-sum buffers. */
+int dl4ss_attn_nblk(int T, int F);
+/* pass 0 (COST): costs (+ optional mask / pred outputs); pass 1 (GRAD): also
+ * dPre (B,T*F,E) = dL/d(h W_lin^T + b) (may alias V: in-place) and dq partials.
+ * V (B,T*F,E) = tanh Linear output; q (B,K,QW), QW = E (magnitude) or 2E (cRM).
+ * X: magnitude (b*x_bstride + row) or complex [re,im] pairs; Y target k of b at
+ * b*y_bstride + k*y_kstride (+ row).  perm (B,K) target per channel (NULL = label
+ * order).  s1/s2 scale the MSE and sum-to-one terms.  part_loss (B,nblk,K*K+1),
+ * part_dq (B,nblk,K,QW).
+ * Replaces EvalVer.py:615-666 (expand + baddbmm + sigmoid + MSE + sum loss) and
+ * main_run_sstune_cRM_EvalVer.py:259-271,688,720-743 (cRM branch). */
+int dl4ss_mask_attn_loss(int pass, int crm, int B, int K, int T, int F, int E, const float* V, const float* q,
+                         const float* X, long long x_bstride, const float* Y, long long y_bstride,
+                         long long y_kstride, const int* perm, float s1, float s2, float* dPre, float* part_loss,
+                         float* part_dq, float* mask_out, float* pred_out, void* stream);
+/* PIT: per utterance the lowest-index permutation minimising the summed costs. */
+int dl4ss_pit_select(const float* part_loss, int B, int K, int nblk, int* perm, void* stream);
+/* loss_out[3] = {total, MSE term, weighted sum-to-one term}; dq = sum of partials. */
+int dl4ss_loss_finalize(const float* part_loss, int B, int K, int nblk, const int* perm, float s1, float s2,
+                        float* loss_out, const float* part_dq, int qw, float* dq, void* stream);
+
+/* ---- speaker queries, reductions, optimizer ------------------------------ */
+/* q[b,k] = Emb[idx[b,k]] (+ W_adj [mean_t h[b]; Emb[idx[b,k]]]); h (B,T,D).
+ * SPEECH_EMBEDDING + ADDJUST: EvalVer.py:348-377,606-608. w_adj may be NULL. */
+int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* idx, const float* emb, const float* w_adj, int K,
+                    int W, float* q, float* mean_out, void* stream);
+/* d_emb (+=, scatter), d_wadj (+=), dh_bcast (B,D) = W_m^T sum_k dq / T. */
+int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* idx, const float* emb, const float* w_adj,
+                    const float* mean, int K, int W, float* d_emb, float* d_wadj, float* dh_bcast, void* stream);
+/* out[n] += sum_m A[m*lda + n] (bias gradients). */
+int dl4ss_colsum(const float* A, long long lda, int M, int N, float* out, void* stream);
+/* torch.optim.Adam step on flat fp32 buffers (EvalVer.py:538-544). */
+int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+               float eps, int step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,138 @@
+"""GPU parity of the dense / recurrent kernels against torch-CPU (fp64) references."""
+import numpy as np
+import pytest
+import torch
+
+from dl4ss_amd import _lib, ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(257, 130, 129), (64, 600, 301), (1000, 77, 16), (5, 3, 2)])
+def test_gemm_f32_matches_fp64(dev, ta, tb, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) if tb else torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = (A.double().T if ta else A.double()) @ (B.double().T if tb else B.double()) + bias.double()
+    out = ops.gemm(A.to(dev), B.to(dev), transA=ta, transB=tb, bias=bias.to(dev)).cpu().double()
+    err = (out - ref).abs().max() / ref.abs().max()
+    assert err < 1e-5, err
+
+
+def test_gemm_tanh_beta_splitk(dev):
+    g = torch.Generator().manual_seed(0)
+    A, B = torch.randn(300, 650, generator=g), torch.randn(650, 200, generator=g)
+    C0 = torch.randn(300, 200, generator=g)
+    ref = torch.tanh(A.double() @ B.double() * 0.05)
+    out = ops.gemm((A * 0.05).to(dev), B.to(dev), epilogue=ops.EPI_TANH).cpu().double()
+    assert (out - ref).abs().max() < 1e-5
+    acc = C0.clone().to(dev)
+    ops.gemm(A.to(dev), B.to(dev), out=acc, beta=1.0, splitk=4)
+    ref2 = C0.double() + A.double() @ B.double()
+    assert ((acc.cpu().double() - ref2).abs().max() / ref2.abs().max()) < 1e-5
+    # strided (column-slice) operands
+    big = torch.randn(400, 90, generator=g)
+    outs = ops.gemm(big[:, 30:60].to(dev) if False else big.to(dev)[:, 30:60], B[:30].to(dev))
+    assert ((outs.cpu().double() - big[:, 30:60].double() @ B[:30].double()).abs().max()) < 1e-3
+
+
+def test_gemm_bf16_tolerance(dev):
+    g = torch.Generator().manual_seed(1)
+    A, B = torch.randn(513, 600, generator=g), torch.randn(2400, 600, generator=g)
+    ref = A.double() @ B.double().T
+    out = ops.gemm(A.to(dev), B.to(dev), transB=True, precision="bf16").cpu().double()
+    rel = ((out - ref).norm() / ref.norm()).item()
+    assert rel < 8e-3, rel
+
+
+def _birnn_ref(cell, B, T, D, H, seed):
+    torch.manual_seed(seed)
+    rnn = (torch.nn.LSTM if cell == "lstm" else torch.nn.GRU)(D, H, 1, batch_first=True, bidirectional=True).double()
+    x = torch.randn(B, T, D, dtype=torch.float64)
+    return rnn, x
+
+
+def _run_birnn_fwd(dev, cell, rnn, x, H):
+    B, T, D = x.shape
+    NGH = (4 if cell == "lstm" else 3) * H
+    wih = torch.cat([rnn.weight_ih_l0, rnn.weight_ih_l0_reverse]).float().to(dev)
+    bih = torch.cat([rnn.bias_ih_l0, rnn.bias_ih_l0_reverse]).float().to(dev)
+    whh = torch.cat([rnn.weight_hh_l0, rnn.weight_hh_l0_reverse]).float().contiguous().to(dev)
+    bhh = torch.cat([rnn.bias_hh_l0, rnn.bias_hh_l0_reverse]).float().to(dev)
+    xd = x.float().to(dev).reshape(B * T, D)
+    G = ops.gemm(xd, wih.detach(), transB=True, bias=bih.detach())
+    out = torch.empty(B, T, 2 * H, device=dev)
+    hprev = torch.empty_like(out)
+    act = torch.empty(B, T, 2, 4 * H, device=dev)
+    cs = torch.empty(B, T, 2, H, device=dev)
+    cellid = 0 if cell == "lstm" else 1
+    ws = _lib.query("dl4ss_birnn_workspace_bytes", cellid, B, H)
+    wsb = torch.empty((ws + 7) // 8, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("dl4ss_birnn_fwd", cellid, B, T, H, _lib.ptr(G), _lib.ptr(whh.detach()), _lib.ptr(bhh.detach()),
+              _lib.ptr(out), _lib.ptr(hprev), _lib.ptr(act), _lib.ptr(cs), _lib.ptr(wsb), ws, _lib.ptr(status),
+              _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    return dict(G=G, out=out, hprev=hprev, act=act, cs=cs, whh=whh, ws=wsb, wsn=ws, status=status, xd=xd, NGH=NGH)
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+@pytest.mark.parametrize("B,T,H", [(3, 17, 300), (32, 9, 300), (1, 40, 300), (5, 11, 40)])
+def test_birnn_fwd_matches_torch(dev, cell, B, T, H):
+    rnn, x = _birnn_ref(cell, B, T, 23, H, B * 100 + T)
+    ref, _ = rnn(x)
+    r = _run_birnn_fwd(dev, cell, rnn, x, H)
+    err = (r["out"].cpu().double() - ref).abs().max().item()
+    assert err < 2e-5, err
+    # hprev is the shifted output (zero at each direction's start)
+    hp = r["hprev"].cpu().double()
+    assert torch.allclose(hp[:, 1:, :H], r["out"].cpu().double()[:, :-1, :H])
+    assert torch.allclose(hp[:, :-1, H:], r["out"].cpu().double()[:, 1:, H:])
+    assert hp[:, 0, :H].abs().max() == 0 and hp[:, -1, H:].abs().max() == 0
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+@pytest.mark.parametrize("B,T,H", [(3, 17, 300), (32, 6, 300), (2, 9, 40)])
+def test_birnn_bwd_matches_autograd(dev, cell, B, T, H):
+    rnn, x = _birnn_ref(cell, B, T, 23, H, 7 + B + T)
+    x.requires_grad_(True)
+    ref, _ = rnn(x)
+    gout = torch.randn_like(ref)
+    bc = torch.randn(B, 2 * H, dtype=torch.float64)
+    (ref * gout).sum().backward(retain_graph=True)
+    # extra broadcast term: d/dh of sum_t bc . h_t
+    (ref * bc[:, None, :]).sum().backward()
+    r = _run_birnn_fwd(dev, cell, rnn, x.detach(), H)
+    NGH = r["NGH"]
+    dG = torch.empty(B * T, 2 * NGH, device=dev)
+    dGh = torch.empty_like(dG) if cell == "gru" else None
+    cellid = 0 if cell == "lstm" else 1
+    _lib.call("dl4ss_birnn_bwd", cellid, B, T, H, _lib.ptr(gout.float().to(dev)), _lib.ptr(bc.float().to(dev)),
+              _lib.ptr(r["whh"]), _lib.ptr(r["act"]), _lib.ptr(r["cs"]), _lib.ptr(r["hprev"]), _lib.ptr(dG),
+              _lib.ptr(dGh), _lib.ptr(r["ws"]), r["wsn"], _lib.ptr(r["status"]), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert int(r["status"].item()) == 0
+    dGh = dG if dGh is None else dGh
+    # weight gradients from dG / dGh via our GEMMs
+    wih = torch.cat([rnn.weight_ih_l0, rnn.weight_ih_l0_reverse])
+    dwih = ops.gemm(dG, r["xd"], transA=True).cpu().double()
+    ref_dwih = torch.cat([rnn.weight_ih_l0.grad, rnn.weight_ih_l0_reverse.grad])
+    assert (dwih - ref_dwih).abs().max() / ref_dwih.abs().max() < 1e-4
+    hp = r["hprev"].view(B * T, 2 * H)
+    for d, name in enumerate(["weight_hh_l0", "weight_hh_l0_reverse"]):
+        dwhh = ops.gemm(dGh[:, d * NGH:(d + 1) * NGH], hp[:, d * H:(d + 1) * H], transA=True).cpu().double()
+        refw = getattr(rnn, name).grad
+        assert (dwhh - refw).abs().max() / refw.abs().max() < 1e-4, name
+    dbih = torch.zeros(2 * NGH, device=dev)
+    ops.colsum(dG, dbih)
+    ref_db = torch.cat([rnn.bias_ih_l0.grad, rnn.bias_ih_l0_reverse.grad])
+    assert (dbih.cpu().double() - ref_db).abs().max() / ref_db.abs().max() < 1e-4
+    dbhh = torch.zeros(2 * NGH, device=dev)
+    ops.colsum(dGh, dbhh)
+    ref_dbh = torch.cat([rnn.bias_hh_l0.grad, rnn.bias_hh_l0_reverse.grad])
+    assert (dbhh.cpu().double() - ref_dbh).abs().max() / ref_dbh.abs().max() < 1e-4
+    dx = ops.gemm(dG, wih.float().to(dev)).cpu().double().view(B, T, -1)
+    assert (dx - x.grad).abs().max() / x.grad.abs().max() < 1e-4

@@ -1,0 +1,142 @@
+"""End-to-end parity of one training step (HIP path) against the CPU oracle on
+identical synthetic mixtures: loss, masked magnitude spectrogram, every
+gradient and the Adam-updated parameters."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dsp, model as om
+from dl4ss_amd import engine, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_features(src, gains, crm):
+    B, K, N = src.shape
+    feats, X, Y = [], [], []
+    for b in range(B):
+        srcs = [dsp.normalise_source(src[b, k].astype(np.float32), N) for k in range(K)]
+        s, m = dsp.mix_sources(srcs, gains[b])
+        Sm = dsp.stft_tf(m)
+        feats.append(np.abs(Sm))
+        if crm:
+            X.append(dsp.convert2(Sm))
+            Y.append(np.stack([dsp.convert2(dsp.stft_tf(s[k])) for k in range(K)]))
+        else:
+            X.append(np.abs(Sm))
+            Y.append(np.stack([np.abs(dsp.stft_tf(s[k])) for k in range(K)]))
+    t = lambda a: torch.from_numpy(np.array(a, dtype=np.float32))  # noqa: E731
+    return t(feats), t(X), t(Y)
+
+
+def _setup(dev, cell, L, B, K, N, mode, seed=3, adjust=True, loss_channels=None):
+    crm = mode == "crm"
+    net = engine.SepNet(cell=cell, num_layers=L, crm=crm, adjust=adjust, device=dev, seed=seed)
+    tr = engine.SepTrainer(net, B, K, N, mode=mode, loss_channels=loss_channels)
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=seed)
+    src, spk, u = gen.batch(B)
+    gains = synth.gains_for(u, K)
+    ref = om.SepModel(cell=cell, num_layers=L, crm=crm, adjust=adjust)
+    ref.load_state_dict({k: v.cpu() for k, v in net.state_dict().items()})
+    return net, tr, src, spk, gains, ref
+
+
+def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, loss_channels=None, adjust=True):
+    net, tr, src, spk, gains, ref = _setup(dev, cell, L, B, K, N, mode, adjust=adjust, loss_channels=loss_channels)
+    feats, X, Y = _oracle_features(src, gains, mode == "crm")
+    idx = torch.from_numpy(spk)
+    # --- oracle step
+    opt = om.make_adam(ref)
+    opt.zero_grad()
+    mask, V, h, q = ref(feats, idx)
+    if mode == "crm":
+        loss_ref, pred_ref = om.loss_crm(mask, X, Y)
+    elif mode == "pit":
+        loss_ref, pred_ref = om.loss_pit(mask, X, Y)
+    elif loss_channels:
+        pred_ref = mask * X[:, None]
+        loss_ref = torch.sum((pred_ref - Y) ** 2) / (B * loss_channels * X.shape[1] * X.shape[2])
+    else:
+        loss_ref, pred_ref = om.loss_label_ordered(mask, X, Y)
+    loss_ref.backward()
+    grads_ref = {n: p.grad.detach().clone() for n, p in ref.named_parameters()}
+    opt.step()
+    # --- HIP step
+    raw = torch.from_numpy(src.astype(np.float32)).to(dev)
+    g = torch.from_numpy(gains.astype(np.float32)).to(dev)
+    sp = torch.from_numpy(spk.astype(np.int32)).to(dev)
+    tr.spk.copy_(sp)
+    tr.features(raw, g)
+    tr.forward()
+    # masked magnitude spectrogram / cRM prediction from the COST pass
+    T, F = tr.T, tr.F
+    shape = (B, K, T * F, 2) if mode == "crm" else (B, K, T * F)
+    pred = torch.empty(shape, device=dev)
+    tr.attn(0, pred_out=pred)
+    loss = tr.loss_and_grad()
+    tr.backward()
+    tr.optimizer_step()
+    tr.check()
+    # loss
+    l = float(loss[0].cpu())
+    assert abs(l - float(loss_ref)) / abs(float(loss_ref)) < tol_loss, (l, float(loss_ref))
+    # masked magnitude (the north-star parity metric): relative L2 <= 1e-3
+    if mode == "label":
+        pr = pred.cpu().view(B, K, T, F)
+        rel = ((pr - pred_ref).norm() / pred_ref.norm()).item()
+        assert rel < 1e-3, rel
+    # gradients
+    for name, gr in grads_ref.items():
+        ours = net.view(name, net.grad).cpu()
+        denom = gr.abs().max().item()
+        if denom == 0:
+            assert ours.abs().max().item() < 1e-9, name
+            continue
+        err = (ours - gr).abs().max().item() / denom
+        assert err < tol_grad, (name, err)
+    # Adam-updated parameters
+    for name, p in ref.named_parameters():
+        ours = net.view(name).cpu()
+        assert (ours - p.detach()).abs().max().item() < 5e-6 + 1e-3 * 2e-4, name
+
+
+def test_step_bilstm_label_order(dev):
+    _compare_step(dev, "lstm", 4, 2, 2, 4000, "label")
+
+
+def test_step_bilstm_full_length_b1(dev):
+    _compare_step(dev, "lstm", 2, 1, 2, 32000, "label")
+
+
+def test_step_bigru_pit(dev):
+    _compare_step(dev, "gru", 2, 3, 2, 3000, "pit")
+
+
+def test_step_bigru_3spk(dev):
+    _compare_step(dev, "gru", 2, 2, 3, 3000, "label")
+
+
+def test_step_crm(dev):
+    _compare_step(dev, "gru", 2, 2, 2, 3000, "crm", tol_grad=5e-3)
+
+
+def test_step_c1_101_channels(dev):
+    # Torch_multi/main_run.py: BiGRU-2L, loss over 101 label channels, no sum term, no ADDJUST
+    _compare_step(dev, "gru", 2, 1, 2, 4000, "label", loss_channels=101, adjust=False)
+
+
+def test_pit_finds_swapped_targets(dev):
+    net, tr, src, spk, gains, ref = _setup(dev, "gru", 1, 4, 2, 2000, "pit")
+    raw = torch.from_numpy(src.astype(np.float32)).to(dev)
+    tr.spk.copy_(torch.from_numpy(spk.astype(np.int32)).to(dev))
+    tr.features(raw, torch.from_numpy(gains.astype(np.float32)).to(dev))
+    tr.forward()
+    tr.attn(0)
+    from dl4ss_amd import _lib
+    _lib.call("dl4ss_pit_select", _lib.ptr(tr.part_loss), tr.B, tr.K, tr.nblk, _lib.ptr(tr.perm), _lib.stream_ptr())
+    p1 = tr.perm.cpu().clone()
+    tr.mag_src.copy_(tr.mag_src.flip(1))
+    tr.attn(0)
+    _lib.call("dl4ss_pit_select", _lib.ptr(tr.part_loss), tr.B, tr.K, tr.nblk, _lib.ptr(tr.perm), _lib.stream_ptr())
+    p2 = tr.perm.cpu()
+    assert torch.equal(p2, p1.flip(1) * 0 + (1 - p1))  # bit-exact permutation indices
