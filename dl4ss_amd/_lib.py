@@ -76,11 +76,16 @@ def stream_ptr(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def ptr(t):
+def ptr(t, strided=False):
+    """Raw device pointer of a CUDA tensor.  Unless the call site passes the
+    strides itself (``strided=True``), the tensor must be contiguous: a kernel
+    sees only the pointer, so a transposed view would be silently misread."""
     if t is None:
         return None
     if not t.is_cuda:
         raise RuntimeError("dl4ss HIP op received a CPU tensor (no CPU fallback)")
+    if not strided and not t.is_contiguous():
+        raise RuntimeError("dl4ss HIP op received a non-contiguous tensor")
     return ctypes.c_void_p(t.data_ptr())
 
 

@@ -114,8 +114,8 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
         raise RuntimeError(f"gemm: out shape {tuple(out.shape)} != {(M, N)}")
     if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
         raise RuntimeError("gemm: bias must be contiguous with N elements")
-    _lib.call("dl4ss_gemm", int(transA), int(transB), M, N, K, _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0),
-              _lib.ptr(out), out.stride(0), _lib.ptr(bias), epilogue, float(beta), PREC[precision], int(splitk),
+    _lib.call("dl4ss_gemm", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0), _lib.ptr(B, True), B.stride(0),
+              _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue, float(beta), PREC[precision], int(splitk),
               _lib.stream_ptr())
     return out
 
@@ -123,7 +123,7 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
 def colsum(A, out):
     """out += A.sum(0) for a row-major matrix view A (M, N)."""
     _mat(A, "colsum")
-    _lib.call("dl4ss_colsum", _lib.ptr(A), A.stride(0), A.shape[0], A.shape[1], _lib.ptr(out), _lib.stream_ptr())
+    _lib.call("dl4ss_colsum", _lib.ptr(A, True), A.stride(0), A.shape[0], A.shape[1], _lib.ptr(out), _lib.stream_ptr())
     return out
 
 

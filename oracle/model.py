@@ -170,7 +170,7 @@ class SepModel(nn.Module):
         w = 2 * emb if crm else emb
         self.mix = MixSpeech(cell, input_fre, hidden, num_layers, emb)
         self.emb = Embedding(num_labels, w)
-        self.adj = Adjust(2 * hidden, w)
+        self.adj = Adjust(2 * hidden, w) if adjust else None
 
     def queries(self, h, spk_idx):
         q = self.emb(spk_idx)

@@ -94,14 +94,15 @@ def test_birnn_fwd_matches_torch(dev, cell, B, T, H):
     assert hp[:, 0, :H].abs().max() == 0 and hp[:, -1, H:].abs().max() == 0
 
 
+@pytest.mark.parametrize("use_bc", [False, True])
 @pytest.mark.parametrize("cell", ["lstm", "gru"])
 @pytest.mark.parametrize("B,T,H", [(3, 17, 300), (32, 6, 300), (2, 9, 40)])
-def test_birnn_bwd_matches_autograd(dev, cell, B, T, H):
+def test_birnn_bwd_matches_autograd(dev, cell, B, T, H, use_bc):
     rnn, x = _birnn_ref(cell, B, T, 23, H, 7 + B + T)
     x.requires_grad_(True)
     ref, _ = rnn(x)
-    gout = torch.randn_like(ref)
-    bc = torch.randn(B, 2 * H, dtype=torch.float64)
+    gout = torch.randn(ref.shape, dtype=torch.float64)  # contiguous (batch_first LSTM output is a view)
+    bc = torch.randn(B, 2 * H, dtype=torch.float64) * float(use_bc)
     (ref * gout).sum().backward(retain_graph=True)
     # extra broadcast term: d/dh of sum_t bc . h_t
     (ref * bc[:, None, :]).sum().backward()
@@ -110,7 +111,8 @@ def test_birnn_bwd_matches_autograd(dev, cell, B, T, H):
     dG = torch.empty(B * T, 2 * NGH, device=dev)
     dGh = torch.empty_like(dG) if cell == "gru" else None
     cellid = 0 if cell == "lstm" else 1
-    _lib.call("dl4ss_birnn_bwd", cellid, B, T, H, _lib.ptr(gout.float().to(dev)), _lib.ptr(bc.float().to(dev)),
+    gout_d, bc_d = gout.float().to(dev), bc.float().to(dev)  # keep alive across the async launch
+    _lib.call("dl4ss_birnn_bwd", cellid, B, T, H, _lib.ptr(gout_d), _lib.ptr(bc_d),
               _lib.ptr(r["whh"]), _lib.ptr(r["act"]), _lib.ptr(r["cs"]), _lib.ptr(r["hprev"]), _lib.ptr(dG),
               _lib.ptr(dGh), _lib.ptr(r["ws"]), r["wsn"], _lib.ptr(r["status"]), _lib.stream_ptr())
     torch.cuda.synchronize()
@@ -136,3 +138,74 @@ def test_birnn_bwd_matches_autograd(dev, cell, B, T, H):
     assert (dbhh.cpu().double() - ref_dbh).abs().max() / ref_dbh.abs().max() < 1e-4
     dx = ops.gemm(dG, wih.float().to(dev)).cpu().double().view(B, T, -1)
     assert (dx - x.grad).abs().max() / x.grad.abs().max() < 1e-4
+
+
+def _manual_birnn(cell, G, whh, bhh, H):
+    """Explicit bidirectional recurrence on precomputed input projections G (B,T,2,NGH) (fp64, autograd)."""
+    B, T = G.shape[:2]
+    outs = [[None] * T, [None] * T]
+    for d in range(2):
+        h = torch.zeros(B, H, dtype=G.dtype)
+        c = torch.zeros(B, H, dtype=G.dtype)
+        order = range(T) if d == 0 else range(T - 1, -1, -1)
+        for t in order:
+            gh = h @ whh[d].T + bhh[d]
+            gx = G[:, t, d]
+            if cell == "lstm":
+                i, f, g, o = (gx + gh).chunk(4, 1)
+                c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+                h = torch.sigmoid(o) * torch.tanh(c)
+            else:
+                xr, xz, xn = gx.chunk(3, 1)
+                hr, hz, hn = gh.chunk(3, 1)
+                r, z = torch.sigmoid(xr + hr), torch.sigmoid(xz + hz)
+                n = torch.tanh(xn + r * hn)
+                h = (1 - z) * n + z * h
+            outs[d][t] = h
+    return torch.cat([torch.stack(outs[0], 1), torch.stack(outs[1], 1)], dim=2)
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+@pytest.mark.parametrize("B,T,H", [(1, 5, 300), (3, 8, 300), (2, 6, 40)])
+def test_birnn_bwd_dG_per_step(dev, cell, B, T, H):
+    ng = 4 if cell == "lstm" else 3
+    NGH = ng * H
+    g = torch.Generator().manual_seed(B * 31 + T)
+    G = torch.randn(B, T, 2, NGH, generator=g, dtype=torch.float64) * 0.5
+    whh = torch.randn(2, NGH, H, generator=g, dtype=torch.float64) / H ** 0.5
+    bhh = torch.randn(2, NGH, generator=g, dtype=torch.float64) * 0.1
+    Gl = G.clone().requires_grad_(True)
+    bl = bhh.clone().requires_grad_(True)
+    out = _manual_birnn(cell, Gl, whh, bl, H)
+    gout = torch.randn(out.shape, generator=g, dtype=torch.float64)
+    (out * gout).sum().backward()
+    cellid = 0 if cell == "lstm" else 1
+    Gd = G.float().to(dev).contiguous()
+    whd = whh.float().to(dev).contiguous()
+    bhd = bhh.float().to(dev).contiguous()
+    o = torch.empty(B, T, 2 * H, device=dev)
+    hp = torch.empty_like(o)
+    act = torch.empty(B, T, 2, 4 * H, device=dev)
+    cs = torch.empty(B, T, 2, H, device=dev)
+    ws = _lib.query("dl4ss_birnn_workspace_bytes", cellid, B, H)
+    wsb = torch.empty((ws + 7) // 8, dtype=torch.int64, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("dl4ss_birnn_fwd", cellid, B, T, H, _lib.ptr(Gd), _lib.ptr(whd), _lib.ptr(bhd), _lib.ptr(o),
+              _lib.ptr(hp), _lib.ptr(act), _lib.ptr(cs), _lib.ptr(wsb), ws, _lib.ptr(st), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert (o.cpu().double() - out.detach()).abs().max() < 1e-5
+    gd = gout.float().to(dev).contiguous()
+    dG = torch.zeros(B * T, 2 * NGH, device=dev)
+    dGh = torch.zeros_like(dG)
+    _lib.call("dl4ss_birnn_bwd", cellid, B, T, H, _lib.ptr(gd), None, _lib.ptr(whd), _lib.ptr(act), _lib.ptr(cs),
+              _lib.ptr(hp), _lib.ptr(dG), _lib.ptr(dGh), _lib.ptr(wsb), ws, _lib.ptr(st), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert int(st.item()) == 0
+    ours = dG.cpu().double().view(B, T, 2, NGH)
+    ref = Gl.grad
+    errs = [[(ours[:, t, d] - ref[:, t, d]).abs().max().item() for t in range(T)] for d in range(2)]
+    scale = ref.abs().max().item()
+    assert max(max(e) for e in errs) < 1e-4 * scale, (errs, scale)
+    # b_hh gradient (sum over b,t of dGh)
+    dgh = (dGh if cell == "gru" else dG).cpu().double().view(B, T, 2, NGH).sum((0, 1))
+    assert (dgh - bl.grad).abs().max() < 1e-4 * bl.grad.abs().max()
