@@ -11,7 +11,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdl4ss_hip.so")
+LIB_PATH = os.environ.get("DL4SS_LIB", os.path.join(_HERE, "libdl4ss_hip.so"))
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -25,8 +25,8 @@ SIGNATURES = {
     "dl4ss_mix_sources": [P, P, I, I, I, P, P, P, P],
     "dl4ss_gemm": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, P],
     "dl4ss_birnn_workspace_bytes": [I, I, I],
-    "dl4ss_birnn_fwd": [I, I, I, I, P, P, P, P, P, P, P, P, LL, P, P],
-    "dl4ss_birnn_bwd": [I, I, I, I, P, P, P, P, P, P, P, P, P, LL, P, P],
+    "dl4ss_birnn_fwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, LL, P, P],
+    "dl4ss_birnn_bwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_attn_nblk": [I, I],
     "dl4ss_mask_attn_loss": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, P, P, P, P],
     "dl4ss_pit_select": [P, I, I, I, P, P],

@@ -23,19 +23,62 @@
 // has consumed it, because producing step s+2 needs all of step s+1).  All
 // spins are bounded: a timeout sets *status and the workgroup exits.
 // Granule buffers are zeroed by hipMemsetAsync in the launch function.
-// Co-residency: grid <= 240 workgroups, resources sized for >= 2 per CU.
+//
+// Wave roles (512 threads = 8 waves, 2 per SIMD): a wave's vmcnt retires
+// loads and stores in issue order, so a wave that polls granules must not
+// carry outstanding stores.  Waves 0-3 do the cell update and ALL global
+// stores (granules first, then prefetch loads for the next step, then the
+// saved activations); waves 4-7 only poll granules into LDS.  All 8 waves run
+// the register-resident matvec (two waves per SIMD keep the VALU issuing).
+// Co-residency: grid <= 240 workgroups.
 #include "common.h"
 
 namespace {
 
 enum { CELL_LSTM = 0, CELL_GRU = 1 };
-constexpr int NT = 256;
-constexpr int WMAX = 104;   // fwd weights per thread
-constexpr int RPLMAX = 20;  // bwd rows per thread
-constexpr int KGLMAX = 6;   // bwd k per thread
+constexpr int NT = 512;
+constexpr int NROLE = 256;   // [0,256): cell + publish ; [256,512): gather
+constexpr int WMAX = 64;     // fwd weights per thread (generic path)
+constexpr int RPLMAX = 20;   // bwd rows per thread
+constexpr int KGLMAX = 6;    // bwd k per thread
+constexpr int HMAX = 320;    // largest hidden size (sizes the per-thread gather/publish offset arrays)
 constexpr unsigned SPIN_LIMIT = 1u << 20;  // ~1 s of polling: a stuck hand-off exits, never hangs
 
 typedef unsigned long long u64;
+
+// Diagnostic build only (-DRNN_STAMPS, tools/build_stamps.py): per-phase s_memtime
+// sums for threads 0 (cell/publish role) and 256 (gather role) of every workgroup.
+#ifdef RNN_STAMPS
+__device__ __forceinline__ u64 stamp_now() {
+  u64 t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP_DECL u64 st_prev = stamp_now(), st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(i) { const u64 n_ = stamp_now(); st_acc[i] += n_ - st_prev; st_prev = n_; }
+#define STAMP_FLUSH                                                                   \
+  if (a.stamps && (threadIdx.x == 0 || threadIdx.x == NROLE))                        \
+    for (int i_ = 0; i_ < 8; ++i_) a.stamps[blockIdx.x * 16 + (threadIdx.x ? 8 : 0) + i_] = st_acc[i_];
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH
+#endif
+
+// Gate nonlinearities on the serial critical path: v_exp + v_rcp (1 ulp) instead of
+// the IEEE division / ocml tanh sequences (the cell update runs on one wave).
+__device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f; }
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned short bf16_rne(float f) {
+  unsigned u = __float_as_uint(f);
+  u += 0x7FFF + ((u >> 16) & 1);
+  return (unsigned short)(u >> 16);
+}
 
 __device__ __forceinline__ void put_granule(u64* g, unsigned tag, float v) {
   const u64 x = ((u64)tag << 32) | (u64)__float_as_uint(v);
@@ -62,6 +105,7 @@ struct RnnArgs {
   float* dGh;            // bwd GRU: grad wrt W_hh h + b_hh (LSTM: == dG, may be null)
   u64* xbuf;             // granules
   int* status;
+  u64* stamps;           // diagnostic build only
 };
 
 __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& group, int& w) {
@@ -75,10 +119,63 @@ __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& grou
   }
 }
 
-template <int CELL, int BC, int KPL_T>
-__global__ __launch_bounds__(NT, 2) void rnn_fwd_kernel(RnnArgs a) {
-  constexpr int WN = KPL_T > 0 ? KPL_T : WMAX;  // weights per thread (compile-time)
+// Per-timestep operand prefetch, run by the gather waves so that the cell waves
+// issue no loads at all (their vmcnt then only ever holds stores): item q is
+// p[q][(t + shift[q]) * stride[q]] (0 outside [0, T)), landing in LDS at dst[q].
+// Loads for step s+1 are issued during step s and committed to LDS at step s+1
+// (by then the granule poll has already waited past them).
+template <int NQ>
+struct StepLoader {
+  const float* p[NQ];
+  int stride[NQ], shift[NQ], dst[NQ];
+  float v[NQ];
+  __device__ __forceinline__ void issue(int t, int T) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int tt = t + shift[q];
+      v[q] = (p[q] != nullptr && tt >= 0 && tt < T) ? p[q][(long long)tt * stride[q]] : 0.0f;
+    }
+  }
+  __device__ __forceinline__ void commit(float* lds) const {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (dst[q] >= 0) lds[dst[q]] = v[q];
+  }
+};
+
+// Poll the granules src[off[g]] (off < 0: nothing to read) until every tag == tag;
+// returns false on timeout.  Offsets are computed once per launch by the caller;
+// all loads of the thread are in flight at once and only stale ones are re-issued.
+template <int GM>
+__device__ __forceinline__ bool gather(const u64* src, const int (&off)[GM], unsigned tag, u64 (&v)[GM]) {
+  const u64 done = (u64)tag << 32;
+#pragma unroll
+  for (int g = 0; g < GM; ++g) v[g] = off[g] >= 0 ? get_granule(src + off[g]) : done;
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int g = 0; g < GM; ++g) ok &= (unsigned)(v[g] >> 32) == tag;
+    if (ok) return true;
+    if (++spins > SPIN_LIMIT) return false;
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int g = 0; g < GM; ++g)
+      if ((unsigned)(v[g] >> 32) != tag) v[g] = get_granule(src + off[g]);
+  }
+}
+
+// MF = false: exact fp32 matvec on the VALU (the parity mode); W_hh slice in fp32
+//      registers, k split over KP thread parts, partial sums combined by the cell thread.
+// MF = true: bf16 MFMA matvec (v_mfma_f32_16x16x32_bf16, fp32 accumulate; the
+//      throughput mode): wave m owns the 16-row tile m of W_hh (bf16 A fragments in
+//      registers for all K), h staged in LDS as bf16 [batch][k] (the B operand), one
+//      MFMA chain per wave -- no partial sums at all.
+template <int CELL, int BC, int KPL_T, bool MF>
+__global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
+  constexpr int WN = MF ? 1 : (KPL_T > 0 ? KPL_T : WMAX);  // fp32 weights per thread (compile-time)
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
+  constexpr int KSMAX = HMAX / 32;
   const int H = a.H, T = a.T, J = a.J;
   const int R = NGATE * J;
   const int ngroups = 2 * a.nchunk;
@@ -88,17 +185,25 @@ __global__ __launch_bounds__(NT, 2) void rnn_fwd_kernel(RnnArgs a) {
   const int b0 = chunk * BC;
   const int j0 = w * J;
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
   const int GH = NGATE * H;
+  const int MT = (R + 15) / 16;
+  constexpr int SHB = KSMAX * 32 + 8;  // bf16 row stride of the MFMA B image (k >= H stays zero)
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sh = smem;                    // [BC][HP]
-  float* spart = sh + BC * a.HP;       // [KP][BC][R]
+  // fp32 path: sh [BC][HP], spart [KP][BC][R]; MFMA path: shb bf16 [16][SHB], sgate [BC][MT*16]
+  float* sh = smem;
+  float* spart = sh + BC * a.HP;
+  unsigned short* shb = reinterpret_cast<unsigned short*>(smem);
+  float* sgate = smem + 8 * SHB;  // after 16 x SHB bf16
+  float* sin = MF ? sgate + BC * MT * 16 : spart + a.KP * BC * R;  // [2][BC*J][4] step inputs (double buffer)
 
-  // ---- weights of this workgroup in registers: thread (r, kp) holds W[row(r)][kp*KPL + i]
+  // ---- weights of this workgroup in registers
   float wreg[WN];
-  const bool mv = tid < R * a.KP;
+  bf16x8 afrag[MF ? KSMAX : 1];
+  const bool mv = MF ? wv < MT : tid < R * a.KP;
   const int r = tid % R, kp = tid / R;
-  {
+  if constexpr (!MF) {  // thread (r, kp) holds W[row(r)][kp*KPL + i]
     const int q = r / J, u = r % J;
     const bool rv = mv && (j0 + u < H);
     const float* wrow = a.Whh + ((long long)d * GH + q * H + j0 + u) * H;
@@ -107,11 +212,23 @@ __global__ __launch_bounds__(NT, 2) void rnn_fwd_kernel(RnnArgs a) {
       const int k = kp * a.KPL + i;
       wreg[i] = (rv && i < a.KPL && k < H) ? wrow[k] : 0.0f;
     }
+    for (int i = tid; i < BC * a.HP; i += NT) sh[i] = 0.0f;  // padding stays zero
+  } else {  // lane holds A[row m*16 + (lane&15)][k = ks*32 + 8(lane>>4) + j]
+    const int rl = wv * 16 + (lane & 15);
+    const int q = rl / J, u = rl % J;
+    const bool rv = mv && rl < R && j0 + u < H;
+    const float* wrow = a.Whh + ((long long)d * GH + q * H + j0 + u) * H;
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = ks * 32 + 8 * (lane >> 4) + j;
+        afrag[ks][j] = (short)bf16_rne((rv && k < H) ? wrow[k] : 0.0f);
+      }
+    for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;  // bf16 image incl. padding rows/cols
   }
-  // zero the LDS h image (padding stays zero)
-  for (int i = tid; i < BC * a.HP; i += NT) sh[i] = 0.0f;
 
-  // ---- cell threads: (b, u)
+  // ---- cell threads (waves 0-3): (b, u)
   const bool ct = tid < BC * J;
   const int cb = tid / J, cu = tid % J;
   const int cj = j0 + cu;
@@ -123,106 +240,168 @@ __global__ __launch_bounds__(NT, 2) void rnn_fwd_kernel(RnnArgs a) {
   float hst = 0.0f, cst = 0.0f;  // h_{t-1}, c_{t-1}
 
   u64* xg = a.xbuf + (long long)group * 2 * BC * H;
-  float gpre[NGATE];
-  auto load_g = [&](int s) {
-    const int t = d == 0 ? s : T - 1 - s;
+  // gather role: granule offsets and LDS destinations, fixed for the whole launch
+  constexpr int GM = (BC * HMAX + NROLE - 1) / NROLE;
+  int goff[GM], gdst[GM];
 #pragma unroll
-    for (int q = 0; q < NGATE; ++q)
-      gpre[q] = cval ? a.G[(((long long)bg * T + t) * 2 + d) * GH + q * H + cj] : 0.0f;
-  };
-  load_g(0);
+  for (int g = 0; g < GM; ++g) {
+    const int i = tid - NROLE + g * NROLE;
+    const bool on = tid >= NROLE && i < BC * H;
+    goff[g] = on ? i : -1;
+    gdst[g] = on ? (i / H) * (MF ? SHB : a.HP) + i % H : 0;
+  }
+  // gather role: input projection G[b][t][d][q*H + j] of every own (b, unit, gate)
+  constexpr int NQ = (BC * 20 * 4 + NROLE - 1) / NROLE;
+  StepLoader<NQ> ld;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = tid - NROLE + q * NROLE;  // item = gate * (BC*J) + cell
+    const int gate = i / (BC * J), cell = i % (BC * J);
+    const int ib = b0 + cell / J, ij = j0 + cell % J;
+    const bool on = tid >= NROLE && gate < NGATE;
+    ld.p[q] = (on && ib < a.B && ij < H) ? a.G + ((long long)ib * T * 2 + d) * GH + gate * H + ij : nullptr;
+    ld.stride[q] = 2 * GH;
+    ld.shift[q] = 0;
+    ld.dst[q] = on ? cell * 4 + gate : -1;
+  }
+  if (tid >= NROLE) ld.issue(d == 0 ? 0 : T - 1, T);
   __syncthreads();
+  STAMP_DECL
 
+  // ---- fused-gate matvec partials: spart[kp][b][r] = sum_i W[r][kp*KPL+i] h[b][kp*KPL+i]
+  auto matvec = [&]() {
+    if (!mv) return;
+    if constexpr (MF) {  // sgate[b][m*16 + row] = sum_k W[row][k] h[b][k]
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const unsigned short* bp = shb + (lane & 15) * SHB + 8 * (lane >> 4);
+      bf16x8 bv[KSMAX];  // all B reads in flight before the MFMA chain (zero A/B beyond H)
+#pragma unroll
+      for (int ks = 0; ks < KSMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
+#pragma unroll
+      for (int ks = 0; ks < KSMAX; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[ks], bv[ks], acc, 0, 0, 0);
+      const int col = lane & 15;
+      if (col < BC) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sgate[col * MT * 16 + wv * 16 + (lane >> 4) * 4 + i] = acc[i];
+      }
+      return;
+    }
+    float acc[BC];
+#pragma unroll
+    for (int bb = 0; bb < BC; ++bb) acc[bb] = 0.0f;
+    const float* hk = sh + kp * a.KPL;
+#pragma unroll
+    for (int i = 0; i < WN; i += 4) {
+      if (KPL_T > 0 || i < a.KPL) {
+#pragma unroll
+        for (int bb = 0; bb < BC; ++bb) {
+          const float4 hv = *reinterpret_cast<const float4*>(hk + bb * a.HP + i);
+          acc[bb] = fmaf(wreg[i], hv.x, acc[bb]);
+          acc[bb] = fmaf(wreg[i + 1], hv.y, acc[bb]);
+          acc[bb] = fmaf(wreg[i + 2], hv.z, acc[bb]);
+          acc[bb] = fmaf(wreg[i + 3], hv.w, acc[bb]);
+        }
+      }
+    }
+#pragma unroll
+    for (int bb = 0; bb < BC; ++bb) spart[(kp * BC + bb) * R + r] = acc[bb];
+  };
+
+  // Role-split loops with the same barrier sequence per step (B1, B2).  Waves 4-7
+  // (gather) issue only loads, waves 0-3 (cell) only stores, so neither loop's
+  // waitcnt state ever has to drain the other kind.
+  if (tid >= NROLE) {
+    for (int s = 0; s < T; ++s) {
+      // ---- gather h_{s-1} (granules, tag s) and commit this step's inputs
+      if (s > 0) {
+        u64 v[GM];
+        if (!gather<GM>(xg + (long long)((s - 1) & 1) * BC * H, goff, (unsigned)s, v)) {
+          atomicOr(a.status, 1);
+          return;
+        }
+#pragma unroll
+        for (int g = 0; g < GM; ++g)
+          if (goff[g] >= 0) {
+            if constexpr (MF)
+              shb[gdst[g]] = bf16_rne(__uint_as_float((unsigned)v[g]));
+            else
+              sh[gdst[g]] = __uint_as_float((unsigned)v[g]);
+          }
+      }
+      ld.commit(sin + (s & 1) * BC * J * 4);
+      if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
+      STAMP(0)
+      __syncthreads();  // B1
+      STAMP(1)
+      matvec();
+      STAMP(2)
+      __syncthreads();  // B2
+      STAMP(3)
+    }
+    STAMP_FLUSH
+    return;
+  }
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? s : T - 1 - s;
-    // ---- gather h_{s-1} of the whole group (granules, tag s)
-    if (s > 0) {
-      const u64* src = xg + (long long)((s - 1) & 1) * BC * H;
-      const unsigned tag = (unsigned)s;
-      for (int i = tid; i < BC * H; i += NT) {
-        u64 v = get_granule(src + i);
-        unsigned spins = 0;
-        while ((unsigned)(v >> 32) != tag) {
-          if (++spins > SPIN_LIMIT) {
-            atomicOr(a.status, 1);
-            return;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          v = get_granule(src + i);
-        }
-        const int bb = i / H, k = i % H;
-        sh[bb * a.HP + k] = __uint_as_float((unsigned)v);
-      }
-      __syncthreads();
-    }
-    // ---- fused-gate matvec partials: spart[kp][b][r] = sum_i W[r][kp*KPL+i] h[b][kp*KPL+i]
-    if (mv) {
-      float acc[BC];
-#pragma unroll
-      for (int bb = 0; bb < BC; ++bb) acc[bb] = 0.0f;
-      const float* hk = sh + kp * a.KPL;
-#pragma unroll
-      for (int i = 0; i < WN; i += 4) {
-        if (KPL_T > 0 || i < a.KPL) {
-#pragma unroll
-          for (int bb = 0; bb < BC; ++bb) {
-            const float4 hv = *reinterpret_cast<const float4*>(hk + bb * a.HP + i);
-            acc[bb] = fmaf(wreg[i], hv.x, acc[bb]);
-            acc[bb] = fmaf(wreg[i + 1], hv.y, acc[bb]);
-            acc[bb] = fmaf(wreg[i + 2], hv.z, acc[bb]);
-            acc[bb] = fmaf(wreg[i + 3], hv.w, acc[bb]);
-          }
-        }
-      }
-#pragma unroll
-      for (int bb = 0; bb < BC; ++bb) spart[(kp * BC + bb) * R + r] = acc[bb];
-    }
-    __syncthreads();
-    // ---- cell update for (b, u)
+    STAMP(0)
+    __syncthreads();  // B1
+    STAMP(1)
+    matvec();
+    STAMP(2)
+    __syncthreads();  // B2
+    STAMP(3)
+    // ---- cell update for (b, u): publish first, then the saved state
     if (ct) {
       float hg[NGATE];
 #pragma unroll
       for (int q = 0; q < NGATE; ++q) {
         float sacc = bh[q];
-        for (int p = 0; p < a.KP; ++p) sacc += spart[(p * BC + cb) * R + q * J + cu];
+        if constexpr (MF)
+          sacc += sgate[cb * MT * 16 + q * J + cu];
+        else
+          for (int p = 0; p < a.KP; ++p) sacc += spart[(p * BC + cb) * R + q * J + cu];
         hg[q] = sacc;
       }
       float gx[NGATE];
 #pragma unroll
-      for (int q = 0; q < NGATE; ++q) gx[q] = gpre[q];
-      if (s + 1 < T) load_g(s + 1);  // prefetch next step's input projection
-      if (cval) {
-        const long long bt = (long long)bg * T + t;
-        float hn;
-        float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;  // act rows are 4H wide for both cells
-        if constexpr (CELL == CELL_LSTM) {
-          const float ig = sigmoidf_(gx[0] + hg[0]);
-          const float fg = sigmoidf_(gx[1] + hg[1]);
-          const float gg = tanhf(gx[2] + hg[2]);
-          const float og = sigmoidf_(gx[3] + hg[3]);
-          cst = fg * cst + ig * gg;
-          hn = og * tanhf(cst);
-          actp[0] = ig; actp[H] = fg; actp[2 * H] = gg; actp[3 * H] = og;
-          a.cs[(bt * 2 + d) * H + cj] = cst;
-        } else {
-          const float rg = sigmoidf_(gx[0] + hg[0]);
-          const float zg = sigmoidf_(gx[1] + hg[1]);
-          const float ng = tanhf(gx[2] + rg * hg[2]);
-          hn = (1.0f - zg) * ng + zg * hst;
-          actp[0] = rg; actp[H] = zg; actp[2 * H] = ng; actp[3 * H] = hg[2];
+      for (int q = 0; q < NGATE; ++q) gx[q] = sin[(s & 1) * BC * J * 4 + tid * 4 + q];
+      if (cj < H) {
+        float hn = 0.0f, st[4] = {0.f, 0.f, 0.f, 0.f};
+        if (cval) {
+          if constexpr (CELL == CELL_LSTM) {
+            const float ig = fsig(gx[0] + hg[0]);
+            const float fg = fsig(gx[1] + hg[1]);
+            const float gg = ftanh(gx[2] + hg[2]);
+            const float og = fsig(gx[3] + hg[3]);
+            cst = fg * cst + ig * gg;
+            hn = og * ftanh(cst);
+            st[0] = ig; st[1] = fg; st[2] = gg; st[3] = og;
+          } else {
+            const float rg = fsig(gx[0] + hg[0]);
+            const float zg = fsig(gx[1] + hg[1]);
+            const float ng = ftanh(gx[2] + rg * hg[2]);
+            hn = (1.0f - zg) * ng + zg * hst;
+            st[0] = rg; st[1] = zg; st[2] = ng; st[3] = hg[2];
+          }
         }
-        a.hprev[bt * 2 * H + d * H + cj] = hst;
-        a.out[bt * 2 * H + d * H + cj] = hn;
-        hst = hn;
+        // padded batch rows (bg >= B) still publish (zeros) so peers never wait on them
         put_granule(xg + (long long)(s & 1) * BC * H + cb * H + cj, (unsigned)(s + 1), hn);
-      } else if (ct && cj < H) {
-        // padded batch rows (bg >= B) still publish so peers never wait on them
-        put_granule(xg + (long long)(s & 1) * BC * H + cb * H + cj, (unsigned)(s + 1), 0.0f);
+        if (cval) {
+          const long long bt = (long long)bg * T + t;
+          float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;  // act rows are 4H wide for both cells
+          actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
+          if constexpr (CELL == CELL_LSTM) a.cs[(bt * 2 + d) * H + cj] = cst;
+          a.hprev[bt * 2 * H + d * H + cj] = hst;
+          a.out[bt * 2 * H + d * H + cj] = hn;
+        }
+        hst = hn;
       }
     }
-    // spart is rewritten only after the next gather's barrier; sh only after this
-    // step's matvec (all threads passed the barrier above) -> no extra barrier.
+    STAMP(4)
+    // sh is rewritten only after the next gather's barrier (all matvec reads are
+    // behind the barrier above); spart only after that barrier too.
   }
+  STAMP_FLUSH
 }
 
 // --------------------------------------------------------------------------
@@ -230,12 +409,21 @@ __global__ __launch_bounds__(NT, 2) void rnn_fwd_kernel(RnnArgs a) {
 // forwards for the reverse direction.  Thread (b,u) owns dh/dc of its unit;
 // the recurrent term dh_rec[b][j] = sum_{rows r} dgh[b][r] W_hh[r][j] is formed
 // as per-workgroup partial sums over the workgroup's own rows (registers hold
-// W[rows of w][k-group]) published for all j, and each consumer sums the NG
-// partials of its own units in fixed order (deterministic).
+// W[rows of w][k-group]) published for all j; each consumer gathers the NG
+// partials of its own units (waves 4-7) and sums them in fixed order.
 // --------------------------------------------------------------------------
-template <int CELL, int BC>
-__global__ __launch_bounds__(NT, 2) void rnn_bwd_kernel(RnnArgs a) {
+//
+// MF = true (bf16 MFMA mode): waves 0-3 hold W_hh^T of the workgroup's rows as bf16
+// A fragments (output unit k on the MFMA row, gate row r on its K), dgh is staged
+// in LDS as the bf16 B image [batch][r]; each 16-unit tile's D lanes publish their
+// granules directly -- no partial-sum buffer, no third barrier.
+template <int CELL, int BC, int RPL_T, int KGL_T, bool MF>
+__global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
+  constexpr int RPLN = MF ? 1 : (RPL_T > 0 ? RPL_T : RPLMAX);  // rows per thread (compile-time)
+  constexpr int KGLN = MF ? 1 : (KGL_T > 0 ? KGL_T : KGLMAX);  // k per thread (compile-time)
+  constexpr int MTWMAX = (HMAX / 16 + 3) / 4;                    // MFMA unit tiles per wave
+  constexpr int KSRMAX = (4 * 20 + 31) / 32;                     // MFMA K-steps over gate rows
   const int H = a.H, T = a.T, J = a.J, NG = a.NG;
   const int R = NGATE * J;
   const int ngroups = 2 * a.nchunk;
@@ -247,27 +435,75 @@ __global__ __launch_bounds__(NT, 2) void rnn_bwd_kernel(RnnArgs a) {
   const int tid = threadIdx.x;
   const int GH = NGATE * H;
   const int AH = 4 * H;  // act row width (LSTM i,f,g,o; GRU r,z,n and W_hn h + b_hn)
+  const int RPAD = a.RP * RPLN;  // padded row count (rows >= R stay zero)
+  const int KW = a.KG * KGLN;
+
+  const int lane = tid & 63, wv = tid >> 6;
+  constexpr int SDG = KSRMAX * 32 + 8;  // bf16 row stride of the MFMA B image (rows >= R stay zero)
+  constexpr int WSPAN = MTWMAX * 16;     // output units per MFMA wave (contiguous)
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sdg = smem;                       // [BC][R]   dgh of this workgroup's rows
-  float* spart = sdg + BC * R;             // [RP][BC][KG*KGL]
-  const int KW = a.KG * a.KGL;
+  // fp32 path: sdg [BC][RPAD] dgh of this workgroup's rows, then sdh, spart [RP][BC][KW]
+  // MFMA path: sdgb bf16 [16][SDG], then sdh
+  float* sdg = smem;
+  unsigned short* sdgb = reinterpret_cast<unsigned short*>(smem);
+  float* sdh = MF ? smem + 8 * SDG : sdg + BC * RPAD;  // [NG][BC][J] gathered partials
+  float* spart = sdh + ((NG * BC * J + 3) & ~3);        // fp32: [RP][BC][KW]; MFMA: [4 waves][BC][WSPAN]
+  float* sop = spart + (MF ? 4 * BC * WSPAN : a.RP * BC * KW);  // [2][BC*J][8] per-step operands
+  for (int i = tid; i < (MF ? 8 * SDG : BC * RPAD) + NG * BC * J; i += NT) smem[i] = 0.0f;
 
-  // thread (kg, rp): rows [rp*RPL, +RPL), k in [kg*KGL, +KGL)
+  // fp32: thread (kg, rp): rows [rp*RPLN, +RPLN), k in [kg*KGLN, +KGLN)
   const int kg = tid % a.KG, rp = tid / a.KG;
-  const bool mv = rp < a.RP;
-  float wreg[RPLMAX][KGLMAX];
+  const bool mv = MF ? wv < 4 : rp < a.RP;
+  float wreg[RPLN][KGLN];
+  bf16x8 afr[MF ? MTWMAX : 1][MF ? KSRMAX : 1];
+  if constexpr (!MF) {
 #pragma unroll
-  for (int i = 0; i < RPLMAX; ++i) {
-    const int rr = rp * a.RPL + i;
-    const int q = rr / J, u = rr % J;
-    const bool rv = mv && i < a.RPL && rr < R && j0 + u < H;
-    const float* wrow = a.Whh + ((long long)d * GH + q * H + j0 + u) * H;
+    for (int i = 0; i < RPLN; ++i) {
+      const int rr = rp * RPLN + i;
+      const int q = rr / J, u = rr % J;
+      const bool rv = mv && rr < R && j0 + u < H;
+      const float* wrow = a.Whh + ((long long)d * GH + q * H + j0 + u) * H;
 #pragma unroll
-    for (int c = 0; c < KGLMAX; ++c) {
-      const int k = kg * a.KGL + c;
-      wreg[i][c] = (rv && c < a.KGL && k < H) ? wrow[k] : 0.0f;
+      for (int c = 0; c < KGLN; ++c) {
+        const int k = kg * KGLN + c;
+        wreg[i][c] = (rv && k < H) ? wrow[k] : 0.0f;
+      }
     }
+  } else {  // tile m = wv*MTWMAX + t: lane holds A[k = m*16 + (lane&15)][r = ks*32 + 8(lane>>4) + j] = W[row(r)][k]
+#pragma unroll
+    for (int t = 0; t < MTWMAX; ++t) {
+      const int k = (wv * MTWMAX + t) * 16 + (lane & 15);
+#pragma unroll
+      for (int ks = 0; ks < KSRMAX; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int rr = ks * 32 + 8 * (lane >> 4) + j;
+          const int q = rr / J, u = rr % J;
+          const bool ok = mv && k < H && rr < R && j0 + u < H;
+          afr[t][ks][j] = (short)bf16_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
+        }
+    }
+  }
+  // gather role: offsets of the NG partials of every own (b, unit), fixed per launch
+  constexpr int GM = (BC * (HMAX + 20) + NROLE - 1) / NROLE;
+  int goff[GM];
+#pragma unroll
+  for (int g = 0; g < GM; ++g) {
+    const int i = tid - NROLE + g * NROLE;
+    goff[g] = -1;
+    if (tid >= NROLE && i < NG * BC * J) {
+      const int p = i / (BC * J), rem = i % (BC * J), bb = rem / J, u = rem % J;
+      if (j0 + u < H) goff[g] = p * BC * H + bb * H + j0 + u;
+    }
+  }
+  // publish role: (b, k) of every granule this thread writes, fixed per launch
+  constexpr int GP = (BC * HMAX + NROLE - 1) / NROLE;
+  int psrc[GP];
+#pragma unroll
+  for (int g = 0; g < GP; ++g) {
+    const int i = tid + g * NROLE;
+    psrc[g] = (!MF && tid < NROLE && i < BC * H) ? (i / H) * KW + i % H : -1;
   }
 
   const bool ct = tid < BC * J;
@@ -279,60 +515,151 @@ __global__ __launch_bounds__(NT, 2) void rnn_bwd_kernel(RnnArgs a) {
   float dh_dir = 0.0f;   // GRU direct dh term carried to the earlier step
 
   u64* xg = a.xbuf + (long long)group * 2 * NG * BC * H;
+  // d(mean_t h) broadcast term: constant over t, loaded once by the cell thread
+  const float doutb = (cval && a.dOutB) ? a.dOutB[(long long)bg * 2 * H + d * H + cj] : 0.0f;
 
-  // prefetched per-step operands for the cell thread
-  float p_dout = 0.f, p_act[4] = {0.f, 0.f, 0.f, 0.f}, p_c = 0.f, p_cprev = 0.f, p_hprev = 0.f;
-  auto load_step = [&](int s) {
-    if (!cval) return;
-    const int t = d == 0 ? T - 1 - s : s;
-    const long long bt = (long long)bg * T + t;
-    p_dout = a.dOut[bt * 2 * H + d * H + cj] + (a.dOutB ? a.dOutB[(long long)bg * 2 * H + d * H + cj] : 0.0f);
-    const float* ap = a.act + (bt * 2 + d) * AH + cj;
+  // gather role: per-step operands of every own (b, unit): 8 slots per cell
+  //   0 dOut, 1..4 act, 5 c (LSTM) / h_prev (GRU), 6 c_prev (LSTM), 7 unused
+  constexpr int NQ = (BC * 20 * 8 + NROLE - 1) / NROLE;
+  StepLoader<NQ> ld;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) p_act[q] = ap[q * H];
-    if constexpr (CELL == CELL_LSTM) {
-      p_c = a.cs[(bt * 2 + d) * H + cj];
-      const int tp = d == 0 ? t - 1 : t + 1;  // the step that ran before t in this direction
-      p_cprev = (tp >= 0 && tp < T) ? a.cs[(((long long)bg * T + tp) * 2 + d) * H + cj] : 0.0f;
-    } else {
-      p_hprev = a.hprev[bt * 2 * H + d * H + cj];
+  for (int q = 0; q < NQ; ++q) {
+    const int i = tid - NROLE + q * NROLE;  // item = slot * (BC*J) + cell
+    const int slot = i / (BC * J), cell = i % (BC * J);
+    const int ib = b0 + cell / J, ij = j0 + cell % J;
+    const bool on = tid >= NROLE && slot < 8;
+    const bool valid = on && ib < a.B && ij < H;
+    const float* p = nullptr;
+    int stride = 2 * H, shift = 0;
+    if (valid) {
+      if (slot == 0) {
+        p = a.dOut + (long long)ib * T * 2 * H + d * H + ij;
+      } else if (slot <= 4) {
+        p = a.act + ((long long)ib * T * 2 + d) * AH + (slot - 1) * H + ij;
+        stride = 2 * AH;
+      } else if (CELL == CELL_LSTM && (slot == 5 || slot == 6)) {
+        p = a.cs + ((long long)ib * T * 2 + d) * H + ij;
+        shift = slot == 6 ? (d == 0 ? -1 : 1) : 0;  // the step that ran before t in this direction
+      } else if (CELL == CELL_GRU && slot == 5) {
+        p = a.hprev + (long long)ib * T * 2 * H + d * H + ij;
+      }
+    }
+    ld.p[q] = p;
+    ld.stride[q] = stride;
+    ld.shift[q] = shift;
+    ld.dst[q] = on ? cell * 8 + slot : -1;
+  }
+  if (tid >= NROLE) ld.issue(d == 0 ? T - 1 : 0, T);
+  STAMP_DECL
+
+  // ---- partials P[b][k] = sum_{own rows} dgh[b][r] W[r][k]
+  auto matvec = [&]() {
+    if (!mv) return;
+    if constexpr (MF) return;  // MFMA path: mfma_publish below
+    float acc[BC][KGLN];
+#pragma unroll
+    for (int bb = 0; bb < BC; ++bb)
+#pragma unroll
+      for (int c = 0; c < KGLN; ++c) acc[bb][c] = 0.0f;
+    const float* gr = sdg + rp * RPLN;
+#pragma unroll
+    for (int i = 0; i < RPLN; ++i) {
+#pragma unroll
+      for (int bb = 0; bb < BC; ++bb) {
+        const float g = gr[bb * RPAD + i];  // padded rows are zero
+#pragma unroll
+        for (int c = 0; c < KGLN; ++c) acc[bb][c] = fmaf(g, wreg[i][c], acc[bb][c]);
+      }
+    }
+#pragma unroll
+    for (int bb = 0; bb < BC; ++bb)
+#pragma unroll
+      for (int c = 0; c < KGLN; ++c) spart[(rp * BC + bb) * KW + kg * KGLN + c] = acc[bb][c];
+  };
+
+  // ---- MFMA path: D[k][b] = sum_r W[r][k] dgh[b][r] per 16-unit tile, published
+  //      straight from the accumulator lanes (col = batch, 4 consecutive units)
+  auto mfma_publish = [&](int s) {
+    const unsigned short* bp = sdgb + (lane & 15) * SDG + 8 * (lane >> 4);
+    bf16x8 bv[KSRMAX];
+#pragma unroll
+    for (int ks = 0; ks < KSRMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
+    // wave-private transpose: D lanes (4 consecutive units of one batch row) -> [BC][WSPAN]
+    float* wsc = spart + wv * BC * WSPAN;
+    const int col = lane & 15;
+#pragma unroll
+    for (int t = 0; t < MTWMAX; ++t) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KSRMAX; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t][ks], bv[ks], acc, 0, 0, 0);
+      if (col < BC) *reinterpret_cast<f32x4*>(wsc + col * WSPAN + t * 16 + 4 * (lane >> 4)) = acc;
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+    // coalesced publish of this wave's contiguous unit span (granules, tag s+1)
+    u64* dst = xg + (long long)(s & 1) * NG * BC * H + (long long)w * BC * H;
+#pragma unroll
+    for (int e0 = 0; e0 < BC * WSPAN; e0 += 64) {
+      const int e = e0 + lane;
+      const int bb = e / WSPAN, k = wv * WSPAN + e % WSPAN;
+      if ((BC * WSPAN) % 64 == 0 || e < BC * WSPAN)
+        if (k < H) put_granule(dst + bb * H + k, (unsigned)(s + 1), wsc[e]);
     }
   };
-  load_step(0);
 
+  // Role-split loops, same barrier sequence per step (B1, B2, B3 -- no B3 on the
+  // MFMA path); see the forward.
+  if (tid >= NROLE) {
+    for (int s = 0; s < T; ++s) {
+      // ---- gather the NG partials of every own unit (tag s) and commit this
+      //      step's operands (issued during the previous step)
+      if (s > 0) {
+        u64 v[GM];
+        if (!gather<GM>(xg + (long long)((s - 1) & 1) * NG * BC * H, goff, (unsigned)s, v)) {
+          atomicOr(a.status, 2);
+          return;
+        }
+#pragma unroll
+        for (int g = 0; g < GM; ++g)  // sdh[i] for i = tid-256 + 256 g ; unmapped entries stay 0
+          if (goff[g] >= 0) sdh[tid - NROLE + g * NROLE] = __uint_as_float((unsigned)v[g]);
+      }
+      ld.commit(sop + (s & 1) * BC * J * 8);
+      if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+      STAMP(0)
+      __syncthreads();  // B1
+      STAMP(1)
+      __syncthreads();  // B2
+      STAMP(3)
+      if (s + 1 == T) break;
+      if constexpr (!MF) {
+        matvec();
+        STAMP(4)
+        __syncthreads();  // B3
+        STAMP(5)
+      }
+    }
+    STAMP_FLUSH
+    return;
+  }
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
-    // ---- cell backward for (b, u)
+    STAMP(0)
+    __syncthreads();  // B1
+    STAMP(1)
+    // ---- cell backward for (b, u): LDS operands only, global stores only
     if (ct) {
       float dh_rec = 0.0f;
-      if (s > 0 && cj < H) {
-        const u64* src = xg + (long long)((s - 1) & 1) * NG * BC * H + cb * H + cj;
-        const unsigned tag = (unsigned)s;
-        for (int p = 0; p < NG; ++p) {
-          const u64* gp = src + (long long)p * BC * H;
-          u64 v = get_granule(gp);
-          unsigned spins = 0;
-          while ((unsigned)(v >> 32) != tag) {
-            if (++spins > SPIN_LIMIT) {
-              atomicOr(a.status, 2);
-              return;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            v = get_granule(gp);
-          }
-          dh_rec += __uint_as_float((unsigned)v);
-        }
-      }
-      const float dout = p_dout;
-      float act[4] = {p_act[0], p_act[1], p_act[2], p_act[3]};
-      const float c = p_c, cprev = p_cprev, hprev = p_hprev;
-      if (s + 1 < T) load_step(s + 1);
+      if (s > 0)
+        for (int p = 0; p < NG; ++p) dh_rec += sdh[(p * BC + cb) * J + cu];
+      const float* op = sop + (s & 1) * BC * J * 8 + tid * 8;
+      const float dout = op[0] + doutb;
+      const float act[4] = {op[1], op[2], op[3], op[4]};
+      const float c = op[5], cprev = op[6], hprev = op[5];
       float dgi[NGATE], dgh[NGATE];
       if (cval) {
         const float dh = dout + dh_rec + dh_dir;
         if constexpr (CELL == CELL_LSTM) {
           const float ig = act[0], fg = act[1], gg = act[2], og = act[3];
-          const float tc = tanhf(c);
+          const float tc = ftanh(c);
           const float dc = dc_next + dh * og * (1.0f - tc * tc);
           dgi[0] = dc * gg * ig * (1.0f - ig);
           dgi[1] = dc * cprev * fg * (1.0f - fg);
@@ -355,6 +682,13 @@ __global__ __launch_bounds__(NT, 2) void rnn_bwd_kernel(RnnArgs a) {
           dgh[1] = dgi[1];
           dgh[2] = dnp * rg;
         }
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) {
+          if constexpr (MF)
+            sdgb[cb * SDG + q * J + cu] = bf16_rne(dgh[q]);
+          else
+            sdg[cb * RPAD + q * J + cu] = dgh[q];
+        }
         const long long bt = (long long)bg * T + t;
         float* dgp = a.dG + (bt * 2 + d) * GH + cj;
 #pragma unroll
@@ -366,58 +700,63 @@ __global__ __launch_bounds__(NT, 2) void rnn_bwd_kernel(RnnArgs a) {
         }
       } else {
 #pragma unroll
-        for (int q = 0; q < NGATE; ++q) dgh[q] = 0.0f;
-      }
-#pragma unroll
-      for (int q = 0; q < NGATE; ++q) sdg[cb * R + q * J + cu] = dgh[q];
-    }
-    __syncthreads();
-    if (s + 1 == T) break;  // nothing flows past the sequence start
-    // ---- partials P[b][k] = sum_{own rows} dgh[b][r] W[r][k]
-    if (mv) {
-      float acc[BC][KGLMAX];
-#pragma unroll
-      for (int bb = 0; bb < BC; ++bb)
-#pragma unroll
-        for (int c = 0; c < KGLMAX; ++c) acc[bb][c] = 0.0f;
-#pragma unroll
-      for (int i = 0; i < RPLMAX; ++i) {
-        if (i < a.RPL) {
-          const int rr = rp * a.RPL + i;
-#pragma unroll
-          for (int bb = 0; bb < BC; ++bb) {
-            const float g = rr < R ? sdg[bb * R + rr] : 0.0f;
-#pragma unroll
-            for (int c = 0; c < KGLMAX; ++c) acc[bb][c] = fmaf(g, wreg[i][c], acc[bb][c]);
-          }
+        for (int q = 0; q < NGATE; ++q) {
+          if constexpr (MF)
+            sdgb[cb * SDG + q * J + cu] = 0;
+          else
+            sdg[cb * RPAD + q * J + cu] = 0.0f;
         }
       }
-#pragma unroll
-      for (int bb = 0; bb < BC; ++bb)
-#pragma unroll
-        for (int c = 0; c < KGLMAX; ++c)
-          if (c < a.KGL) spart[(rp * BC + bb) * KW + kg * a.KGL + c] = acc[bb][c];
     }
-    __syncthreads();
-    // ---- reduce over row parts and publish granules (tag s+1) for every k
+    STAMP(2)
+    __syncthreads();  // B2
+    STAMP(3)
+    if (s + 1 == T) break;  // nothing flows past the sequence start
+    if constexpr (MF) {
+      mfma_publish(s);
+      STAMP(6)
+      continue;
+    }
+    matvec();
+    STAMP(4)
+    __syncthreads();  // B3
+    STAMP(5)
+    // ---- reduce over row parts and publish granules (tag s+1): waves 0-3 only
     {
       u64* dst = xg + (long long)(s & 1) * NG * BC * H + (long long)w * BC * H;
-      for (int i = tid; i < BC * H; i += NT) {
-        const int bb = i / H, k = i % H;
-        float v = 0.0f;
-        for (int p = 0; p < a.RP; ++p) v += spart[(p * BC + bb) * KW + k];
-        put_granule(dst + i, (unsigned)(s + 1), v);
+#pragma unroll
+      for (int g = 0; g < GP; ++g) {
+        if (psrc[g] >= 0) {
+          float v = 0.0f;
+          for (int p = 0; p < a.RP; ++p) v += spart[p * BC * KW + psrc[g]];
+          put_granule(dst + tid + g * NROLE, (unsigned)(s + 1), v);
+        }
       }
     }
-    // sdg / spart are rewritten only after barriers every thread has passed
-    __syncthreads();
+    STAMP(6)
+    // sdg is rewritten after the next gather barrier, spart after the next cell
+    // barrier, sdh after this step's barriers: every reader is behind them.
+  }
+  STAMP_FLUSH
+}
+
+// compile-time (rows, k) per thread of the BPTT matvec: the shipped H = 300 plans
+// (LSTM R=80: 20 x 3, GRU R=60: 20 x 2) and the generic (guard-free, zero-padded) maxima
+void bwd_dims(int rpl, int kgl, int& rpln, int& kgln) {
+  if ((rpl == 20 && kgl == 3) || (rpl == 20 && kgl == 2)) {
+    rpln = rpl;
+    kgln = kgl;
+  } else {
+    rpln = RPLMAX;
+    kgln = KGLMAX;
   }
 }
 
 struct Plan {
   int BC, NG, J, nchunk;
   int KP, KPL, HP, RP, RPL, KG, KGL;
-  size_t smem_fwd, smem_bwd;
+  size_t smem_fwd, smem_bwd;        // fp32 VALU matvec
+  size_t smem_fwd_mf, smem_bwd_mf;  // bf16 MFMA matvec
 };
 
 bool make_plan(int cell, int B, int H, Plan& p) {
@@ -429,7 +768,7 @@ bool make_plan(int cell, int B, int H, Plan& p) {
     int KPL = (H + KP - 1) / KP;
     KPL = (KPL + 3) / 4 * 4;
     if (KPL > WMAX) continue;
-    // bwd: RP row parts x KG k-groups <= 256
+    // bwd: RP row parts x KG k-groups <= NT
     int best_rp = -1, best_kg = 0;
     for (int RP = 1; RP <= 16; ++RP) {
       const int RPL = (R + RP - 1) / RP;
@@ -439,57 +778,88 @@ bool make_plan(int cell, int B, int H, Plan& p) {
     }
     if (best_rp < 0) continue;
     const int NG = (H + J - 1) / J;
+    if (H > HMAX || J > 20) continue;  // gather/publish offset arrays are sized for H <= HMAX
     int BC = 0;
     for (int bc : {1, 2, 4, 8}) {
       const int nchunk = (B + bc - 1) / bc;
-      if (2 * nchunk * NG <= 240) { BC = bc; break; }
+      if (2 * nchunk * NG <= 240 && bc * J <= NROLE) {
+        BC = bc;
+        break;
+      }
     }
     if (!BC) continue;
     p.BC = BC; p.NG = NG; p.J = J; p.nchunk = (B + BC - 1) / BC;
     p.KP = KP; p.KPL = KPL; p.HP = KP * KPL;
     p.RP = best_rp; p.RPL = (R + best_rp - 1) / best_rp; p.KG = best_kg; p.KGL = (H + best_kg - 1) / best_kg;
-    p.smem_fwd = sizeof(float) * (BC * p.HP + KP * BC * R);
-    p.smem_bwd = sizeof(float) * (BC * R + p.RP * BC * p.KG * p.KGL);
+    int rpln, kgln;
+    bwd_dims(p.RPL, p.KGL, rpln, kgln);
+    p.smem_fwd = sizeof(float) * (BC * p.HP + KP * BC * R + 2 * BC * J * 4);
+    p.smem_bwd = sizeof(float) * (BC * p.RP * rpln + NG * BC * J + 3 + p.RP * BC * p.KG * kgln + 2 * BC * J * 8);
+    const int SHB = HMAX + 8, MT = (R + 15) / 16, SDG = (4 * 20 + 31) / 32 * 32 + 8;
+    p.smem_fwd_mf = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * J * 4);
+    p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
     return true;
   }
   return false;
 }
 
 template <int CELL, int BC>
-void launch_fwd(const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
-  // compile-time k-slice lengths for the shipped H = 300 plans (LSTM J=20: 100, GRU J=20: 76)
-  if (a.KPL == 100)
-    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 100>), dim3(grid), dim3(NT), smem, st, a);
-  else if (a.KPL == 76)
-    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 76>), dim3(grid), dim3(NT), smem, st, a);
+void launch_fwd(const RnnArgs& a, bool mf, int grid, size_t smem, hipStream_t st) {
+  // compile-time k-slice lengths for the shipped H = 300 plans (LSTM J=20: 52, GRU J=20: 40)
+  if (mf)
+    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, true>), dim3(grid), dim3(NT), smem, st, a);
+  else if (a.KPL == 52)
+    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 52, false>), dim3(grid), dim3(NT), smem, st, a);
+  else if (a.KPL == 40)
+    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 40, false>), dim3(grid), dim3(NT), smem, st, a);
   else
-    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0>), dim3(grid), dim3(NT), smem, st, a);
+    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, false>), dim3(grid), dim3(NT), smem, st, a);
 }
 template <int CELL, int BC>
-void launch_bwd(const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
-  hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC>), dim3(grid), dim3(NT), smem, st, a);
+void launch_bwd(const RnnArgs& a, bool mf, int grid, size_t smem, hipStream_t st) {
+  int rpln, kgln;
+  bwd_dims(a.RPL, a.KGL, rpln, kgln);
+  if (mf)
+    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 0, 0, true>), dim3(grid), dim3(NT), smem, st, a);
+  else if (rpln == 20 && kgln == 3)
+    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 20, 3, false>), dim3(grid), dim3(NT), smem, st, a);
+  else if (rpln == 20 && kgln == 2)
+    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 20, 2, false>), dim3(grid), dim3(NT), smem, st, a);
+  else
+    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 0, 0, false>), dim3(grid), dim3(NT), smem, st, a);
 }
 
 template <int CELL>
-int dispatch(bool fwd, int BC, const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
+int dispatch(bool fwd, bool mf, int BC, const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
   switch (BC) {
-    case 1: fwd ? launch_fwd<CELL, 1>(a, grid, smem, st) : launch_bwd<CELL, 1>(a, grid, smem, st); break;
-    case 2: fwd ? launch_fwd<CELL, 2>(a, grid, smem, st) : launch_bwd<CELL, 2>(a, grid, smem, st); break;
-    case 4: fwd ? launch_fwd<CELL, 4>(a, grid, smem, st) : launch_bwd<CELL, 4>(a, grid, smem, st); break;
-    case 8: fwd ? launch_fwd<CELL, 8>(a, grid, smem, st) : launch_bwd<CELL, 8>(a, grid, smem, st); break;
+    case 1: fwd ? launch_fwd<CELL, 1>(a, mf, grid, smem, st) : launch_bwd<CELL, 1>(a, mf, grid, smem, st); break;
+    case 2: fwd ? launch_fwd<CELL, 2>(a, mf, grid, smem, st) : launch_bwd<CELL, 2>(a, mf, grid, smem, st); break;
+    case 4: fwd ? launch_fwd<CELL, 4>(a, mf, grid, smem, st) : launch_bwd<CELL, 4>(a, mf, grid, smem, st); break;
+    case 8: fwd ? launch_fwd<CELL, 8>(a, mf, grid, smem, st) : launch_bwd<CELL, 8>(a, mf, grid, smem, st); break;
     default: return (int)hipErrorInvalidValue;
   }
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
 
+#ifdef RNN_STAMPS
+u64* g_stamps = nullptr;
+#endif
+
 void fill_args(RnnArgs& a, const Plan& p, int B, int T, int H) {
+#ifdef RNN_STAMPS
+  a.stamps = g_stamps;
+#endif
   a.B = B; a.T = T; a.H = H; a.J = p.J; a.NG = p.NG; a.nchunk = p.nchunk;
   a.KP = p.KP; a.KPL = p.KPL; a.HP = p.HP;
   a.RP = p.RP; a.RPL = p.RPL; a.KG = p.KG; a.KGL = p.KGL;
 }
 
 }  // namespace
+
+#ifdef RNN_STAMPS
+DL4SS_API void dl4ss_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
+#endif
 
 DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
   Plan p;
@@ -500,10 +870,11 @@ DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
   return fwd > bwd ? fwd : bwd;
 }
 
-DL4SS_API int dl4ss_birnn_fwd(int cell, int B, int T, int H, const float* G, const float* W_hh, const float* b_hh,
+DL4SS_API int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh, const float* b_hh,
                               float* out, float* hprev, float* act, float* cs, void* workspace,
                               long long ws_bytes, int* status, void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
+  DL4SS_REQUIRE(precision == 0 || precision == 1);
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && out && hprev && act && workspace && status);
   DL4SS_REQUIRE(cell == CELL_GRU || cs);
   Plan p;
@@ -519,15 +890,17 @@ DL4SS_API int dl4ss_birnn_fwd(int cell, int B, int T, int H, const float* G, con
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
   a.status = status;
   const int grid = (int)(groups * p.NG);
-  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, p.BC, a, grid, p.smem_fwd, st)
-                           : dispatch<CELL_GRU>(true, p.BC, a, grid, p.smem_fwd, st);
+  const bool mf = precision == 1;
+  const size_t smem = mf ? p.smem_fwd_mf : p.smem_fwd;
+  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, mf, p.BC, a, grid, smem, st)
+                           : dispatch<CELL_GRU>(true, mf, p.BC, a, grid, smem, st);
 }
 
-DL4SS_API int dl4ss_birnn_bwd(int cell, int B, int T, int H, const float* dOut, const float* dOut_bcast,
-                              const float* W_hh,
-                              const float* act, const float* cs, const float* hprev, float* dG, float* dGh,
-                              void* workspace, long long ws_bytes, int* status, void* stream) {
+DL4SS_API int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, const float* dOut, const float* dOut_bcast,
+                              const float* W_hh, const float* act, const float* cs, const float* hprev, float* dG,
+                              float* dGh, void* workspace, long long ws_bytes, int* status, void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
+  DL4SS_REQUIRE(precision == 0 || precision == 1);
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && dG && workspace && status);
   DL4SS_REQUIRE(cell == CELL_GRU ? (dGh && hprev) : (cs != nullptr));
   Plan p;
@@ -544,6 +917,8 @@ DL4SS_API int dl4ss_birnn_bwd(int cell, int B, int T, int H, const float* dOut, 
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
   a.status = status;
   const int grid = (int)(groups * p.NG);
-  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, p.BC, a, grid, p.smem_bwd, st)
-                           : dispatch<CELL_GRU>(false, p.BC, a, grid, p.smem_bwd, st);
+  const bool mf = precision == 1;
+  const size_t smem = mf ? p.smem_bwd_mf : p.smem_bwd;
+  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, p.BC, a, grid, smem, st)
+                           : dispatch<CELL_GRU>(false, mf, p.BC, a, grid, smem, st);
 }

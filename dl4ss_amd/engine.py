@@ -105,13 +105,16 @@ class SepTrainer:
     """Buffers and the step schedule for one (B, K, N) workload."""
 
     def __init__(self, net, batch, k, n_samples, mode="label", precision="fp32", lr=2e-4, sum_weight=0.5,
-                 loss_channels=None, betas=(0.9, 0.999), eps=1e-8, process_group=None):
+                 loss_channels=None, betas=(0.9, 0.999), eps=1e-8, process_group=None, rnn_precision=None):
         if mode not in ("label", "pit", "crm"):
             raise ValueError(mode)
         if (mode == "crm") != net.crm:
             raise ValueError("cRM mode needs a cRM net (query width 2E) and vice versa")
         self.net, self.B, self.K, self.N = net, batch, k, n_samples
         self.mode, self.precision = mode, precision
+        # recurrent matvec precision (defaults to the GEMM precision): "fp32" exact VALU,
+        # "bf16" MFMA with fp32 accumulate and fp32 cell state
+        self.rnn_precision = rnn_precision or precision
         self.lr, self.betas, self.eps = lr, betas, eps
         self.pg = process_group
         self.T = ops.n_frames(n_samples)
@@ -186,9 +189,9 @@ class SepTrainer:
         for l in range(net.L):
             ops.gemm(x, net.cat_view("weight_ih", l), transB=True, bias=net.cat_view("bias_ih", l), out=self.G,
                      precision=self.precision)
-            _lib.call("dl4ss_birnn_fwd", cell, B, T, H, _lib.ptr(self.G), _lib.ptr(net.cat_view("weight_hh", l)),
-                      _lib.ptr(net.cat_view("bias_hh", l)), _lib.ptr(self.out[l]), _lib.ptr(self.hprev[l]),
-                      _lib.ptr(self.act[l]), _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.rnn_ws),
+            _lib.call("dl4ss_birnn_fwd", cell, ops.PREC[self.rnn_precision], B, T, H, _lib.ptr(self.G),
+                      _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
+                      _lib.ptr(self.out[l]), _lib.ptr(self.hprev[l]), _lib.ptr(self.act[l]), _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.rnn_ws),
                       self.ws_bytes, _lib.ptr(self.status), st)
             x = self.out[l].view(BT, 2 * H)
         ops.gemm(x, net.view("mix.Linear.weight"), transB=True, bias=net.view("mix.Linear.bias"),
@@ -250,7 +253,7 @@ class SepTrainer:
         for l in range(net.L - 1, -1, -1):
             dG = self.G
             dGh = self.dGh if self.dGh is not None else dG
-            _lib.call("dl4ss_birnn_bwd", cell, B, T, H, _lib.ptr(dH),
+            _lib.call("dl4ss_birnn_bwd", cell, ops.PREC[self.rnn_precision], B, T, H, _lib.ptr(dH),
                       _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), _lib.ptr(dG),

@@ -72,17 +72,19 @@ long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
 /* One layer, both directions: G (B,T,2,NG*H) = X W_ih^T + b_ih (NG = 4 LSTM / 3 GRU),
  * W_hh (2, NG*H, H), b_hh (2, NG*H) -> out (B,T,2H) [fwd | reverse], hprev (B,T,2H)
  * (h_{t-1} per step), act (B,T,2,4H) gate activations, cs (B,T,2,H) LSTM cells.
+ * precision 0: exact fp32 recurrent matvec (VALU); 1: bf16 operands on MFMA with fp32
+ * accumulate (cell state, gates and all outputs stay fp32).
  * *status != 0 after the call means a hand-off timed out (results invalid).
  * Replaces the cuDNN recurrence of nn.LSTM / nn.GRU(batch_first, bidirectional)
  * at TDAA_beta/main_run_sstune_EvalVer.py:282-293, Torch_multi/main_run.py:263-273. */
-int dl4ss_birnn_fwd(int cell, int B, int T, int H, const float* G, const float* W_hh, const float* b_hh, float* out,
-                    float* hprev, float* act, float* cs, void* workspace, long long ws_bytes, int* status,
-                    void* stream);
+int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
+                    const float* b_hh, float* out, float* hprev, float* act, float* cs, void* workspace,
+                    long long ws_bytes, int* status, void* stream);
 /* BPTT of one layer: dOut (B,T,2H) (+ dOut_bcast (B,2H) at every t, may be NULL) ->
  * dG (B,T,2,NG*H) grad of the input projection (pre-activation) and, for GRU, dGh
  * grad of W_hh h + b_hh (for LSTM they coincide; dGh may be NULL). */
-int dl4ss_birnn_bwd(int cell, int B, int T, int H, const float* dOut, const float* dOut_bcast, const float* W_hh,
-                    const float* act, const float* cs, const float* hprev, float* dG, float* dGh, void* workspace,
+int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, const float* dOut, const float* dOut_bcast,
+                    const float* W_hh, const float* act, const float* cs, const float* hprev, float* dG, float* dGh, void* workspace,
                     long long ws_bytes, int* status, void* stream);
 
 /* ---- speaker-query mask attention + loss (fused forward/backward) -------- */

@@ -71,7 +71,7 @@ def _run_birnn_fwd(dev, cell, rnn, x, H):
     ws = _lib.query("dl4ss_birnn_workspace_bytes", cellid, B, H)
     wsb = torch.empty((ws + 7) // 8, dtype=torch.int64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.call("dl4ss_birnn_fwd", cellid, B, T, H, _lib.ptr(G), _lib.ptr(whh.detach()), _lib.ptr(bhh.detach()),
+    _lib.call("dl4ss_birnn_fwd", cellid, 0, B, T, H, _lib.ptr(G), _lib.ptr(whh.detach()), _lib.ptr(bhh.detach()),
               _lib.ptr(out), _lib.ptr(hprev), _lib.ptr(act), _lib.ptr(cs), _lib.ptr(wsb), ws, _lib.ptr(status),
               _lib.stream_ptr())
     torch.cuda.synchronize()
@@ -112,7 +112,7 @@ def test_birnn_bwd_matches_autograd(dev, cell, B, T, H, use_bc):
     dGh = torch.empty_like(dG) if cell == "gru" else None
     cellid = 0 if cell == "lstm" else 1
     gout_d, bc_d = gout.float().to(dev), bc.float().to(dev)  # keep alive across the async launch
-    _lib.call("dl4ss_birnn_bwd", cellid, B, T, H, _lib.ptr(gout_d), _lib.ptr(bc_d),
+    _lib.call("dl4ss_birnn_bwd", cellid, 0, B, T, H, _lib.ptr(gout_d), _lib.ptr(bc_d),
               _lib.ptr(r["whh"]), _lib.ptr(r["act"]), _lib.ptr(r["cs"]), _lib.ptr(r["hprev"]), _lib.ptr(dG),
               _lib.ptr(dGh), _lib.ptr(r["ws"]), r["wsn"], _lib.ptr(r["status"]), _lib.stream_ptr())
     torch.cuda.synchronize()
@@ -140,8 +140,29 @@ def test_birnn_bwd_matches_autograd(dev, cell, B, T, H, use_bc):
     assert (dx - x.grad).abs().max() / x.grad.abs().max() < 1e-4
 
 
-def _manual_birnn(cell, G, whh, bhh, H):
-    """Explicit bidirectional recurrence on precomputed input projections G (B,T,2,NGH) (fp64, autograd)."""
+def _bf16(x):
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+class _Bf16MatVec(torch.autograd.Function):
+    """gh = bf16(h) bf16(W)^T with fp64 accumulate; backward dh = bf16(dgh) bf16(W):
+    the operand rounding of the kernels' bf16 MFMA recurrence (precision 1)."""
+
+    @staticmethod
+    def forward(ctx, h, w):
+        wb = _bf16(w)
+        ctx.save_for_backward(wb)
+        return _bf16(h) @ wb.T
+
+    @staticmethod
+    def backward(ctx, g):
+        (wb,) = ctx.saved_tensors
+        return _bf16(g) @ wb, None
+
+
+def _manual_birnn(cell, G, whh, bhh, H, bf16=False):
+    """Explicit bidirectional recurrence on precomputed input projections G (B,T,2,NGH) (fp64, autograd).
+    bf16=True rounds the recurrent matvec operands (forward h and W, backward dgh) to bf16."""
     B, T = G.shape[:2]
     outs = [[None] * T, [None] * T]
     for d in range(2):
@@ -149,7 +170,7 @@ def _manual_birnn(cell, G, whh, bhh, H):
         c = torch.zeros(B, H, dtype=G.dtype)
         order = range(T) if d == 0 else range(T - 1, -1, -1)
         for t in order:
-            gh = h @ whh[d].T + bhh[d]
+            gh = (_Bf16MatVec.apply(h, whh[d]) if bf16 else h @ whh[d].T) + bhh[d]
             gx = G[:, t, d]
             if cell == "lstm":
                 i, f, g, o = (gx + gh).chunk(4, 1)
@@ -165,9 +186,15 @@ def _manual_birnn(cell, G, whh, bhh, H):
     return torch.cat([torch.stack(outs[0], 1), torch.stack(outs[1], 1)], dim=2)
 
 
+@pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("cell", ["lstm", "gru"])
-@pytest.mark.parametrize("B,T,H", [(1, 5, 300), (3, 8, 300), (2, 6, 40)])
-def test_birnn_bwd_dG_per_step(dev, cell, B, T, H):
+@pytest.mark.parametrize("B,T,H", [(1, 5, 300), (3, 8, 300), (2, 6, 40), (32, 12, 300)])
+def test_birnn_bwd_dG_per_step(dev, cell, B, T, H, prec):
+    """prec 0: exact fp32 recurrence vs fp64 (1e-5 abs on h, 1e-4 rel on dG).
+    prec 1: bf16-operand MFMA recurrence vs an fp64 recurrence with the same operand
+    rounding (_Bf16MatVec); tolerance 1e-3 abs on h, 2e-3 rel on dG (fp32 vs fp64
+    accumulation can flip an operand's bf16 rounding, 2^-9 relative, which then
+    propagates through the recurrence)."""
     ng = 4 if cell == "lstm" else 3
     NGH = ng * H
     g = torch.Generator().manual_seed(B * 31 + T)
@@ -176,8 +203,9 @@ def test_birnn_bwd_dG_per_step(dev, cell, B, T, H):
     bhh = torch.randn(2, NGH, generator=g, dtype=torch.float64) * 0.1
     Gl = G.clone().requires_grad_(True)
     bl = bhh.clone().requires_grad_(True)
-    out = _manual_birnn(cell, Gl, whh, bl, H)
+    out = _manual_birnn(cell, Gl, whh, bl, H, bf16=prec == 1)
     gout = torch.randn(out.shape, generator=g, dtype=torch.float64)
+    tol_h, tol_g = (1e-5, 1e-4) if prec == 0 else (1e-3, 2e-3)
     (out * gout).sum().backward()
     cellid = 0 if cell == "lstm" else 1
     Gd = G.float().to(dev).contiguous()
@@ -190,14 +218,14 @@ def test_birnn_bwd_dG_per_step(dev, cell, B, T, H):
     ws = _lib.query("dl4ss_birnn_workspace_bytes", cellid, B, H)
     wsb = torch.empty((ws + 7) // 8, dtype=torch.int64, device=dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.call("dl4ss_birnn_fwd", cellid, B, T, H, _lib.ptr(Gd), _lib.ptr(whd), _lib.ptr(bhd), _lib.ptr(o),
+    _lib.call("dl4ss_birnn_fwd", cellid, prec, B, T, H, _lib.ptr(Gd), _lib.ptr(whd), _lib.ptr(bhd), _lib.ptr(o),
               _lib.ptr(hp), _lib.ptr(act), _lib.ptr(cs), _lib.ptr(wsb), ws, _lib.ptr(st), _lib.stream_ptr())
     torch.cuda.synchronize()
-    assert (o.cpu().double() - out.detach()).abs().max() < 1e-5
+    assert (o.cpu().double() - out.detach()).abs().max() < tol_h
     gd = gout.float().to(dev).contiguous()
     dG = torch.zeros(B * T, 2 * NGH, device=dev)
     dGh = torch.zeros_like(dG)
-    _lib.call("dl4ss_birnn_bwd", cellid, B, T, H, _lib.ptr(gd), None, _lib.ptr(whd), _lib.ptr(act), _lib.ptr(cs),
+    _lib.call("dl4ss_birnn_bwd", cellid, prec, B, T, H, _lib.ptr(gd), None, _lib.ptr(whd), _lib.ptr(act), _lib.ptr(cs),
               _lib.ptr(hp), _lib.ptr(dG), _lib.ptr(dGh), _lib.ptr(wsb), ws, _lib.ptr(st), _lib.stream_ptr())
     torch.cuda.synchronize()
     assert int(st.item()) == 0
@@ -205,7 +233,7 @@ def test_birnn_bwd_dG_per_step(dev, cell, B, T, H):
     ref = Gl.grad
     errs = [[(ours[:, t, d] - ref[:, t, d]).abs().max().item() for t in range(T)] for d in range(2)]
     scale = ref.abs().max().item()
-    assert max(max(e) for e in errs) < 1e-4 * scale, (errs, scale)
+    assert max(max(e) for e in errs) < tol_g * scale, (errs, scale)
     # b_hh gradient (sum over b,t of dGh)
     dgh = (dGh if cell == "gru" else dG).cpu().double().view(B, T, 2, NGH).sum((0, 1))
-    assert (dgh - bl.grad).abs().max() < 1e-4 * bl.grad.abs().max()
+    assert (dgh - bl.grad).abs().max() < tol_g * bl.grad.abs().max()

@@ -29,10 +29,10 @@ def _oracle_features(src, gains, crm):
     return t(feats), t(X), t(Y)
 
 
-def _setup(dev, cell, L, B, K, N, mode, seed=3, adjust=True, loss_channels=None):
+def _setup(dev, cell, L, B, K, N, mode, seed=3, adjust=True, loss_channels=None, precision="fp32"):
     crm = mode == "crm"
     net = engine.SepNet(cell=cell, num_layers=L, crm=crm, adjust=adjust, device=dev, seed=seed)
-    tr = engine.SepTrainer(net, B, K, N, mode=mode, loss_channels=loss_channels)
+    tr = engine.SepTrainer(net, B, K, N, mode=mode, loss_channels=loss_channels, precision=precision)
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=seed)
     src, spk, u = gen.batch(B)
     gains = synth.gains_for(u, K)
@@ -41,8 +41,10 @@ def _setup(dev, cell, L, B, K, N, mode, seed=3, adjust=True, loss_channels=None)
     return net, tr, src, spk, gains, ref
 
 
-def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, loss_channels=None, adjust=True):
-    net, tr, src, spk, gains, ref = _setup(dev, cell, L, B, K, N, mode, adjust=adjust, loss_channels=loss_channels)
+def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, loss_channels=None, adjust=True,
+                  precision="fp32", tol_pred=1e-3):
+    net, tr, src, spk, gains, ref = _setup(dev, cell, L, B, K, N, mode, adjust=adjust, loss_channels=loss_channels,
+                                           precision=precision)
     feats, X, Y = _oracle_features(src, gains, mode == "crm")
     idx = torch.from_numpy(spk)
     # --- oracle step
@@ -80,11 +82,11 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
     # loss
     l = float(loss[0].cpu())
     assert abs(l - float(loss_ref)) / abs(float(loss_ref)) < tol_loss, (l, float(loss_ref))
-    # masked magnitude (the north-star parity metric): relative L2 <= 1e-3
+    # masked magnitude (the north-star parity metric): relative L2 <= 1e-3 (fp32)
     if mode == "label":
         pr = pred.cpu().view(B, K, T, F)
         rel = ((pr - pred_ref).norm() / pred_ref.norm()).item()
-        assert rel < 1e-3, rel
+        assert rel < tol_pred, rel
     # gradients (report every tensor's relative error on failure)
     errs = {}
     for name, gr in grads_ref.items():
@@ -93,6 +95,8 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
         errs[name] = (ours - gr).abs().max().item() / denom if denom > 0 else ours.abs().max().item()
     bad = {k: v for k, v in errs.items() if v > tol_grad}
     assert not bad, (bad, errs)
+    if precision != "fp32":
+        return  # a first Adam step is ~lr*sign(g): not comparable where bf16 moved a small gradient's sign
     # Adam-updated parameters: first step moves each weight by ~lr*sign(g); allow sign
     # disagreements only where the gradient itself is at rounding level
     for name, p in ref.named_parameters():
@@ -125,6 +129,17 @@ def test_step_crm(dev):
 def test_step_c1_101_channels(dev):
     # Torch_multi/main_run.py: BiGRU-2L, loss over 101 label channels, no sum term, no ADDJUST
     _compare_step(dev, "gru", 2, 1, 2, 4000, "label", loss_channels=101, adjust=False)
+
+
+def test_step_bilstm_bf16(dev):
+    """bf16 mode (bf16 GEMM operands + bf16 MFMA recurrence, fp32 accumulate and state)
+    against the fp32 oracle: loss 1e-2 rel, masked magnitude 1e-2 rel L2, grads 5e-2 of max."""
+    _compare_step(dev, "lstm", 4, 4, 2, 8000, "label", precision="bf16", tol_loss=1e-2, tol_grad=5e-2,
+                  tol_pred=1e-2)
+
+
+def test_step_bigru_bf16(dev):
+    _compare_step(dev, "gru", 2, 3, 2, 3000, "pit", precision="bf16", tol_loss=1e-2, tol_grad=5e-2, tol_pred=1e-2)
 
 
 def test_sepnet_state_dict_keys_match_oracle():

@@ -24,7 +24,7 @@ print("manual vs torch", (out2 - ref).abs().max().item())
 (out2 * gout).sum().backward()
 gout_d = gout.float().to(dev)
 dG = torch.zeros(B * T, 2 * NGH, device=dev)
-_lib.call("dl4ss_birnn_bwd", 0, B, T, H, _lib.ptr(gout_d), None, _lib.ptr(r["whh"]), _lib.ptr(r["act"]),
+_lib.call("dl4ss_birnn_bwd", 0, 0, B, T, H, _lib.ptr(gout_d), None, _lib.ptr(r["whh"]), _lib.ptr(r["act"]),
           _lib.ptr(r["cs"]), _lib.ptr(r["hprev"]), _lib.ptr(dG), None, _lib.ptr(r["ws"]), r["wsn"],
           _lib.ptr(r["status"]), _lib.stream_ptr())
 torch.cuda.synchronize()

@@ -1,0 +1,70 @@
+"""Diagnostic: per-phase cycle shares of the persistent BiRNN kernels.
+
+Builds a separate library with -DRNN_STAMPS (never the shipped one), runs one
+BiLSTM layer fwd + bwd at the bench shape and prints, per role thread, the
+average cycles per timestep spent in each phase."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from dl4ss_amd import build as B  # noqa: E402
+
+LIB = os.path.join(ROOT, "dl4ss_amd", "libdl4ss_hip_stamps.so")
+
+
+def build_stamps():
+    objs = []
+    os.makedirs("/tmp/stamps_obj", exist_ok=True)
+    for f in sorted(os.listdir(B.CSRC)):
+        if f.endswith(".hip"):
+            o = f"/tmp/stamps_obj/{f[:-4]}.o"
+            subprocess.run([B.HIPCC, *B.FLAGS, "-DRNN_STAMPS", "-I", B.CSRC, "-c", os.path.join(B.CSRC, f), "-o", o],
+                           check=True)
+            objs.append(o)
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", LIB], check=True)
+
+
+def main():
+    if not os.path.exists(LIB) or "--rebuild" in sys.argv:
+        build_stamps()
+    os.environ["DL4SS_LIB"] = LIB
+    import ctypes
+    import torch
+    from dl4ss_amd import _lib, engine
+
+    dev = torch.device("cuda")
+    Bsz, T, H = 32, 251, 300
+    net = engine.SepNet(cell="lstm", num_layers=1, device=dev)
+    prec = "bf16" if "--bf16" in sys.argv else "fp32"
+    tr = engine.SepTrainer(net, Bsz, 2, 32000, precision=prec)
+    stamps = torch.zeros(240 * 16, dtype=torch.int64, device=dev)
+    lib = _lib.lib()
+    lib.dl4ss_debug_set_stamps.argtypes = [ctypes.c_void_p]
+    lib.dl4ss_debug_set_stamps(ctypes.c_void_p(stamps.data_ptr()))
+    x = torch.randn(Bsz, T, 129, device=dev)
+    for rep in range(2):
+        stamps.zero_()
+        tr.forward(feats=x)
+        torch.cuda.synchronize()
+        fw = stamps.view(240, 16).double().cpu() / T
+        stamps.zero_()
+        tr.dq.normal_()
+        tr.V.normal_()
+        tr.backward()
+        torch.cuda.synchronize()
+        bw = stamps.view(240, 16).double().cpu() / T
+    names_f = ["gather", "bar1", "matvec", "bar2", "cell"]
+    names_b = ["gather", "bar1", "cell", "bar2", "matvec", "bar3", "publish"]
+    print(f"precision {prec}")
+    for title, st, names in (("fwd", fw, names_f), ("bwd", bw, names_b)):
+        for role, off in (("thread0 (cell/publish)", 0), ("thread256 (gather)", 8)):
+            m = st[:, off:off + len(names)].mean(0)
+            tot = float(m.sum())
+            print(f"{title} {role}: total {tot:.0f} cyc/step = " +
+                  ", ".join(f"{n} {float(v):.0f}" for n, v in zip(names, m)))
+
+
+if __name__ == "__main__":
+    main()
