@@ -1,14 +1,16 @@
 """Benchmark: mixtures/sec of the full separation training step on MI355X.
 
-Workload (BASELINE.json configs[1]): 2-speaker synthetic
-WSJ0-shaped mixtures, 8 kHz, 4 s (N = 32000 -> T = 251, F = 129), BiLSTM-4L
-(H = 300) mask net, Linear(600 -> 129*50) + tanh, embedding + ADDJUST queries,
-label-ordered MSE + 0.5 sum-to-one loss, backward, (DP all-reduce), Adam --
+Workload (BASELINE.json configs[1] "2-spk PIT BiLSTM magnitude mask bf16, batch=32",
+SURVEY section 8d C2): 2-speaker synthetic WSJ0-shaped mixtures, 8 kHz, 4 s
+(N = 32000 -> T = 251, F = 129), BiLSTM-4L (H = 300) mask net, Linear(600 -> 129*50)
++ tanh, embedding + ADDJUST queries, PIT MSE + 0.5 sum-to-one loss, backward,
+(DP all-reduce), Adam; bf16 GEMM / recurrent-matvec operands with fp32 accumulate,
+fp32 state, loss, gradients and optimizer --
 32 mixtures per GPU per step (weak scaling).  Inputs (raw sources, gains,
 speaker ids) are resident in HBM before the timed region; the step starts at
 preprocessing + STFT.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|bf16]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32] [--mode pit|label]
 
 N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL).
 """
@@ -34,8 +36,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--mode", default="label", choices=["label", "pit"])
+    ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
+    ap.add_argument("--mode", default="pit", choices=["label", "pit"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-batch", type=int, default=2)
@@ -66,7 +68,7 @@ def cpu_baseline(args, N, K):
             feats.append(dsp.magnitude(m))
             Y.append(np.stack([dsp.magnitude(s[k]) for k in range(K)]))
         f = torch.from_numpy(np.array(feats))
-        om.train_step(ref, opt, f, f, torch.from_numpy(np.array(Y)), torch.from_numpy(spk))
+        om.train_step(ref, opt, f, f, torch.from_numpy(np.array(Y)), torch.from_numpy(spk), mode=args.mode)
 
     one_step()  # warm-up
     t0 = time.perf_counter()
@@ -75,7 +77,7 @@ def cpu_baseline(args, N, K):
     dt = time.perf_counter() - t0
     return {"value": args.cpu_batch * args.cpu_steps / dt, "unit": "mixtures/s", "cores": cores, "kind": "port",
             "sample": f"{args.cpu_steps} step(s) of {args.cpu_batch} mixtures (of the B={args.batch} workload), "
-                      "oracle torch-CPU fp32 BiLSTM-4L fwd+bwd+Adam incl. numpy STFT features"}
+                      f"oracle torch-CPU fp32 BiLSTM-4L fwd+{args.mode} loss+bwd+Adam incl. numpy STFT features"}
 
 
 def main():
@@ -200,7 +202,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "fp32" else "bf16",
             "data": "synthetic speech-shaped sources (harmonic stack + AM + noise), seed 1+1000*rank, HBM-resident",
-            "config": {"workload": "C2: 2-spk label-ordered BiLSTM-4L magnitude mask, B=32/GPU, N=32000 (T=251,F=129),"
+            "config": {"workload": f"C2: 2-spk {args.mode} BiLSTM-4L magnitude mask, B=32/GPU, N=32000 (T=251,F=129),"
                                    " full step: mix+STFT+fwd+loss+bwd+allreduce+Adam",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
                        "precision": args.precision, "loss": args.mode},

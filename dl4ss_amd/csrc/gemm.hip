@@ -19,6 +19,7 @@
 // gradients, whose K = B*T is long and whose tile count is small).
 #include "common.h"
 #include <type_traits>
+#include <hip/hip_bf16.h>
 
 namespace {
 
@@ -207,6 +208,224 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int M, int N, int K, const 
     }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 throughput kernel.  128x128x32 tiles, 256 threads (2x2 waves of 64x64,
+// 2x2 v_mfma_f32_32x32x16_bf16 accumulators).  Both operands live in LDS as
+// bf16 [row][k] (k contiguous, row stride 40 elements = 80 B: the 16-lane phases
+// of every ds_read_b128 fragment read hit 16 distinct 4-bank groups), whatever
+// their HBM layout: k-contiguous operands are read as 2 x float4 per 8-k chunk,
+// row-contiguous ones as float4 over 4 rows x 4 k-rows and transposed in
+// registers; fp32 -> bf16 by v_cvt_pk_bf16_f32 (RNE) at the LDS store.
+// Global loads of tile k+1 are in flight during the MFMAs of tile k (register
+// prefetch), LDS is double-buffered: one barrier per k-tile.  Tiles are mapped
+// XCD-major (blockIdx % 8 = XCD): each XCD owns a contiguous N-major range of
+// tiles, so the workgroups sharing an operand panel share an L2.
+// ---------------------------------------------------------------------------
+constexpr int GB_BK = 32, GB_LDK = GB_BK + 8;
+
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  __hip_bfloat162 v = __float22bfloat162_rn(make_float2(a, b));
+  return *reinterpret_cast<unsigned*>(&v);
+}
+
+template <bool KC>
+struct GOperand {
+  float4 v[4];  // 16 fp32 of the next k-tile
+  // KC : chunks c = tid + 256 i (i < 2): row c >> 2, k 8 (c & 3) .. +8  -> v[2i], v[2i+1]
+  // !KC: row group rg = tid & 31 (rows 4 rg..+4), k group kg = tid >> 5 (k 4 kg..+4) -> v[j] = k-row j
+  __device__ __forceinline__ void load(const float* __restrict__ G, long long ld, int r0, int rmax, int k0, int kmax,
+                                       bool vec) {
+    const int t = threadIdx.x;
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = t + 256 * i;
+        const int gr = r0 + (c >> 2), gk = k0 + 8 * (c & 3);
+        const float* p = G + (long long)gr * ld + gk;
+        if (vec && gr < rmax && gk + 8 <= kmax) {
+          v[2 * i] = *reinterpret_cast<const float4*>(p);
+          v[2 * i + 1] = *reinterpret_cast<const float4*>(p + 4);
+        } else {
+          float e[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = (gr < rmax && gk + j < kmax) ? p[j] : 0.0f;
+          v[2 * i] = make_float4(e[0], e[1], e[2], e[3]);
+          v[2 * i + 1] = make_float4(e[4], e[5], e[6], e[7]);
+        }
+      }
+    } else {
+      const int gr = r0 + 4 * (t & 31), gk0 = k0 + 4 * (t >> 5);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int gk = gk0 + j;
+        const float* p = G + (long long)gk * ld + gr;
+        if (vec && gk < kmax && gr + 4 <= rmax) {
+          v[j] = *reinterpret_cast<const float4*>(p);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) e[c] = (gk < kmax && gr + c < rmax) ? p[c] : 0.0f;
+          v[j] = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(unsigned short* __restrict__ s) const {
+    const int t = threadIdx.x;
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = t + 256 * i;
+        uint4 w;
+        w.x = pk_bf16(v[2 * i].x, v[2 * i].y);
+        w.y = pk_bf16(v[2 * i].z, v[2 * i].w);
+        w.z = pk_bf16(v[2 * i + 1].x, v[2 * i + 1].y);
+        w.w = pk_bf16(v[2 * i + 1].z, v[2 * i + 1].w);
+        *reinterpret_cast<uint4*>(s + (c >> 2) * GB_LDK + 8 * (c & 3)) = w;
+      }
+    } else {
+      const int r = 4 * (t & 31), k = 4 * (t >> 5);
+      uint2 w0, w1, w2, w3;  // row r + c: k .. k+3
+      w0.x = pk_bf16(v[0].x, v[1].x); w0.y = pk_bf16(v[2].x, v[3].x);
+      w1.x = pk_bf16(v[0].y, v[1].y); w1.y = pk_bf16(v[2].y, v[3].y);
+      w2.x = pk_bf16(v[0].z, v[1].z); w2.y = pk_bf16(v[2].z, v[3].z);
+      w3.x = pk_bf16(v[0].w, v[1].w); w3.y = pk_bf16(v[2].w, v[3].w);
+      *reinterpret_cast<uint2*>(s + (r + 0) * GB_LDK + k) = w0;
+      *reinterpret_cast<uint2*>(s + (r + 1) * GB_LDK + k) = w1;
+      *reinterpret_cast<uint2*>(s + (r + 2) * GB_LDK + k) = w2;
+      *reinterpret_cast<uint2*>(s + (r + 3) * GB_LDK + k) = w3;
+    }
+  }
+};
+
+template <bool A_KC, bool B_KC, int EPI, bool ATOMIC>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, const float* __restrict__ A,
+                                                          long long lda, const float* __restrict__ B, long long ldb,
+                                                          float* __restrict__ C, long long ldc,
+                                                          const float* __restrict__ bias, float beta,
+                                                          int k_per_split, int grid_m, int grid_n, int vec) {
+  __shared__ __attribute__((aligned(16))) unsigned short sA[2][BM * GB_LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short sB[2][BN * GB_LDK];
+
+  // XCD-major, then grouped: each XCD owns a contiguous range of the grouped tile
+  // order (8 M-tiles x all N-tiles per group, M fastest), so the ~64 workgroups an
+  // XCD runs at once cover an 8 x 8 block of tiles: 16 operand panels in its L2.
+  const int ntiles = grid_m * grid_n;
+  const int per_xcd = (ntiles + 7) / 8;
+  const int tile = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  if (tile >= ntiles) return;
+  constexpr int GROUP = 8;
+  const int gsize = GROUP * grid_n;
+  const int first_m = (tile / gsize) * GROUP;
+  const int gm_here = min(grid_m - first_m, GROUP);
+  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  if (kbeg >= kend) return;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  GOperand<A_KC> oa;
+  GOperand<B_KC> ob;
+  const bool va = vec & 1, vb = vec & 2;
+  oa.load(A, lda, m0, M, kbeg, kend, va);
+  ob.load(B, ldb, n0, N, kbeg, kend, vb);
+  oa.store(sA[0]);
+  ob.store(sB[0]);
+  __syncthreads();
+
+  const int nk = (kend - kbeg + GB_BK - 1) / GB_BK;
+  const int fr = lane & 31, fk = 8 * (lane >> 5);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      oa.load(A, lda, m0, M, kbeg + (kt + 1) * GB_BK, kend, va);
+      ob.load(B, ldb, n0, N, kbeg + (kt + 1) * GB_BK, kend, vb);
+    }
+    const unsigned short* a = sA[cur];
+    const unsigned short* b = sB[cur];
+#pragma unroll
+    for (int kk = 0; kk < GB_BK; kk += 16) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a + (wm + fr) * GB_LDK + kk + fk);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + (wm + 32 + fr) * GB_LDK + kk + fk);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(b + (wn + fr) * GB_LDK + kk + fk);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(b + (wn + 32 + fr) * GB_LDK + kk + fk);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      oa.store(sA[cur ^ 1]);
+      ob.store(sB[cur ^ 1]);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] -> row (r&3) + 8*(r>>2) + 4*(lane>>5), col lane&31
+  const bool add_bias = bias && blockIdx.z == 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + (lane & 31);
+      if (col >= N) continue;
+      const float bv = add_bias ? bias[col] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= M) continue;
+        float v = acc[i][j][r] + bv;
+        float* cp = C + (long long)row * ldc + col;
+        if constexpr (ATOMIC) {
+          atomicAdd(cp, v);
+        } else {
+          if (beta != 0.0f) v += beta * *cp;
+          if (EPI == EPI_TANH) v = tanhf(v);
+          *cp = v;
+        }
+      }
+    }
+}
+
+template <bool A_KC, bool B_KC>
+int launch_bf16(int M, int N, int K, const float* A, long long lda, const float* B, long long ldb, float* C,
+                long long ldc, const float* bias, int epi, float beta, int splitk, hipStream_t st) {
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  if (splitk < 1) splitk = 1;
+  int kps = (K + splitk - 1) / splitk;
+  kps = (kps + GB_BK - 1) / GB_BK * GB_BK;
+  splitk = (K + kps - 1) / kps;
+  const int ntiles = gm * gn;
+  dim3 grid(8 * ((ntiles + 7) / 8), 1, splitk);
+  // 16-B vector loads need 16-B aligned rows (ld % 4 == 0) and base pointers
+  const int vec = ((lda % 4 == 0 && ((uintptr_t)A & 15) == 0) ? 1 : 0) |
+                  ((ldb % 4 == 0 && ((uintptr_t)B & 15) == 0) ? 2 : 0);
+  if (splitk > 1) {
+    if (epi != EPI_NONE || beta != 1.0f) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_bf16_kernel<A_KC, B_KC, EPI_NONE, true>), grid, dim3(NT), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, bias, beta, kps, gm, gn, vec);
+  } else if (epi == EPI_TANH) {
+    hipLaunchKernelGGL((gemm_bf16_kernel<A_KC, B_KC, EPI_TANH, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, bias, beta, kps, gm, gn, vec);
+  } else {
+    hipLaunchKernelGGL((gemm_bf16_kernel<A_KC, B_KC, EPI_NONE, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, bias, beta, kps, gm, gn, vec);
+  }
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
 template <bool A_KC, bool B_KC, int PREC>
 int launch_prec(int M, int N, int K, const float* A, long long lda, const float* B, long long ldb, float* C,
                 long long ldc, const float* bias, int epi, float beta, int splitk, hipStream_t st) {
@@ -237,7 +456,7 @@ template <bool A_KC, bool B_KC>
 int launch(int prec, int M, int N, int K, const float* A, long long lda, const float* B, long long ldb, float* C,
            long long ldc, const float* bias, int epi, float beta, int splitk, hipStream_t st) {
   if (prec == PREC_BF16)
-    return launch_prec<A_KC, B_KC, PREC_BF16>(M, N, K, A, lda, B, ldb, C, ldc, bias, epi, beta, splitk, st);
+    return launch_bf16<A_KC, B_KC>(M, N, K, A, lda, B, ldb, C, ldc, bias, epi, beta, splitk, st);
   return launch_prec<A_KC, B_KC, PREC_F32>(M, N, K, A, lda, B, ldb, C, ldc, bias, epi, beta, splitk, st);
 }
 

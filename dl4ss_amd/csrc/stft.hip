@@ -87,20 +87,64 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   return i;
 }
 
+// Copy n floats LDS -> global with 16-B stores for the aligned body (the tile of
+// 16 consecutive frames is one contiguous range of the (sig, t, bin) output).
+__device__ __forceinline__ void store_tile(float* __restrict__ dst, const float* src, int n, int tid) {
+  const int h = min((int)(((16 - ((uintptr_t)dst & 15)) & 15) >> 2), n);  // floats before 16-B alignment
+  if (tid < h) dst[tid] = src[tid];
+  const int nv = (n - h) >> 2;
+  float4* d4 = reinterpret_cast<float4*>(dst + h);
+  const float* s = src + h;
+  for (int i = tid; i < nv; i += 256) d4[i] = make_float4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
+  const int t0 = h + 4 * nv;
+  if (tid < n - t0) dst[t0 + tid] = src[t0 + tid];
+}
+
+// Span of tile `tile` into registers: thread owns span[4 (tid + 256 r) .. +3], r < 3.
+// Interior tiles: one 16-B load per piece; the two edge tiles of a signal resolve
+// the reflect padding per sample.
+struct SpanRegs {
+  float4 v[3];
+};
+__device__ __forceinline__ void load_span(const float* __restrict__ x, int n_samples, int frames_tiles, long long tile,
+                                          int tid, SpanRegs& r) {
+  const long long sig = tile / frames_tiles;
+  const int t0 = (int)(tile % frames_tiles) * FPW;
+  const float* xs = x + sig * (long long)n_samples;
+  const int base = HOPL * t0 - NFFT / 2;  // x index of span[0]
+  const bool fast = base >= 0 && base + SPAN <= n_samples && ((((uintptr_t)(xs + base)) & 15) == 0);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int i = 4 * (tid + 256 * q);
+    if (i < SPAN) {
+      if (fast) {
+        r.v[q] = __ldg(reinterpret_cast<const float4*>(xs + base + i));
+      } else {
+        float e[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int xi = base + i + c;
+          e[c] = (xi > -n_samples && xi < 2 * n_samples - 1) ? __ldg(xs + reflect_idx(xi, n_samples)) : 0.0f;
+        }
+        r.v[q] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  }
+}
+
+// One workgroup loops over tiles (16 consecutive frames of one signal) in grid
+// stride; the next tile's span is loaded into registers while the current one is
+// transformed, so HBM latency hides behind the DFT even at 3 workgroups per CU.
 __global__ __launch_bounds__(256) void stft_fwd_kernel(const float* __restrict__ x, int n_samples, int T,
-                                                       int frames_tiles, int flags, float2* __restrict__ Xc,
-                                                       float* __restrict__ mag) {
-  __shared__ float sx[SPAN];
+                                                       int frames_tiles, long long n_tiles, int flags,
+                                                       float* __restrict__ Xc, float* __restrict__ mag) {
+  __shared__ __attribute__((aligned(16))) float sx[SPAN];
   __shared__ float sw[NFFT];
   __shared__ float2 stw[NFFT];
-  __shared__ float2 sy[FPW][16 * YS];
+  __shared__ __attribute__((aligned(16))) float2 sy[FPW][16 * YS];  // transpose; then the output tile
 
   const int tid = threadIdx.x;
-  const long long sig = blockIdx.x / frames_tiles;
-  const int t0 = (blockIdx.x % frames_tiles) * FPW;
-  const float* xs = x + sig * (long long)n_samples;
-
-  // window + twiddles (LDS-resident, accurate)
+  // window + twiddles (LDS-resident, accurate), once per workgroup
   {
     float s, c;
     sincospif((float)tid / 128.0f, &s, &c);
@@ -108,57 +152,68 @@ __global__ __launch_bounds__(256) void stft_fwd_kernel(const float* __restrict__
     const float sh = sinpif((float)tid / 256.0f);
     sw[tid] = sh * sh;  // periodic Hann: 0.5 - 0.5 cos(2 pi n / 256) = sin^2(pi n / 256)
   }
-  // coalesced load of the padded span covering frames [t0, t0+16)
-  const int base = HOPL * t0 - NFFT / 2;  // x index of span[0]
-  for (int i = tid; i < SPAN; i += 256) {
-    const int xi = base + i;
-    float v = 0.0f;
-    if (xi > -n_samples && xi < 2 * n_samples - 1) v = __ldg(xs + reflect_idx(xi, n_samples));
-    sx[i] = v;
-  }
-  __syncthreads();
-
+  long long tile = blockIdx.x;
+  SpanRegs pf;
+  if (tile < n_tiles) load_span(x, n_samples, frames_tiles, tile, tid, pf);
   const int fr = tid >> 4;  // frame within tile
   const int j = tid & 15;
-  const int t = t0 + fr;
-
-  // stage 1: lane j = n2; DFT16 over n1 of xw[16 n1 + j], twiddle W256^{j k1}
-  {
-    float2 v[16], o[16];
-    const float* fx = sx + HOPL * fr;
-#pragma unroll
-    for (int n1 = 0; n1 < 16; ++n1) {
-      const int n = 16 * n1 + j;
-      v[n1] = make_float2(fx[n] * sw[n], 0.0f);
-    }
-    dft16<-1>(v, o);
-#pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) sy[fr][k1 * YS + j] = cmul(o[k1], stw[(j * k1) & 255]);
-  }
-  __syncthreads();
-
-  // stage 2: lane j = k1; DFT16 over n2 -> X[j + 16 k2]
-  float2 v[16], o[16];
-#pragma unroll
-  for (int n2 = 0; n2 < 16; ++n2) v[n2] = sy[fr][j * YS + n2];
-  dft16<-1>(v, o);
-
-  if (t >= T) return;
-  const long long row = (sig * T + t) * (long long)NBIN;
   const bool conj = flags & F_CONJ;
+  float2* tc = reinterpret_cast<float2*>(&sy[0][0]);      // output tile: FPW x NBIN complex
+  float* tm = reinterpret_cast<float*>(tc + FPW * NBIN);  // FPW x NBIN magnitude
+
+  for (; tile < n_tiles; tile += gridDim.x) {
+    __syncthreads();  // previous tile's output staging fully read
 #pragma unroll
-  for (int k2 = 0; k2 < 9; ++k2) {
-    const int k = j + 16 * k2;
-    if (k < NBIN) {
-      float2 X = o[k2];
-      if (conj) X.y = -X.y;
-      if (flags & F_COMPLEX) Xc[row + k] = X;
-      if (flags & (F_MAG | F_LOGMAG)) {
+    for (int q = 0; q < 3; ++q) {
+      const int i = 4 * (tid + 256 * q);
+      if (i < SPAN) *reinterpret_cast<float4*>(sx + i) = pf.v[q];
+    }
+    __syncthreads();
+    const long long next = tile + gridDim.x;
+    if (next < n_tiles) load_span(x, n_samples, frames_tiles, next, tid, pf);  // in flight during the DFT
+
+    // stage 1: lane j = n2; DFT16 over n1 of xw[16 n1 + j], twiddle W256^{j k1}
+    {
+      float2 v[16], o[16];
+      const float* fx = sx + HOPL * fr;
+#pragma unroll
+      for (int n1 = 0; n1 < 16; ++n1) {
+        const int n = 16 * n1 + j;
+        v[n1] = make_float2(fx[n] * sw[n], 0.0f);
+      }
+      dft16<-1>(v, o);
+#pragma unroll
+      for (int k1 = 0; k1 < 16; ++k1) sy[fr][k1 * YS + j] = cmul(o[k1], stw[(j * k1) & 255]);
+    }
+    __syncthreads();
+    // stage 2: lane j = k1; DFT16 over n2 -> X[j + 16 k2]
+    float2 o[16];
+    {
+      float2 v[16];
+#pragma unroll
+      for (int n2 = 0; n2 < 16; ++n2) v[n2] = sy[fr][j * YS + n2];
+      dft16<-1>(v, o);
+    }
+    __syncthreads();  // sy is reused as the output tile below
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) {
+      const int k = j + 16 * k2;
+      if (k < NBIN) {
+        float2 X = o[k2];
+        if (conj) X.y = -X.y;
+        tc[fr * NBIN + k] = X;
         float m = sqrtf(X.x * X.x + X.y * X.y);
         if (flags & F_LOGMAG) m = logf(m + 2.220446049250313e-16f);
-        mag[row + k] = m;
+        tm[fr * NBIN + k] = m;
       }
     }
+    __syncthreads();
+    const long long sig = tile / frames_tiles;
+    const int t0 = (int)(tile % frames_tiles) * FPW;
+    const int nfr = min(FPW, T - t0);
+    const long long row0 = (sig * T + t0) * (long long)NBIN;
+    if (flags & F_COMPLEX) store_tile(Xc + 2 * row0, reinterpret_cast<const float*>(tc), 2 * nfr * NBIN, tid);
+    if (flags & (F_MAG | F_LOGMAG)) store_tile(mag + row0, tm, nfr * NBIN, tid);
   }
 }
 
@@ -257,8 +312,11 @@ DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int
   if (n_sig == 0) return 0;
   const int T = 1 + n_samples / HOPL;
   const int tiles = (T + FPW - 1) / FPW;
-  hipLaunchKernelGGL(stft_fwd_kernel, dim3((unsigned)(n_sig * tiles)), dim3(256), 0, as_stream(stream), x,
-                     n_samples, T, tiles, flags, reinterpret_cast<float2*>(X_c64), mag);
+  // grid-stride launch sized to the resident capacity (3 workgroups per CU: LDS and VGPRs)
+  const long long n_tiles = n_sig * tiles;
+  const long long grid = n_tiles < 256LL * 3 ? n_tiles : 256LL * 3;
+  hipLaunchKernelGGL(stft_fwd_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), x, n_samples, T, tiles,
+                     n_tiles, flags, X_c64, mag);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

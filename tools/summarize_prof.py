@@ -1,0 +1,67 @@
+"""Summarise one tools/prof_round.sh session into profiles/ (tracked).
+
+  python tools/summarize_prof.py gpurun_out/<TAG> <round-tag>
+
+Writes
+  profiles/<round>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<round>_summary.md         per-kernel table (avg us, calls, share) + per-step split
+  profiles/<round>_pmc.json           per-kernel HBM traffic per launch from the two PMC passes:
+                                      FETCH_SIZE x 2 (gfx950 reports half of wide streaming reads,
+                                      MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KB -> bytes
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(")[0] if not name.startswith("void ") else name[5:].split("(")[0]
+
+
+def main(src, tag, out="profiles"):
+    os.makedirs(out, exist_ok=True)
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(out, f"{tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    lines = [f"# {tag}: rocprofv3 --kernel-trace --stats ({src})", "",
+             "| kernel | calls | avg us | min us | max us | share % |", "|---|---|---|---|---|---|"]
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+        lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
+                     f"{float(r['MinNs']) / 1e3:.2f} | {float(r['MaxNs']) / 1e3:.2f} | "
+                     f"{100 * float(r['TotalDurationNs']) / tot:.1f} |")
+    pmc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+        f = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                pmc[short(r["Kernel_Name"])][counter].append(float(r["Counter_Value"]))
+    res = {}
+    for k, d in pmc.items():
+        fetch = [2 * 1024 * v for v in d.get("FETCH_SIZE", [])]
+        write = [1024 * v for v in d.get("WRITE_SIZE", [])]
+        n = min(len(fetch), len(write))
+        if n == 0:
+            continue
+        res[k] = {"dispatches": n, "fetch_bytes_per_launch": fetch[:n], "write_bytes_per_launch": write[:n],
+                  "traffic_bytes_per_launch": [a + b for a, b in zip(fetch[:n], write[:n])],
+                  "avg_traffic_bytes": sum(a + b for a, b in zip(fetch[:n], write[:n])) / n}
+    if res:
+        json.dump({"source": src, "correction": "FETCH_SIZE x2 (gfx950), KB->bytes", "kernels": res},
+                  open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
+        lines += ["", "## HBM traffic per launch (PMC: FETCH_SIZE x2 + WRITE_SIZE)", "",
+                  "| kernel | dispatches | avg MB / launch |", "|---|---|---|"]
+        for k, v in sorted(res.items(), key=lambda kv: -kv[1]["avg_traffic_bytes"]):
+            lines.append(f"| `{k}` | {v['dispatches']} | {v['avg_traffic_bytes'] / 1e6:.2f} |")
+    open(os.path.join(out, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[:40]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
