@@ -209,19 +209,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int M, int N, int K, const 
 }
 
 // ---------------------------------------------------------------------------
-// bf16 throughput kernel.  128x128x32 tiles, 256 threads (2x2 waves of 64x64,
+// bf16 throughput kernel.  128x128x64 tiles, 256 threads (2x2 waves of 64x64,
 // 2x2 v_mfma_f32_32x32x16_bf16 accumulators).  Both operands live in LDS as
-// bf16 [row][k] (k contiguous, row stride 40 elements = 80 B: the 16-lane phases
+// bf16 [row][k] (k contiguous, row stride 72 elements = 144 B: the 16-lane phases
 // of every ds_read_b128 fragment read hit 16 distinct 4-bank groups), whatever
 // their HBM layout: k-contiguous operands are read as 2 x float4 per 8-k chunk,
-// row-contiguous ones as float4 over 4 rows x 4 k-rows and transposed in
+// row-contiguous ones as float4 over 4 rows x 8 k-rows and transposed in
 // registers; fp32 -> bf16 by v_cvt_pk_bf16_f32 (RNE) at the LDS store.
-// Global loads of tile k+1 are in flight during the MFMAs of tile k (register
-// prefetch), LDS is double-buffered: one barrier per k-tile.  Tiles are mapped
+// Global loads of tile k+1 (64 KB per workgroup) are in flight during the MFMAs
+// of tile k (register prefetch into a single LDS buffer, two barriers per tile).  Tiles are mapped
 // XCD-major (blockIdx % 8 = XCD): each XCD owns a contiguous N-major range of
 // tiles, so the workgroups sharing an operand panel share an L2.
 // ---------------------------------------------------------------------------
-constexpr int GB_BK = 32, GB_LDK = GB_BK + 8;
+constexpr int GB_BK = 64, GB_LDK = GB_BK + 8;  // 144-B LDS rows
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   __hip_bfloat162 v = __float22bfloat162_rn(make_float2(a, b));
@@ -230,17 +230,17 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
 
 template <bool KC>
 struct GOperand {
-  float4 v[4];  // 16 fp32 of the next k-tile
-  // KC : chunks c = tid + 256 i (i < 2): row c >> 2, k 8 (c & 3) .. +8  -> v[2i], v[2i+1]
-  // !KC: row group rg = tid & 31 (rows 4 rg..+4), k group kg = tid >> 5 (k 4 kg..+4) -> v[j] = k-row j
+  float4 v[8];  // 32 fp32 of the next 128 x 64 k-tile
+  // KC : chunks c = tid + 256 i (i < 4): row c >> 3, k 8 (c & 7) .. +8  -> v[2i], v[2i+1]
+  // !KC: row group rg = tid & 31 (rows 4 rg..+4), k group kg = tid >> 5 (k 8 kg..+8) -> v[j] = k-row j
   __device__ __forceinline__ void load(const float* __restrict__ G, long long ld, int r0, int rmax, int k0, int kmax,
                                        bool vec) {
     const int t = threadIdx.x;
     if constexpr (KC) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 4; ++i) {
         const int c = t + 256 * i;
-        const int gr = r0 + (c >> 2), gk = k0 + 8 * (c & 3);
+        const int gr = r0 + (c >> 3), gk = k0 + 8 * (c & 7);
         const float* p = G + (long long)gr * ld + gk;
         if (vec && gr < rmax && gk + 8 <= kmax) {
           v[2 * i] = *reinterpret_cast<const float4*>(p);
@@ -254,9 +254,9 @@ struct GOperand {
         }
       }
     } else {
-      const int gr = r0 + 4 * (t & 31), gk0 = k0 + 4 * (t >> 5);
+      const int gr = r0 + 4 * (t & 31), gk0 = k0 + 8 * (t >> 5);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 8; ++j) {
         const int gk = gk0 + j;
         const float* p = G + (long long)gk * ld + gr;
         if (vec && gk < kmax && gr + 4 <= rmax) {
@@ -274,26 +274,25 @@ struct GOperand {
     const int t = threadIdx.x;
     if constexpr (KC) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 4; ++i) {
         const int c = t + 256 * i;
         uint4 w;
         w.x = pk_bf16(v[2 * i].x, v[2 * i].y);
         w.y = pk_bf16(v[2 * i].z, v[2 * i].w);
         w.z = pk_bf16(v[2 * i + 1].x, v[2 * i + 1].y);
         w.w = pk_bf16(v[2 * i + 1].z, v[2 * i + 1].w);
-        *reinterpret_cast<uint4*>(s + (c >> 2) * GB_LDK + 8 * (c & 3)) = w;
+        *reinterpret_cast<uint4*>(s + (c >> 3) * GB_LDK + 8 * (c & 7)) = w;
       }
     } else {
-      const int r = 4 * (t & 31), k = 4 * (t >> 5);
-      uint2 w0, w1, w2, w3;  // row r + c: k .. k+3
-      w0.x = pk_bf16(v[0].x, v[1].x); w0.y = pk_bf16(v[2].x, v[3].x);
-      w1.x = pk_bf16(v[0].y, v[1].y); w1.y = pk_bf16(v[2].y, v[3].y);
-      w2.x = pk_bf16(v[0].z, v[1].z); w2.y = pk_bf16(v[2].z, v[3].z);
-      w3.x = pk_bf16(v[0].w, v[1].w); w3.y = pk_bf16(v[2].w, v[3].w);
-      *reinterpret_cast<uint2*>(s + (r + 0) * GB_LDK + k) = w0;
-      *reinterpret_cast<uint2*>(s + (r + 1) * GB_LDK + k) = w1;
-      *reinterpret_cast<uint2*>(s + (r + 2) * GB_LDK + k) = w2;
-      *reinterpret_cast<uint2*>(s + (r + 3) * GB_LDK + k) = w3;
+      const int r = 4 * (t & 31), k = 8 * (t >> 5);
+      uint4 w[4];  // row r + c: k .. k+7
+#define GB_ROW(c, f)                                                                          \
+  w[c].x = pk_bf16(v[0].f, v[1].f); w[c].y = pk_bf16(v[2].f, v[3].f);                         \
+  w[c].z = pk_bf16(v[4].f, v[5].f); w[c].w = pk_bf16(v[6].f, v[7].f);
+      GB_ROW(0, x) GB_ROW(1, y) GB_ROW(2, z) GB_ROW(3, w)
+#undef GB_ROW
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(s + (r + c) * GB_LDK + k) = w[c];
     }
   }
 };
@@ -304,8 +303,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
                                                           float* __restrict__ C, long long ldc,
                                                           const float* __restrict__ bias, float beta,
                                                           int k_per_split, int grid_m, int grid_n, int vec) {
-  __shared__ __attribute__((aligned(16))) unsigned short sA[2][BM * GB_LDK];
-  __shared__ __attribute__((aligned(16))) unsigned short sB[2][BN * GB_LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short sA[BM * GB_LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short sB[BN * GB_LDK];
 
   // XCD-major, then grouped: each XCD owns a contiguous range of the grouped tile
   // order (8 M-tiles x all N-tiles per group, M fastest), so the ~64 workgroups an
@@ -340,34 +339,29 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
   const bool va = vec & 1, vb = vec & 2;
   oa.load(A, lda, m0, M, kbeg, kend, va);
   ob.load(B, ldb, n0, N, kbeg, kend, vb);
-  oa.store(sA[0]);
-  ob.store(sB[0]);
-  __syncthreads();
 
+  // single LDS buffer, register prefetch: tile k+1's global loads are in flight
+  // during tile k's MFMAs (64 KB per workgroup, 2 workgroups per CU)
   const int nk = (kend - kbeg + GB_BK - 1) / GB_BK;
   const int fr = lane & 31, fk = 8 * (lane >> 5);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    oa.store(sA);
+    ob.store(sB);
+    __syncthreads();
     if (kt + 1 < nk) {
       oa.load(A, lda, m0, M, kbeg + (kt + 1) * GB_BK, kend, va);
       ob.load(B, ldb, n0, N, kbeg + (kt + 1) * GB_BK, kend, vb);
     }
-    const unsigned short* a = sA[cur];
-    const unsigned short* b = sB[cur];
 #pragma unroll
     for (int kk = 0; kk < GB_BK; kk += 16) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a + (wm + fr) * GB_LDK + kk + fk);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + (wm + 32 + fr) * GB_LDK + kk + fk);
-      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(b + (wn + fr) * GB_LDK + kk + fk);
-      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(b + (wn + 32 + fr) * GB_LDK + kk + fk);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(sA + (wm + fr) * GB_LDK + kk + fk);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(sA + (wm + 32 + fr) * GB_LDK + kk + fk);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(sB + (wn + fr) * GB_LDK + kk + fk);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(sB + (wn + 32 + fr) * GB_LDK + kk + fk);
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (kt + 1 < nk) {
-      oa.store(sA[cur ^ 1]);
-      ob.store(sB[cur ^ 1]);
     }
     __syncthreads();
   }

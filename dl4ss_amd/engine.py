@@ -246,10 +246,12 @@ class SepTrainer:
                   _lib.ptr(self.dh_bcast) if net.adjust else None, st)
         dPre = self.V
         hL = self.out[-1].view(BT, 2 * H)
-        ops.gemm(dPre, hL, transA=True, out=net.view("mix.Linear.weight", g), precision=self.precision)
+        # grads were zeroed above: weight gradients accumulate (beta 1) with split-K
+        ops.gemm(dPre, hL, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto",
+                 precision=self.precision)
         ops.colsum(dPre, net.view("mix.Linear.bias", g))
         dH = self.dH[0]
-        ops.gemm(dPre, net.view("mix.Linear.weight"), out=dH, precision=self.precision)
+        ops.gemm(dPre, net.view("mix.Linear.weight"), out=dH, splitk="auto", precision=self.precision)
         for l in range(net.L - 1, -1, -1):
             dG = self.G
             dGh = self.dGh if self.dGh is not None else dG
@@ -260,18 +262,18 @@ class SepTrainer:
                       _lib.ptr(self.dGh) if self.dGh is not None else None, _lib.ptr(self.rnn_ws), self.ws_bytes,
                       _lib.ptr(self.status), st)
             xl = self.mag_mix.view(BT, -1) if l == 0 else self.out[l - 1].view(BT, 2 * H)
-            ops.gemm(dG, xl, transA=True, out=net.cat_view("weight_ih", l, g), splitk=4, beta=1.0,
+            ops.gemm(dG, xl, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0,
                      precision=self.precision)
             ops.colsum(dG, net.cat_view("bias_ih", l, g))
             whh_g = net.cat_view("weight_hh", l, g)
             hp = self.hprev[l].view(BT, 2 * H)
             for d in range(2):
                 ops.gemm(dGh[:, d * NGH:(d + 1) * NGH], hp[:, d * H:(d + 1) * H], transA=True,
-                         out=whh_g[d * NGH:(d + 1) * NGH], splitk=4, beta=1.0, precision=self.precision)
+                         out=whh_g[d * NGH:(d + 1) * NGH], splitk="auto", beta=1.0, precision=self.precision)
             ops.colsum(dGh, net.cat_view("bias_hh", l, g))
             if l > 0:
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
-                ops.gemm(dG, net.cat_view("weight_ih", l), out=dH_next, precision=self.precision)
+                ops.gemm(dG, net.cat_view("weight_ih", l), out=dH_next, splitk="auto", precision=self.precision)
                 dH = dH_next
 
     def allreduce(self):

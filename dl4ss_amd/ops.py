@@ -93,11 +93,21 @@ def _mat(t, name):
     return t
 
 
+def auto_splitk(M, N, K, target_wgs=1024, min_k=512):
+    """Split-K factor that gives a short-and-wide GEMM ~target_wgs workgroups (128 x 128
+    tiles) while keeping >= min_k of K per split."""
+    tiles = -(-M // 128) * -(-N // 128)
+    s = max(1, min(-(-target_wgs // tiles), K // min_k))
+    return int(s)
+
+
 def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.0, out=None, precision="fp32",
          splitk=1):
     """out = op(A) @ op(B) (+ bias) (tanh) (+ beta*out).  op(A) = A.T if transA.
 
     A is stored (M, K) or (K, M) if transA; B is stored (K, N) or (N, K) if transB.
+    splitk="auto": split K over workgroups (fp32 atomics) when the tile grid is small
+    (needs epilogue none; a beta = 0 output is zeroed first).
     """
     _mat(A, "gemm(A)")
     _mat(B, "gemm(B)")
@@ -114,6 +124,13 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
         raise RuntimeError(f"gemm: out shape {tuple(out.shape)} != {(M, N)}")
     if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
         raise RuntimeError("gemm: bias must be contiguous with N elements")
+    if splitk == "auto":
+        splitk = auto_splitk(M, N, K) if epilogue == EPI_NONE else 1
+        if splitk > 1 and beta == 0.0:
+            out.zero_()
+            beta = 1.0
+        elif splitk > 1 and beta != 1.0:
+            splitk = 1
     _lib.call("dl4ss_gemm", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0), _lib.ptr(B, True), B.stride(0),
               _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue, float(beta), PREC[precision], int(splitk),
               _lib.stream_ptr())

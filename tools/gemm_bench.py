@@ -35,8 +35,8 @@ def main():
         B = torch.randn(*((N, K) if tb else (K, N)), device=dev)
         C = torch.zeros(M, N, device=dev)
         bias = torch.randn(N, device=dev) if not ta else None
-        kw = dict(transA=ta, transB=tb, out=C, precision=prec, splitk=sk, bias=bias if sk == 1 else None,
-                  epilogue=epi, beta=1.0 if sk > 1 else 0.0)
+        sk = "auto" if epi == 0 else 1
+        kw = dict(transA=ta, transB=tb, out=C, precision=prec, splitk=sk, bias=None, epilogue=epi, beta=0.0)
         for _ in range(3):
             ops.gemm(A, B, **kw)
         torch.cuda.synchronize()
@@ -50,7 +50,8 @@ def main():
         ms = s.elapsed_time(e) / it
         tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12
         total_ms += ms
-        print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "splitk": sk, "us": round(ms * 1e3, 1),
+        print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "splitk": ops.auto_splitk(M, N, K) if sk == "auto" else 1,
+                          "us": round(ms * 1e3, 1),
                           "TFLOP/s": round(tf, 1)}), flush=True)
     print(json.dumps({"precision": prec, "sum_us_one_each": round(total_ms * 1e3, 1)}))
 
