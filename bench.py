@@ -99,9 +99,9 @@ def main():
     B, K, N = args.batch, 2, 32000
     net = engine.SepNet(cell="lstm", num_layers=4, hidden=300, emb=50, num_labels=101, device=dev, seed=1)
     if world > 1:  # identical initial weights on every rank
-        import torch.distributed as dist
+        from dl4ss_amd import dp
 
-        dist.broadcast(net.flat, 0)
+        dp.broadcast_params_(net.flat, pg)
     tr = engine.SepTrainer(net, B, K, N, mode=args.mode, precision=args.precision, process_group=pg)
 
     # synthetic input pool, resident in HBM (seed 1 + 1000 * rank)
@@ -157,11 +157,9 @@ def main():
     elapsed = time.perf_counter() - t0
     tr.check()
     if world > 1:
-        import torch.distributed as dist
+        from dl4ss_amd import dp
 
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = dp.max_over_ranks(elapsed, dev, pg)
     loss_v = float(loss[0].item())
     if not np.isfinite(loss_v):
         raise RuntimeError("non-finite loss")

@@ -313,32 +313,53 @@ __global__ void pit_select_kernel(const float* __restrict__ part, int B, int nbl
 
 // loss = s1 * sum_b sum_k C[b][k][perm k] + s2 * S ; also dq = sum_blk part_dq (fixed order)
 template <int K>
-__global__ void finalize_kernel(const float* __restrict__ part, int B, int nblk, const int* __restrict__ perm,
-                                float s1, float s2, float* __restrict__ loss_out, const float* __restrict__ part_dq,
-                                int qw, float* __restrict__ dq) {
-  // block 0: loss (single thread, fixed order) ; other threads: dq
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid == 0) {
+__global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int B, int nblk,
+                                                       const int* __restrict__ perm, float s1, float s2,
+                                                       float* __restrict__ loss_out,
+                                                       const float* __restrict__ part_dq, int qw,
+                                                       float* __restrict__ dq) {
+  // block 0: loss, 256 fixed-stride fp64 partial sums + fixed-order tree (deterministic)
+  if (blockIdx.x == 0) {
+    __shared__ double r1[256], r2[256];
     double l1 = 0.0, l2 = 0.0;
-    for (int b = 0; b < B; ++b) {
-      for (int blk = 0; blk < nblk; ++blk) {
-        const float* p = part + ((long long)b * nblk + blk) * (K * K + 1);
+    for (int i = threadIdx.x; i < B * nblk; i += 256) {
+      const int b = i / nblk;
+      const float* p = part + (long long)i * (K * K + 1);
 #pragma unroll
-        for (int k = 0; k < K; ++k) l1 += p[k * K + (perm ? perm[b * K + k] : k)];
-        l2 += p[K * K];
-      }
+      for (int k = 0; k < K; ++k) l1 += p[k * K + (perm ? perm[b * K + k] : k)];
+      l2 += p[K * K];
     }
-    loss_out[0] = (float)(s1 * l1 + s2 * l2);
-    loss_out[1] = (float)(s1 * l1);
-    loss_out[2] = (float)(s2 * l2);
+    r1[threadIdx.x] = l1;
+    r2[threadIdx.x] = l2;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) {
+        r1[threadIdx.x] += r1[threadIdx.x + w];
+        r2[threadIdx.x] += r2[threadIdx.x + w];
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      loss_out[0] = (float)(s1 * r1[0] + s2 * r2[0]);
+      loss_out[1] = (float)(s1 * r1[0]);
+      loss_out[2] = (float)(s2 * r2[0]);
+    }
+    return;
   }
+  // blocks 1..: dq = sum over the utterance's blocks, fixed order
   if (dq) {
     const int n = B * K * qw;
-    for (int i = tid; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x; i < n; i += (gridDim.x - 1) * blockDim.x) {
       const int b = i / (K * qw), j = i % (K * qw);
-      float s = 0.f;
-      for (int blk = 0; blk < nblk; ++blk) s += part_dq[((long long)b * nblk + blk) * K * qw + j];
-      dq[i] = s;
+      const float* pd = part_dq + (long long)b * nblk * K * qw + j;
+      float a0 = 0.f, a1 = 0.f;
+      int blk = 0;
+      for (; blk + 1 < nblk; blk += 2) {
+        a0 += pd[(long long)blk * K * qw];
+        a1 += pd[(long long)(blk + 1) * K * qw];
+      }
+      if (blk < nblk) a0 += pd[(long long)blk * K * qw];
+      dq[i] = a0 + a1;
     }
   }
 }
@@ -410,7 +431,7 @@ DL4SS_API int dl4ss_loss_finalize(const float* part_loss, int B, int K, int nblk
                                   void* stream) {
   DL4SS_REQUIRE(part_loss && loss_out && B > 0 && K >= 1 && K <= 3);
   hipStream_t st = as_stream(stream);
-  dim3 grid(cdiv((long long)B * K * (qw > 0 ? qw : 1), 256)), blk(256);
+  dim3 grid(1 + (dq ? cdiv((long long)B * K * (qw > 0 ? qw : 1), 256) : 0)), blk(256);
   if (K == 1) hipLaunchKernelGGL(finalize_kernel<1>, grid, blk, 0, st, part_loss, B, nblk, perm, s1, s2, loss_out, part_dq, qw, dq);
   if (K == 2) hipLaunchKernelGGL(finalize_kernel<2>, grid, blk, 0, st, part_loss, B, nblk, perm, s1, s2, loss_out, part_dq, qw, dq);
   if (K == 3) hipLaunchKernelGGL(finalize_kernel<3>, grid, blk, 0, st, part_loss, B, nblk, perm, s1, s2, loss_out, part_dq, qw, dq);

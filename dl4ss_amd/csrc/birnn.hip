@@ -595,6 +595,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
       if (col < BC) *reinterpret_cast<f32x4*>(wsc + col * WSPAN + t * 16 + 4 * (lane >> 4)) = acc;
     }
     __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+    STAMP(4)
     // coalesced publish of this wave's contiguous unit span (granules, tag s+1)
     u64* dst = xg + (long long)(s & 1) * NG * BC * H + (long long)w * BC * H;
 #pragma unroll

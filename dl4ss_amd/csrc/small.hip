@@ -10,22 +10,45 @@ namespace {
 //   ADDJUST: EvalVer.py:373-375 and 606-608 (q <- q + adjust(h, q)), no bias
 // one workgroup per utterance: mean over T of h (B,T,D) then K tiny matvecs
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void query_fwd_kernel(const float* __restrict__ h, int T, int D,
+// mean_t h[b, :, c]: block = 64 columns x 4 time phases, grid (B, ceil(D/64));
+// each thread keeps 4 independent loads in flight, phases combined in fixed order
+__global__ __launch_bounds__(256) void time_mean_kernel(const float* __restrict__ h, int T, int D,
+                                                        float* __restrict__ mean_out) {
+  __shared__ float sp[4][64];
+  const int b = blockIdx.x;
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;
+  const float* hb = h + (long long)b * T * D + c;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < D) {
+    int t = ph;
+    for (; t + 12 < T; t += 16) {
+      s0 += hb[(long long)t * D];
+      s1 += hb[(long long)(t + 4) * D];
+      s2 += hb[(long long)(t + 8) * D];
+      s3 += hb[(long long)(t + 12) * D];
+    }
+    for (; t < T; t += 4) s0 += hb[(long long)t * D];
+  }
+  sp[ph][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ph == 0 && c < D) {
+    const int l = threadIdx.x;
+    mean_out[(long long)b * D + c] = ((sp[0][l] + sp[1][l]) + (sp[2][l] + sp[3][l])) / (float)T;
+  }
+}
+
+// one workgroup per utterance: K*W outputs, each a (D + W)-long dot product
+__global__ __launch_bounds__(256) void query_fwd_kernel(const float* __restrict__ mean, int D,
                                                         const int* __restrict__ idx, const float* __restrict__ emb,
                                                         const float* __restrict__ wadj, int K, int W,
-                                                        float* __restrict__ q, float* __restrict__ mean_out) {
+                                                        float* __restrict__ q) {
   extern __shared__ float sm[];
   float* smean = sm;       // [D]
   float* se = sm + D;      // [K][W]
   const int b = blockIdx.x;
-  const float* hb = h + (long long)b * T * D;
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float s = 0.f;
-    for (int t = 0; t < T; ++t) s += hb[(long long)t * D + c];
-    const float m = s / (float)T;
-    smean[c] = m;
-    if (mean_out) mean_out[(long long)b * D + c] = m;
-  }
+  if (wadj)
+    for (int c = threadIdx.x; c < D; c += blockDim.x) smean[c] = mean[(long long)b * D + c];
   for (int i = threadIdx.x; i < K * W; i += blockDim.x) {
     const int k = i / W, o = i % W;
     se[i] = emb[(long long)idx[b * K + k] * W + o];
@@ -36,10 +59,15 @@ __global__ __launch_bounds__(256) void query_fwd_kernel(const float* __restrict_
     float v = se[i];
     if (wadj) {
       const float* wr = wadj + (long long)o * (D + W);
-      float acc = 0.f;
-      for (int c = 0; c < D; ++c) acc = fmaf(wr[c], smean[c], acc);
-      for (int c = 0; c < W; ++c) acc = fmaf(wr[D + c], se[k * W + c], acc);
-      v += acc;
+      float a0 = 0.f, a1 = 0.f;
+      int c = 0;
+      for (; c + 1 < D; c += 2) {
+        a0 = fmaf(wr[c], smean[c], a0);
+        a1 = fmaf(wr[c + 1], smean[c + 1], a1);
+      }
+      for (; c < D; ++c) a0 = fmaf(wr[c], smean[c], a0);
+      for (c = 0; c < W; ++c) a1 = fmaf(wr[D + c], se[k * W + c], a1);
+      v += a0 + a1;
     }
     q[((long long)b * K + k) * W + o] = v;
   }
@@ -144,9 +172,14 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 DL4SS_API int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* idx, const float* emb,
                               const float* w_adj, int K, int W, float* q, float* mean_out, void* stream) {
   DL4SS_REQUIRE(h && idx && emb && q && B > 0 && T > 0 && D > 0 && K > 0 && W > 0);
+  DL4SS_REQUIRE(!w_adj || mean_out);  // ADJUST needs the time mean (also saved for the backward)
+  hipStream_t st = as_stream(stream);
+  if (mean_out) {
+    hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(256), 0, st, h, T, D, mean_out);
+    DL4SS_CHECK_LAUNCH();
+  }
   const size_t smem = sizeof(float) * (D + K * W);
-  hipLaunchKernelGGL(query_fwd_kernel, dim3(B), dim3(256), smem, as_stream(stream), h, T, D, idx, emb, w_adj, K, W,
-                     q, mean_out);
+  hipLaunchKernelGGL(query_fwd_kernel, dim3(B), dim3(256), smem, st, mean_out, D, idx, emb, w_adj, K, W, q);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,40 @@
+"""Data-parallel host logic: one process per GPU, the utterance
+batch sharded across ranks, one flat-gradient all-reduce per step.
+
+Kept free of HIP calls so the multi-rank behaviour is testable with the ``gloo``
+backend on CPU (``tests/test_dp_cpu.py``); on the GPU box the same calls run over
+RCCL (backend ``nccl``) on the device buffers.
+"""
+import torch
+import torch.distributed as dist
+
+
+def world(pg=None):
+    return dist.get_world_size(pg) if dist.is_available() and dist.is_initialized() else 1
+
+
+def broadcast_params_(flat, pg=None, src=0):
+    """Identical initial weights on every rank (rank `src`'s)."""
+    if world(pg) > 1:
+        dist.broadcast(flat, src, group=pg)
+    return flat
+
+
+def allreduce_mean_(flat, pg=None):
+    """grad <- mean over ranks of the per-rank grads.  Every rank's loss is a mean
+    over its own equal-sized shard, so the mean of the per-rank gradients is the
+    gradient of the global-batch mean loss (the single-GPU reference's objective)."""
+    n = world(pg)
+    if n > 1:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=pg)
+        flat.mul_(1.0 / n)
+    return flat
+
+
+def max_over_ranks(value, device, pg=None):
+    """Max of a host float over ranks (bench timing: the slowest rank's time)."""
+    if world(pg) == 1:
+        return float(value)
+    t = torch.tensor([float(value)], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=pg)
+    return float(t.item())

@@ -277,12 +277,12 @@ class SepTrainer:
                 dH = dH_next
 
     def allreduce(self):
+        """One RCCL all-reduce of the flat gradient buffer (mean over ranks)."""
         if self.pg is None:
             return
-        import torch.distributed as dist
+        from . import dp
 
-        dist.all_reduce(self.net.grad, op=dist.ReduceOp.SUM, group=self.pg)
-        self.net.grad.mul_(1.0 / dist.get_world_size(self.pg))
+        dp.allreduce_mean_(self.net.grad, self.pg)
 
     def optimizer_step(self):
         self.step_count += 1

@@ -1,0 +1,115 @@
+"""Multi-rank data parallelism on CPU (gloo, world_size 2): the same host calls the
+GPU path makes over RCCL (dl4ss_amd.dp), checked against a single-process run of
+the oracle step on the global batch.
+
+Rank r generates its own synthetic shard (seed 1 + 1000 r, as bench.py), computes
+the oracle loss / gradients on it, all-reduces the flat gradient (mean) and takes
+an Adam step; the result must equal the single-process step on the concatenated
+global batch (the reference's objective: MSE means over the whole batch)."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dl4ss_amd import dp, synth
+from oracle import dsp, model as om
+
+N = 2000
+K = 2
+B_PER_RANK = 2
+
+
+def _features(src, gains):
+    feats, Y = [], []
+    for b in range(src.shape[0]):
+        srcs = [dsp.normalise_source(src[b, k].astype(np.float32), N) for k in range(K)]
+        s, m = dsp.mix_sources(srcs, gains[b])
+        feats.append(np.abs(dsp.stft_tf(m)))
+        Y.append(np.stack([np.abs(dsp.stft_tf(s[k])) for k in range(K)]))
+    return torch.from_numpy(np.array(feats, np.float32)), torch.from_numpy(np.array(Y, np.float32))
+
+
+def _shard(rank):
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1, rank=rank)
+    src, spk, u = gen.batch(B_PER_RANK)
+    f, Y = _features(src, synth.gains_for(u, K))
+    return f, Y, torch.from_numpy(spk)
+
+
+def _model():
+    torch.manual_seed(0)
+    return om.SepModel(cell="gru", num_layers=1, hidden=32, emb=8)
+
+
+def _flat_grads(model):
+    return torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    model = _model()
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    if rank == 1:
+        flat.add_(1.0)  # diverged init: broadcast must restore rank 0's weights
+    dp.broadcast_params_(flat)
+    off = 0
+    with torch.no_grad():
+        for p in model.parameters():
+            p.copy_(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+    f, Y, spk = _shard(rank)
+    opt = om.make_adam(model)
+    opt.zero_grad()
+    mask, _, _, _ = model(f, spk)
+    loss, _ = om.loss_label_ordered(mask, f, Y)
+    loss.backward()
+    g = dp.allreduce_mean_(_flat_grads(model))
+    off = 0
+    for p in model.parameters():
+        p.grad.copy_(g[off:off + p.numel()].view_as(p))
+        off += p.numel()
+    opt.step()
+    tmax = dp.max_over_ranks(float(rank + 1), "cpu")
+    out[rank] = (g.clone(), torch.cat([p.detach().reshape(-1) for p in model.parameters()]), tmax)
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_dp_two_ranks_equals_global_batch():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    # single-process reference on the global batch (rank shards concatenated)
+    shards = [_shard(r) for r in range(world)]
+    f = torch.cat([s[0] for s in shards])
+    Y = torch.cat([s[1] for s in shards])
+    spk = torch.cat([s[2] for s in shards])
+    model = _model()
+    opt = om.make_adam(model)
+    opt.zero_grad()
+    mask, _, _, _ = model(f, spk)
+    loss, _ = om.loss_label_ordered(mask, f, Y)
+    loss.backward()
+    g_ref = _flat_grads(model)
+    opt.step()
+    p_ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    for r in range(world):
+        g, p, tmax = out[r]
+        assert torch.allclose(g, g_ref, rtol=1e-4, atol=1e-7), (g - g_ref).abs().max()
+        assert torch.allclose(p, p_ref, rtol=1e-5, atol=1e-7)
+        assert tmax == 2.0
+    # the two ranks' synthetic shards are different utterances
+    assert not torch.equal(shards[0][0], shards[1][0])

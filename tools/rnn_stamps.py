@@ -56,7 +56,7 @@ def main():
         torch.cuda.synchronize()
         bw = stamps.view(240, 16).double().cpu() / T
     names_f = ["gather", "bar1", "matvec", "bar2", "cell"]
-    names_b = ["gather", "bar1", "cell", "bar2", "matvec", "bar3", "publish"]
+    names_b = ["gather", "bar1", "cell", "bar2", "matvec/mfma", "bar3", "publish"]
     print(f"precision {prec}")
     for title, st, names in (("fwd", fw, names_f), ("bwd", bw, names_b)):
         for role, off in (("thread0 (cell/publish)", 0), ("thread256 (gather)", 8)):
