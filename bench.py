@@ -30,6 +30,41 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
+PMC_FILE = "profiles/r01_pmc.json"
+
+
+def stft_grid_threads(n_sig, T):
+    """Launch grid (threads) of dl4ss_stft_fwd: 32-frame tiles, capped at 3 workgroups
+    per CU (stft.hip)."""
+    tiles = n_sig * ((T + 31) // 32)
+    return min(tiles, 256 * 3) * 256
+
+
+def stft_grids(B, K, T):
+    return [stft_grid_threads(B, T), stft_grid_threads(B * K, T)]
+
+
+def pmc_traffic(kernel, grids):
+    """HBM bytes of one measured unit (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected) from
+    the committed rocprofv3 PMC passes of this same bench command (tools/prof_round.sh +
+    tools/summarize_prof.py): the sum over `grids` (launch grid sizes in threads that
+    make up the unit) of the average traffic of the launches with that grid; None if
+    the summary is absent."""
+    path = os.path.join(ROOT, PMC_FILE)
+    try:
+        with open(path) as f:
+            launches = json.load(f)["kernels"][kernel]["launches"]
+    except (OSError, KeyError, ValueError):
+        return None
+    total = 0.0
+    for g in grids:
+        v = [l["traffic"] for l in launches if l["grid"] == g]
+        if not v:
+            return None
+        total += sum(v) / len(v)
+    return total
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -39,8 +74,9 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--mode", default="pit", choices=["label", "pit"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=1)
-    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--no-stft-standalone", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=24)
+    ap.add_argument("--cpu-batch", type=int, default=8)
     return ap.parse_args()
 
 
@@ -182,6 +218,31 @@ def main():
     torch.cuda.synchronize()
     gemm_ms = g0.elapsed_time(g1) / 20
     gemm_flops = 2.0 * B * T * 600 * 2400
+    # standalone STFT at the north-star measurement size (>= 2048 signals, ~1 GB of
+    # traffic per launch, complex + magnitude outputs): the >= 50 % HBM target
+    sa = None
+    if not args.no_stft_standalone:
+        n_sa = 2048
+        xs = torch.randn(n_sa, N, device=dev)
+        Xs = torch.empty(n_sa, T, F, 2, device=dev)
+        Ms = torch.empty(n_sa, T, F, device=dev)
+        for _ in range(3):
+            ops.stft(xs, out_c=Xs, out_mag=Ms)
+        h0, h1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        h0.record()
+        for _ in range(10):
+            ops.stft(xs, out_c=Xs, out_mag=Ms)
+        h1.record()
+        torch.cuda.synchronize()
+        sa_ms = h0.elapsed_time(h1) / 10
+        sa_bytes = n_sa * (4 * N + 12 * T * F)
+        sa_gbs = sa_bytes / (sa_ms * 1e-3) / 1e9
+        sa = {"bound": "hbm", "kernel": "stft_fwd (one launch: 2048 signals x N=32000, complex + magnitude; "
+                                        "the north-star STFT roofline measurement)",
+              "achieved": sa_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sa_gbs / HBM_PEAK_GBS,
+              "traffic": pmc_traffic("stft_fwd_kernel", [stft_grid_threads(n_sa, T)]),
+              "traffic_source": PMC_FILE, "launch_ms": sa_ms, "algorithmic_bytes": sa_bytes}
+        del xs, Xs, Ms
 
     if rank == 0:
         value = B * world * args.steps / elapsed
@@ -205,9 +266,13 @@ def main():
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
                        "precision": args.precision, "loss": args.mode},
             "loss": loss_v,
-            "roofline": {"bound": "hbm", "kernel": "stft_fwd (2 launches/step: 32 mixtures + 64 sources, mag)", "achieved": stft_gbs,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": stft_gbs / HBM_PEAK_GBS, "traffic": None,
-                         "launch_ms": stft_ms, "algorithmic_bytes": stft_bytes},
+            "roofline": sa,
+            "roofline_instep": {"bound": "hbm", "kernel": "stft_fwd in-step (2 launches/step: 32 mixtures + 64 "
+                                                         "sources, magnitude)",
+                                "achieved": stft_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": stft_gbs / HBM_PEAK_GBS,
+                                "traffic": pmc_traffic("stft_fwd_kernel", stft_grids(B, K, T)),
+                                "traffic_source": PMC_FILE, "launch_ms": stft_ms, "algorithmic_bytes": stft_bytes},
             "roofline_mfma": {"bound": "mfma", "kernel": "gemm (BiLSTM input projection 8032x2400x600)",
                               "achieved": gemm_tf, "peak": MFMA_PEAK[args.precision], "unit": "TFLOP/s",
                               "frac": gemm_tf / MFMA_PEAK[args.precision], "launch_ms": gemm_ms},

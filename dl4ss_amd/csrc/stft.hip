@@ -87,43 +87,43 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   return i;
 }
 
-// Copy n floats LDS -> global with 16-B stores for the aligned body (the tile of
-// 16 consecutive frames is one contiguous range of the (sig, t, bin) output).
-__device__ __forceinline__ void store_tile(float* __restrict__ dst, const float* src, int n, int tid) {
-  const int h = min((int)(((16 - ((uintptr_t)dst & 15)) & 15) >> 2), n);  // floats before 16-B alignment
-  if (tid < h) dst[tid] = src[tid];
-  const int nv = (n - h) >> 2;
-  float4* d4 = reinterpret_cast<float4*>(dst + h);
-  const float* s = src + h;
-  for (int i = tid; i < nv; i += 256) d4[i] = make_float4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
-  const int t0 = h + 4 * nv;
-  if (tid < n - t0) dst[t0 + tid] = src[t0 + tid];
-}
+// ---------------------------------------------------------------------------
+// Forward STFT.  A tile is FPT = 32 consecutive frames of one signal.  Frames are
+// transformed in pairs: z = w.x_a + i w.x_b is one complex 256-point DFT and
+//   X_a[k] = (Z[k] + conj Z[256-k]) / 2,   X_b[k] = (Z[k] - conj Z[256-k]) / 2i,
+// which halves the DFT work of real input.  16 lanes per pair run the 16 x 16
+// Cooley-Tukey (two in-register radix-4x4 DFT16 + one LDS transpose); Z is then
+// staged in LDS and every thread emits consecutive output bins of the tile (the
+// tile is one contiguous range of the (signal, frame, bin) layout), so complex
+// and magnitude stores are fully coalesced.  One workgroup walks tiles in grid
+// stride with the next span's 16-B loads in flight during the current DFT.
+// ---------------------------------------------------------------------------
+constexpr int FPT = 32;                  // frames per tile
+constexpr int SPAN2 = HOPL * FPT + NFFT;  // 4352 samples
+constexpr int SPAN2_Q = SPAN2 / 4;        // 1088 float4
+constexpr int PFQ = (SPAN2_Q + 255) / 256;  // float4 per thread (5)
 
-// Span of tile `tile` into registers: thread owns span[4 (tid + 256 r) .. +3], r < 3.
-// Interior tiles: one 16-B load per piece; the two edge tiles of a signal resolve
-// the reflect padding per sample.
 struct SpanRegs {
-  float4 v[3];
+  float4 v[PFQ];
 };
-__device__ __forceinline__ void load_span(const float* __restrict__ x, int n_samples, int frames_tiles, long long tile,
+__device__ __forceinline__ void load_span(const float* __restrict__ x, int n_samples, int tiles_per_sig, int tile,
                                           int tid, SpanRegs& r) {
-  const long long sig = tile / frames_tiles;
-  const int t0 = (int)(tile % frames_tiles) * FPW;
-  const float* xs = x + sig * (long long)n_samples;
+  const int sig = tile / tiles_per_sig;
+  const int t0 = (tile - sig * tiles_per_sig) * FPT;
+  const float* xs = x + (long long)sig * n_samples;
   const int base = HOPL * t0 - NFFT / 2;  // x index of span[0]
-  const bool fast = base >= 0 && base + SPAN <= n_samples && ((((uintptr_t)(xs + base)) & 15) == 0);
+  const bool fast = base >= 0 && base + SPAN2 <= n_samples && ((((uintptr_t)(xs + base)) & 15) == 0);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int i = 4 * (tid + 256 * q);
-    if (i < SPAN) {
+  for (int q = 0; q < PFQ; ++q) {
+    const int i4 = tid + 256 * q;
+    if (i4 < SPAN2_Q) {
       if (fast) {
-        r.v[q] = __ldg(reinterpret_cast<const float4*>(xs + base + i));
+        r.v[q] = __ldg(reinterpret_cast<const float4*>(xs + base) + i4);
       } else {
         float e[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const int xi = base + i + c;
+          const int xi = base + 4 * i4 + c;
           e[c] = (xi > -n_samples && xi < 2 * n_samples - 1) ? __ldg(xs + reflect_idx(xi, n_samples)) : 0.0f;
         }
         r.v[q] = make_float4(e[0], e[1], e[2], e[3]);
@@ -132,19 +132,17 @@ __device__ __forceinline__ void load_span(const float* __restrict__ x, int n_sam
   }
 }
 
-// One workgroup loops over tiles (16 consecutive frames of one signal) in grid
-// stride; the next tile's span is loaded into registers while the current one is
-// transformed, so HBM latency hides behind the DFT even at 3 workgroups per CU.
-__global__ __launch_bounds__(256) void stft_fwd_kernel(const float* __restrict__ x, int n_samples, int T,
-                                                       int frames_tiles, long long n_tiles, int flags,
-                                                       float* __restrict__ Xc, float* __restrict__ mag) {
-  __shared__ __attribute__((aligned(16))) float sx[SPAN];
+__global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restrict__ x, int n_samples, int T,
+                                                          int tiles_per_sig, int n_tiles, int flags,
+                                                          float2* __restrict__ Xc, float* __restrict__ mag) {
+  __shared__ __attribute__((aligned(16))) float sx[SPAN2];
   __shared__ float sw[NFFT];
   __shared__ float2 stw[NFFT];
-  __shared__ __attribute__((aligned(16))) float2 sy[FPW][16 * YS];  // transpose; then the output tile
+  // transpose [pair][row][col ^ row] (XOR swizzle instead of padding keeps LDS at
+  // 52 KB: 3 workgroups per CU), then Z[pair][256]
+  __shared__ __attribute__((aligned(16))) float2 sy[FPT / 2][NFFT];
 
   const int tid = threadIdx.x;
-  // window + twiddles (LDS-resident, accurate), once per workgroup
   {
     float s, c;
     sincospif((float)tid / 128.0f, &s, &c);
@@ -152,68 +150,105 @@ __global__ __launch_bounds__(256) void stft_fwd_kernel(const float* __restrict__
     const float sh = sinpif((float)tid / 256.0f);
     sw[tid] = sh * sh;  // periodic Hann: 0.5 - 0.5 cos(2 pi n / 256) = sin^2(pi n / 256)
   }
-  long long tile = blockIdx.x;
+  int tile = blockIdx.x;
   SpanRegs pf;
-  if (tile < n_tiles) load_span(x, n_samples, frames_tiles, tile, tid, pf);
-  const int fr = tid >> 4;  // frame within tile
+  if (tile < n_tiles) load_span(x, n_samples, tiles_per_sig, tile, tid, pf);
+  const int pr = tid >> 4;  // frame pair within the tile
   const int j = tid & 15;
   const bool conj = flags & F_CONJ;
-  float2* tc = reinterpret_cast<float2*>(&sy[0][0]);      // output tile: FPW x NBIN complex
-  float* tm = reinterpret_cast<float*>(tc + FPW * NBIN);  // FPW x NBIN magnitude
+  const bool want_c = flags & F_COMPLEX, want_m = flags & (F_MAG | F_LOGMAG), logm = flags & F_LOGMAG;
+  float2* sz = &sy[0][0];  // Z of pair p at sz[p * 256 + k]
 
   for (; tile < n_tiles; tile += gridDim.x) {
-    __syncthreads();  // previous tile's output staging fully read
+    __syncthreads();  // previous tile's Z fully read
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = 4 * (tid + 256 * q);
-      if (i < SPAN) *reinterpret_cast<float4*>(sx + i) = pf.v[q];
+    for (int q = 0; q < PFQ; ++q) {
+      const int i4 = tid + 256 * q;
+      if (i4 < SPAN2_Q) reinterpret_cast<float4*>(sx)[i4] = pf.v[q];
     }
     __syncthreads();
-    const long long next = tile + gridDim.x;
-    if (next < n_tiles) load_span(x, n_samples, frames_tiles, next, tid, pf);  // in flight during the DFT
+    const int next = tile + gridDim.x;
+    if (next < n_tiles) load_span(x, n_samples, tiles_per_sig, next, tid, pf);  // in flight during the DFT
 
-    // stage 1: lane j = n2; DFT16 over n1 of xw[16 n1 + j], twiddle W256^{j k1}
+    // stage 1: lane j = n2; DFT16 over n1 of z[16 n1 + j], twiddle W256^{j k1}
     {
       float2 v[16], o[16];
-      const float* fx = sx + HOPL * fr;
+      const float* fa = sx + HOPL * (2 * pr);
+      const float* fb = fa + HOPL;
 #pragma unroll
       for (int n1 = 0; n1 < 16; ++n1) {
         const int n = 16 * n1 + j;
-        v[n1] = make_float2(fx[n] * sw[n], 0.0f);
+        const float wn = sw[n];
+        v[n1] = make_float2(fa[n] * wn, fb[n] * wn);
       }
       dft16<-1>(v, o);
 #pragma unroll
-      for (int k1 = 0; k1 < 16; ++k1) sy[fr][k1 * YS + j] = cmul(o[k1], stw[(j * k1) & 255]);
+      for (int k1 = 0; k1 < 16; ++k1) sy[pr][k1 * 16 + (j ^ k1)] = cmul(o[k1], stw[(j * k1) & 255]);
     }
     __syncthreads();
-    // stage 2: lane j = k1; DFT16 over n2 -> X[j + 16 k2]
+    // stage 2: lane j = k1; DFT16 over n2 -> Z[j + 16 k2]
     float2 o[16];
     {
       float2 v[16];
 #pragma unroll
-      for (int n2 = 0; n2 < 16; ++n2) v[n2] = sy[fr][j * YS + n2];
+      for (int n2 = 0; n2 < 16; ++n2) v[n2] = sy[pr][j * 16 + (n2 ^ j)];
       dft16<-1>(v, o);
     }
-    __syncthreads();  // sy is reused as the output tile below
+    // a pair's 16 lanes sit in one wave and have all read their rows above, so Z
+    // overwrites the pair's transpose region without a workgroup barrier
 #pragma unroll
-    for (int k2 = 0; k2 < 9; ++k2) {
-      const int k = j + 16 * k2;
-      if (k < NBIN) {
-        float2 X = o[k2];
-        if (conj) X.y = -X.y;
-        tc[fr * NBIN + k] = X;
-        float m = sqrtf(X.x * X.x + X.y * X.y);
-        if (flags & F_LOGMAG) m = logf(m + 2.220446049250313e-16f);
-        tm[fr * NBIN + k] = m;
+    for (int k2 = 0; k2 < 16; ++k2) sz[pr * NFFT + j + 16 * k2] = o[k2];
+    __syncthreads();
+
+    // split the pairs and emit the tile: thread (parity, bin) = (tid >> 7, tid & 127)
+    // writes bin k of frames 2 it + parity (waves 0-1 even frames, 2-3 odd: no
+    // divergence); a wave stores 64 consecutive bins of one frame.  Bin 128 by 32
+    // threads at the end.
+    const int sig = tile / tiles_per_sig;
+    const int t0 = (tile - sig * tiles_per_sig) * FPT;
+    const int nfr = min(FPT, T - t0);
+    const long long row0 = ((long long)sig * T + t0) * NBIN;
+    const int par = tid >> 7, k = tid & 127;
+    const int km = (NFFT - k) & (NFFT - 1);
+    float2* xc = Xc + row0 + par * NBIN + k;
+    float* xm = mag + row0 + par * NBIN + k;
+    for (int it = 0; 2 * it + par < nfr; ++it) {
+      const float2 zk = sz[it * NFFT + k];
+      const float2 zm = sz[it * NFFT + km];
+      float2 X = par == 0 ? make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y))
+                          : make_float2(0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x));
+      if (conj) X.y = -X.y;
+#ifdef STFT_NT_STORES
+      if (want_c) {
+        __builtin_nontemporal_store(X.x, &xc[2 * it * NBIN].x);
+        __builtin_nontemporal_store(X.y, &xc[2 * it * NBIN].y);
+      }
+      if (want_m) {
+        float m = __builtin_amdgcn_sqrtf(X.x * X.x + X.y * X.y);
+        if (logm) m = __logf(m + 2.220446049250313e-16f);
+        __builtin_nontemporal_store(m, &xm[2 * it * NBIN]);
+      }
+#else
+      if (want_c) xc[2 * it * NBIN] = X;
+      if (want_m) {
+        float m = __builtin_amdgcn_sqrtf(X.x * X.x + X.y * X.y);
+        if (logm) m = __logf(m + 2.220446049250313e-16f);
+        xm[2 * it * NBIN] = m;
+      }
+#endif
+    }
+    if (tid < nfr) {  // Nyquist bin: Z[128] pairs with itself
+      const int f = tid;
+      const float2 z = sz[(f >> 1) * NFFT + 128];
+      float2 X = (f & 1) == 0 ? make_float2(z.x, 0.0f) : make_float2(z.y, 0.0f);
+      if (conj) X.y = -X.y;
+      if (want_c) Xc[row0 + f * NBIN + 128] = X;
+      if (want_m) {
+        float m = fabsf(X.x);
+        if (logm) m = __logf(m + 2.220446049250313e-16f);
+        mag[row0 + f * NBIN + 128] = m;
       }
     }
-    __syncthreads();
-    const long long sig = tile / frames_tiles;
-    const int t0 = (int)(tile % frames_tiles) * FPW;
-    const int nfr = min(FPW, T - t0);
-    const long long row0 = (sig * T + t0) * (long long)NBIN;
-    if (flags & F_COMPLEX) store_tile(Xc + 2 * row0, reinterpret_cast<const float*>(tc), 2 * nfr * NBIN, tid);
-    if (flags & (F_MAG | F_LOGMAG)) store_tile(mag + row0, tm, nfr * NBIN, tid);
   }
 }
 
@@ -311,12 +346,13 @@ DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int
   DL4SS_REQUIRE(!((flags & (F_MAG | F_LOGMAG)) && !mag));
   if (n_sig == 0) return 0;
   const int T = 1 + n_samples / HOPL;
-  const int tiles = (T + FPW - 1) / FPW;
-  // grid-stride launch sized to the resident capacity (3 workgroups per CU: LDS and VGPRs)
+  const int tiles = (T + FPT - 1) / FPT;
+  // grid-stride launch sized to the resident capacity (3 workgroups per CU)
   const long long n_tiles = n_sig * tiles;
+  DL4SS_REQUIRE(n_tiles < (1LL << 31));
   const long long grid = n_tiles < 256LL * 3 ? n_tiles : 256LL * 3;
   hipLaunchKernelGGL(stft_fwd_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), x, n_samples, T, tiles,
-                     n_tiles, flags, X_c64, mag);
+                     (int)n_tiles, flags, reinterpret_cast<float2*>(X_c64), mag);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

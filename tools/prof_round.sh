@@ -3,6 +3,7 @@
 #   1. standalone STFT roofline probe (>= 2048 signals)
 #   2. rocprofv3 --kernel-trace --stats of a short bench run  -> gpurun_out/$TAG/trace
 #   3. two PMC passes (FETCH_SIZE, WRITE_SIZE; separate passes)  -> gpurun_out/$TAG/pmc_{fetch,write}
+#      (per launch, with its grid size: bench.py picks the launches of each measured unit)
 # Every GPU step has its own time limit; the chain stops at the first failure.
 TAG=${TAG:-prof}
 BARGS=${BARGS:---steps 3 --warmup 1 --no-cpu-baseline}

@@ -34,6 +34,20 @@ def main(src, tag, out="profiles"):
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
                      f"{float(r['MinNs']) / 1e3:.2f} | {float(r['MaxNs']) / 1e3:.2f} | "
                      f"{100 * float(r['TotalDurationNs']) / tot:.1f} |")
+    # per-(kernel, grid) split of the trace: the STFT runs at two sizes in bench.py
+    # (in-step launches and the standalone 2048-signal probe)
+    tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        by = collections.defaultdict(list)
+        for r in csv.DictReader(open(tr)):
+            nm = short(r["Kernel_Name"])
+            if "stft" in nm or "gemm" in nm:
+                by[(nm, r.get("Grid_Size", r.get("Grid_Size_X", "?")))].append(
+                    (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        lines += ["", "## STFT / GEMM launches by grid size", "", "| kernel | grid | calls | avg us |",
+                  "|---|---|---|---|"]
+        for (nm, g), v in sorted(by.items()):
+            lines.append(f"| `{nm}` | {g} | {len(v)} | {sum(v) / len(v):.2f} |")
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
     for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
         f = os.path.join(src, sub, "run_counter_collection.csv")
@@ -41,17 +55,19 @@ def main(src, tag, out="profiles"):
             continue
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter:
-                pmc[short(r["Kernel_Name"])][counter].append(float(r["Counter_Value"]))
+                pmc[short(r["Kernel_Name"])][counter].append((int(r["Grid_Size"]), float(r["Counter_Value"])))
     res = {}
     for k, d in pmc.items():
-        fetch = [2 * 1024 * v for v in d.get("FETCH_SIZE", [])]
-        write = [1024 * v for v in d.get("WRITE_SIZE", [])]
+        fetch = [(g, 2 * 1024 * v) for g, v in d.get("FETCH_SIZE", [])]
+        write = [(g, 1024 * v) for g, v in d.get("WRITE_SIZE", [])]
         n = min(len(fetch), len(write))
         if n == 0:
             continue
-        res[k] = {"dispatches": n, "fetch_bytes_per_launch": fetch[:n], "write_bytes_per_launch": write[:n],
-                  "traffic_bytes_per_launch": [a + b for a, b in zip(fetch[:n], write[:n])],
-                  "avg_traffic_bytes": sum(a + b for a, b in zip(fetch[:n], write[:n])) / n}
+        # the two passes run the same command: dispatch i of one pass is dispatch i of the other
+        per = [{"grid": gf, "fetch": vf, "write": vw, "traffic": vf + vw}
+               for (gf, vf), (gw, vw) in zip(fetch[:n], write[:n]) if gf == gw]
+        res[k] = {"dispatches": len(per), "launches": per,
+                  "avg_traffic_bytes": sum(p["traffic"] for p in per) / max(1, len(per))}
     if res:
         json.dump({"source": src, "correction": "FETCH_SIZE x2 (gfx950), KB->bytes", "kernels": res},
                   open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
