@@ -35,9 +35,16 @@ SIGNATURES = {
     "dl4ss_query_bwd": [P, I, I, I, P, P, P, P, I, I, P, P, P, P],
     "dl4ss_colsum": [P, LL, I, I, P, P],
     "dl4ss_adam": [P, P, P, P, LL, F, F, F, F, I, P],
+    "dl4ss_istft_apply": [P, P, LL, I, I, I, I, P, P],
+    "dl4ss_tanh_bwd": [P, P, P, LL, P],
+    "dl4ss_attn_dot_nblk": [I],
+    "dl4ss_attn_dot_fwd": [P, P, I, I, I, I, I, P, P],
+    "dl4ss_attn_dot_bwd": [P, P, I, P, P, I, I, I, I, P, P, P, P],
+    "dl4ss_top_k_mask": [P, I, I, F, I, P, P, P, P],
 }
 # entry points that return a value rather than a hipError_t
-RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int}
+RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
+            "dl4ss_attn_dot_nblk": ctypes.c_int}
 
 _lib = None
 

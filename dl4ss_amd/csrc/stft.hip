@@ -28,7 +28,7 @@ constexpr int FPW = 16;             // frames per workgroup
 constexpr int SPAN = HOPL * FPW + NFFT;  // 2304 samples
 constexpr int YS = 17;              // padded row stride (complex) of the transpose
 
-enum { F_COMPLEX = 1, F_MAG = 2, F_LOGMAG = 4, F_CONJ = 8 };
+enum { F_COMPLEX = 1, F_MAG = 2, F_LOGMAG = 4, F_CONJ = 8, F_APPLY_MAG = 16, F_APPLY_CRM = 32 };
 
 // cos / sin of 2*pi*m/16
 __device__ constexpr float C16[16] = {1.0f, 0.92387953251128674f, 0.70710678118654752f, 0.38268343236508977f,
@@ -261,8 +261,12 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
 // p = m + 128 and needs frames p/128 and p/128 - 1, so the workgroup owning
 // m in [128 t0, 128 t0 + 2048) needs frames t0 .. t0+16 (one recomputed).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void istft_kernel(const float2* __restrict__ S, int T, int flags,
-                                                    float* __restrict__ y, int out_len, int tiles) {
+// aux (mask-apply modes): signal `sig` is synthesised from mixture sig / k_per_ref:
+//   F_APPLY_MAG: S_hat = aux_mag[sig] * exp(i angle X_mix)        (EvalVer.py:56-65)
+//   F_APPLY_CRM: S_hat = aux_cplx[sig] (x) X_mix, complex product  (cRM_EvalVer.py:96-99, 720-728)
+__global__ __launch_bounds__(256) void istft_kernel(const float2* __restrict__ S, const float* __restrict__ aux,
+                                                    int k_per_ref, int T, int flags, float* __restrict__ y,
+                                                    int out_len, int tiles) {
   // frames t0 .. t0+16 (17 frames), each 256 real samples after irfft*window
   __shared__ float2 stw[NFFT];
   __shared__ float sw[NFFT];
@@ -293,12 +297,21 @@ __global__ __launch_bounds__(256) void istft_kernel(const float2* __restrict__ S
       const int k = 16 * k1 + j;
       float2 z = make_float2(0.f, 0.f);
       if (t >= 0 && t < T) {
-        const long long row = (sig * T + t) * (long long)NBIN;
+        const long long ref = (flags & (F_APPLY_MAG | F_APPLY_CRM)) ? sig / k_per_ref : sig;
+        const int kk = k < NBIN ? k : NFFT - k;
+        z = S[(ref * T + t) * (long long)NBIN + kk];
+        const long long arow = (sig * T + t) * (long long)NBIN + kk;
+        if (flags & F_APPLY_MAG) {
+          const float m = aux[arow], a = sqrtf(z.x * z.x + z.y * z.y);
+          z = a > 0.0f ? make_float2(z.x * (m / a), z.y * (m / a)) : make_float2(m, 0.0f);
+        } else if (flags & F_APPLY_CRM) {
+          float2 mk = reinterpret_cast<const float2*>(aux)[arow];
+          if (conj) mk.y = -mk.y;  // S holds conj(X): conj(M X) = conj(M) conj(X)
+          z = cmul(mk, z);
+        }
         if (k < NBIN) {
-          z = S[row + k];
           if (conj) z.y = -z.y;
         } else {
-          z = S[row + (NFFT - k)];
           if (!conj) z.y = -z.y;  // Hermitian: Z[256-k] = conj(Z[k])
         }
         if (k == 0 || k == 128) z.y = 0.0f;  // irfft ignores imag of DC/Nyquist
@@ -364,7 +377,24 @@ DL4SS_API int dl4ss_istft(const float* S_c64, long long n_sig, int T, int n_fft,
   const int out_len = HOPL * (T - 1);
   const int tiles = (T - 1 + FPW - 1) / FPW;
   hipLaunchKernelGGL(istft_kernel, dim3((unsigned)(n_sig * tiles)), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<const float2*>(S_c64), T, flags, y, out_len, tiles);
+                     reinterpret_cast<const float2*>(S_c64), nullptr, 1, T, flags & F_CONJ, y, out_len, tiles);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+// Mask apply + overlap-add iSTFT in one pass (eval path, SURVEY R12 + R16): n_sig
+// output signals, signal s from mixture s / k_per_mix.  mode 0: aux = masked
+// magnitude (n_sig, T, 129) with the mixture phase; mode 1: aux = complex ratio
+// mask (n_sig, T, 129, 2) multiplied with the mixture spectrum.
+DL4SS_API int dl4ss_istft_apply(const float* X_mix_c64, const float* aux, long long n_sig, int k_per_mix, int T,
+                                int mode, int conj, float* y, void* stream) {
+  DL4SS_REQUIRE(X_mix_c64 && aux && y && T >= 2 && n_sig >= 0 && k_per_mix >= 1 && (mode == 0 || mode == 1));
+  if (n_sig == 0) return 0;
+  const int out_len = HOPL * (T - 1);
+  const int tiles = (T - 1 + FPW - 1) / FPW;
+  const int flags = (mode == 0 ? F_APPLY_MAG : F_APPLY_CRM) | (conj ? F_CONJ : 0);
+  hipLaunchKernelGGL(istft_kernel, dim3((unsigned)(n_sig * tiles)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float2*>(X_mix_c64), aux, k_per_mix, T, flags, y, out_len, tiles);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

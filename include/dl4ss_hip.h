@@ -44,6 +44,13 @@ int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int n_fft, in
  * flags: DL4SS_STFT_CONJ only. */
 int dl4ss_istft(const float* S_c64, long long n_sig, int T, int n_fft, int hop, int flags, float* y,
                 void* stream);
+/* Mask apply + iSTFT in one pass (eval output path): signal s (n_sig of them) is
+ * synthesised from mixture s / k_per_mix.  mode 0: aux = masked magnitude (n_sig,T,129)
+ * with the mixture phase (EvalVer.py:56-65); mode 1: aux = complex ratio mask
+ * (n_sig,T,129,2) times the mixture spectrum (cRM_EvalVer.py:96-99,720-728).
+ * conj: the mixture spectrum is stored conjugated (librosa <= 0.5). */
+int dl4ss_istft_apply(const float* X_mix_c64, const float* aux, long long n_sig, int k_per_mix, int T, int mode,
+                      int conj, float* y, void* stream);
 
 /* ---- R1 preprocessing / mixing ----------------------------------------- */
 /* raw (B, K, N) -> out_src (B, K, N): each source x -> (x - mean) / max|x - mean| * gain;
@@ -122,6 +129,25 @@ int dl4ss_colsum(const float* A, long long lda, int M, int N, float* out, void* 
 /* torch.optim.Adam step on flat fp32 buffers (EvalVer.py:538-544). */
 int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
                float eps, int step, void* stream);
+
+/* ---- kernels behind the reference-API nn.Modules (dl4ss_amd/compat/myNet.py) ---- */
+/* dpre = dv * (1 - v^2): backward of MIX_SPEECH's tanh(Linear) (EvalVer.py:298-299). */
+int dl4ss_tanh_bwd(const float* v, const float* dv, float* dpre, long long n, void* stream);
+/* Row blocks of the ATTENTION 'dot' backward (size of part_dq: Bq * nblk * E). */
+int dl4ss_attn_dot_nblk(int R);
+/* ATTENTION 'dot': mask (Bq,R) = act(V (Bq,R,E) . q (Bq, row stride q_stride)); act 0 =
+ * sigmoid (EvalVer.py:216-226), 1 = 10 tanh, the cRM branch per query half (cRM:259-271). */
+int dl4ss_attn_dot_fwd(const float* V, const float* q, int q_stride, int Bq, int R, int E, int act, float* mask,
+                       void* stream);
+/* Its backward: dV += dE q (may be NULL; accumulates, so both cRM halves add) and
+ * dq (Bq,E) = sum_r dE V (deterministic partial sums, part_dq: Bq*nblk*E). */
+int dl4ss_attn_dot_bwd(const float* V, const float* q, int q_stride, const float* mask, const float* dmask, int Bq,
+                       int R, int E, int act, float* dV, float* part_dq, float* dq, void* stream);
+/* top_k_mask (EvalVer.py:390-405, main_run.py:340-355): mask (B,N) of the first
+ * min(top_k, #{p > alpha}) entries in descending order (ties: lower index first);
+ * idx (B,top_k) the selected ids ascending (-1 padded), count (B); idx/count may be NULL. */
+int dl4ss_top_k_mask(const float* prob, int B, int N, float alpha, int top_k, float* mask, int* idx, int* count,
+                     void* stream);
 
 #ifdef __cplusplus
 }

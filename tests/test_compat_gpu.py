@@ -1,0 +1,235 @@
+"""Reference-API modules on the HIP path (dl4ss_amd.compat), against the oracle /
+torch-CPU references with identical weights: forward values and autograd
+gradients of MIX_SPEECH (BiGRU and BiLSTM), ATTENTION ('dot' and cRM),
+SPEECH_EMBEDDING (gather and dense), ADDJUST, top_k_mask; the loaders' batch-dict
+contract and features; mask-apply + iSTFT; and one driver-style training step
+(EvalVer.py:586-675 shape) compared with the oracle step."""
+import numpy as np
+import pytest
+import torch
+
+from dl4ss_amd import compat
+from oracle import dsp, model as om
+
+pytestmark = pytest.mark.gpu
+compat.install()
+import config  # noqa: E402
+import myNet  # noqa: E402
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("cell,layers", [("gru", 2), ("lstm", 2)])
+def test_mix_speech_fwd_bwd_vs_torch(dev, cell, layers):
+    torch.manual_seed(0)
+    B, T, F = 3, 21, 129
+    m = myNet.MIX_SPEECH(F, T, cell=cell, num_layers=layers, return_hidden=True).to(dev)
+    ref = om.MixSpeech(cell, F, 300, layers, 50)
+    ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    x = torch.rand(B, T, F)
+    v, h = m(x.to(dev))
+    v_ref, h_ref = ref(x)
+    assert _rel(v, v_ref) < 1e-4 and _rel(h, h_ref) < 1e-4
+    g = torch.randn_like(v_ref)
+    (v * g.to(dev)).sum().backward()
+    (v_ref * g).sum().backward()
+    for (n, p), (n2, p2) in zip(m.named_parameters(), ref.named_parameters()):
+        assert n == n2
+        assert _rel(p.grad, p2.grad) < 2e-3, (n, _rel(p.grad, p2.grad))
+
+
+@pytest.mark.parametrize("crm", [False, True])
+def test_attention_dot_fwd_bwd(dev, crm):
+    torch.manual_seed(1)
+    Bq, T, F, E = 4, 7, 129, 50
+    att = myNet.ATTENTION(E, 'dot', crm=crm).to(dev)
+    V = torch.randn(Bq, T, F, E, requires_grad=True)
+    q = (0.3 * torch.randn(Bq, 2 * E if crm else E)).requires_grad_(True)
+    Vd = V.detach().to(dev).requires_grad_(True)
+    qd = q.detach().to(dev).requires_grad_(True)
+    mask = att(Vd, qd)
+    if crm:  # cRM_EvalVer.py:259-271: 10 tanh(V . q_half), stacked on the last dim
+        e1 = torch.einsum("btfe,be->btf", V, q[:, :E])
+        e2 = torch.einsum("btfe,be->btf", V, q[:, E:])
+        ref = torch.stack([10 * torch.tanh(e1), 10 * torch.tanh(e2)], dim=-1)
+    else:
+        ref = torch.sigmoid(torch.einsum("btfe,be->btf", V, q))
+    assert mask.shape == ref.shape
+    assert _rel(mask, ref) < 1e-5
+    g = torch.randn_like(ref)
+    (mask * g.to(dev)).sum().backward()
+    (ref * g).sum().backward()
+    assert _rel(Vd.grad, V.grad) < 1e-4 and _rel(qd.grad, q.grad) < 1e-4
+
+
+def test_embedding_adjust_fwd_bwd(dev):
+    torch.manual_seed(2)
+    B, K, T, W, D = 3, 2, 11, 50, 600
+    emb = myNet.SPEECH_EMBEDDING(101, W, 5, crm=False).to(dev)
+    adj = myNet.ADDJUST(D, W, crm=False).to(dev)
+    ref_emb = om.Embedding(101, W)
+    ref_adj = om.Adjust(D, W)
+    ref_emb.load_state_dict({k: v.cpu() for k, v in emb.state_dict().items()})
+    ref_adj.load_state_dict({k: v.cpu() for k, v in adj.state_dict().items()})
+    idx = [np.array([3, 40]), np.array([0, 100]), np.array([7, 8])]
+    h = torch.randn(B, T, D)
+    hd = h.to(dev).requires_grad_(True)
+    h.requires_grad_(True)
+    q = emb(None, idx)
+    out = q + adj(hd, q)
+    qr = ref_emb(torch.from_numpy(np.array(idx)))
+    out_r = qr + ref_adj(h, qr)
+    assert _rel(out, out_r) < 1e-5
+    g = torch.randn_like(out_r)
+    (out * g.to(dev)).sum().backward()
+    (out_r * g).sum().backward()
+    assert _rel(emb.layer.weight.grad, ref_emb.layer.weight.grad) < 1e-5
+    assert _rel(adj.layer.weight.grad, ref_adj.layer.weight.grad) < 1e-5
+    assert _rel(hd.grad, h.grad) < 1e-5
+    # dense masked form (main_run.py:318-327)
+    mask = torch.zeros(B, 101)
+    mask[0, [3, 40]] = 1
+    mask[1, [0, 100]] = 1
+    mask[2, 5] = 1
+    dense = emb(mask)
+    ref_dense = ref_emb.layer.weight.detach()[None] * mask[:, :, None]
+    assert _rel(dense, ref_dense) < 1e-6
+
+
+def test_top_k_mask_device_vs_oracle(dev):
+    g = torch.Generator().manual_seed(3)
+    p = torch.rand(8, 101, generator=g)
+    for alpha, k in [(0.5, 2), (0.5, 101), (-0.5, 2), (0.9, 3), (0.99, 5)]:
+        ours = myNet.top_k_mask(p, alpha, k)
+        ref = om.top_k_mask(p, alpha, k)
+        assert torch.equal(ours, ref), (alpha, k)
+    # ground-truth multi-hot (the training path): exactly the active speakers
+    y = torch.zeros(4, 101)
+    y[0, [1, 50]] = 1
+    y[1, [0, 100]] = 1
+    y[2, [7, 8]] = 1
+    y[3, [99, 3]] = 1
+    assert torch.equal(myNet.top_k_mask(y, 0.5, 101), y)
+
+
+def test_prepare_data_contract_and_features(dev):
+    import predata_multiAims_dB as pdb
+
+    config.BATCH_SIZE, config.MAX_LEN = 3, 8000
+    try:
+        g = pdb.prepare_data('global', 'train')
+        spk, d2i, i2d, T, F, frames, n = next(g)
+        assert n == 101 and spk == sorted(spk) and d2i[spk[5]] == 5 and i2d[5] == spk[5]
+        assert (T, F, frames) == (1 + 8000 // 128, 129, 32)
+        d = next(pdb.prepare_data('once', 'train'))
+        for k in ("mix_wav", "mix_feas", "mix_phase", "aim_fea", "aim_spkname", "query", "num_all_spk",
+                  "multi_spk_fea_list", "multi_spk_wav_list"):
+            assert k in d, k
+        assert d["mix_wav"].dtype == np.float64 and d["mix_wav"].shape == (3, 8000)
+        assert d["mix_feas"].dtype == np.float32 and d["mix_feas"].shape == (3, T, F)
+        assert d["mix_phase"].dtype == np.complex64 and d["mix_phase"].shape == (3, T, F)
+        for b in range(3):
+            srcs = d["multi_spk_wav_list"][b]
+            assert len(srcs) == 2
+            # mixture = sum of the gained sources; features = |STFT| (numpy restatement)
+            assert np.abs(sum(srcs.values()) - d["mix_wav"][b]).max() < 1e-5
+            ref = np.abs(dsp.stft_tf(d["mix_wav"][b]))
+            assert np.abs(d["mix_feas"][b] - ref).max() / ref.max() < 1e-5
+            assert np.abs(np.abs(d["mix_phase"][b]) - ref).max() / ref.max() < 1e-5
+            for name, w in srcs.items():
+                fr = np.abs(dsp.stft_tf(w))
+                assert np.abs(d["multi_spk_fea_list"][b][name] - fr).max() / fr.max() < 1e-5
+                # peak-normalised then gained: max|x| is 1 or the dB gain 10^(5/20 u) <= 1.78
+                assert 0.999 < np.abs(w).max() < 1.7783
+    finally:
+        config.BATCH_SIZE, config.MAX_LEN = 16, 40000
+
+
+def test_fromlist_crm_loader(dev):
+    import predata_fromList_cRM_123 as pfl
+
+    c = pfl.config
+    bs, ml = c.BATCH_SIZE, c.MAX_LEN
+    c.BATCH_SIZE, c.MAX_LEN = 2, 4000
+    try:
+        d = next(pfl.prepare_data('once', 'train'))
+        T = 1 + 4000 // 128
+        assert d["mix_mag"].shape == (2, T, 129, 2) and d["batch_total"] > 0
+        ref = pfl.convert2(dsp.stft_tf(d["mix_wav"][0]))
+        assert np.abs(d["mix_mag"][0] - ref).max() / np.abs(ref).max() < 1e-5
+        for name, w in d["multi_spk_wav_list"][0].items():
+            tr = pfl.convert2(dsp.stft_tf(w))
+            assert np.abs(d["multi_spk_fea_list"][0][name] - tr).max() / np.abs(tr).max() < 1e-5
+    finally:
+        c.BATCH_SIZE, c.MAX_LEN = bs, ml
+
+
+@pytest.mark.parametrize("crm", [False, True])
+def test_mask_apply_istft_vs_oracle(dev, crm):
+    import bss_test
+
+    rng = np.random.default_rng(4)
+    B, K, N = 2, 2, 4000
+    mix = rng.standard_normal((B, N))
+    Xc = np.stack([dsp.convert2(dsp.stft_tf(mix[b])) for b in range(B)])  # (B,T,F,2)
+    T = Xc.shape[1]
+    if crm:
+        pred = rng.standard_normal((B, K, T, 129, 2)).astype(np.float32)
+    else:
+        pred = rng.uniform(0, 1, (B, K, T, 129)).astype(np.float32) * np.abs(Xc[:, None, ..., 0] + 1j * Xc[:, None, ..., 1])
+    y = bss_test.reconstruct(torch.from_numpy(pred).to(dev), torch.from_numpy(Xc.astype(np.float32)).to(dev), crm=crm)
+    for b in range(B):
+        X = Xc[b, ..., 0] + 1j * Xc[b, ..., 1]
+        for k in range(K):
+            if crm:  # P = M (x) X (cRM_EvalVer.py:720-728), then istft
+                S = (pred[b, k, ..., 0] + 1j * pred[b, k, ..., 1]) * X
+            else:  # magnitude with the mixture phase (EvalVer.py:56-65)
+                S = pred[b, k] * np.exp(1j * np.angle(X))
+            ref = dsp.istft(S.T if S.shape[0] != 129 else S)
+            out = y[b, k].cpu().numpy()
+            assert out.shape == ref.shape
+            assert np.abs(out - ref).max() / np.abs(ref).max() < 1e-4
+
+
+def test_driver_style_step_matches_oracle(dev):
+    """The EvalVer.py:586-675 step written against the reference modules (MIX_SPEECH
+    with hidden, SPEECH_EMBEDDING gather, ADDJUST, ATTENTION dot, expand + MSE + sum
+    loss in torch), run through myNet; gradients vs the oracle SepModel step."""
+    torch.manual_seed(5)
+    B, K, T, F = 2, 2, 17, 129
+    mix_hidden_layer_3d = myNet.MIX_SPEECH(F, T, cell="lstm", num_layers=2, return_hidden=True).to(dev)
+    emb_layer = myNet.SPEECH_EMBEDDING(101, 50, 5, crm=False).to(dev)
+    adjust_layer = myNet.ADDJUST(600, 50, crm=False).to(dev)
+    att = myNet.ATTENTION(50, 'dot', crm=False).to(dev)
+    ref = om.SepModel(cell="lstm", num_layers=2)
+    sd = {**{f"mix.{k}": v for k, v in mix_hidden_layer_3d.state_dict().items()},
+          **{f"emb.{k}": v for k, v in emb_layer.state_dict().items()},
+          **{f"adj.{k}": v for k, v in adjust_layer.state_dict().items()}}
+    ref.load_state_dict({k: v.cpu() for k, v in sd.items()})
+    feats = torch.rand(B, T, F)
+    Y = torch.rand(B, K, T, F)
+    idx = [np.array([3, 40]), np.array([0, 100])]
+    # --- driver-style forward on the HIP modules
+    x = feats.to(dev)
+    mix_speech_hidden, mix_tmp_hidden = mix_hidden_layer_3d(x)
+    q = emb_layer(None, idx)
+    q = adjust_layer(mix_tmp_hidden, q) + q
+    V5 = mix_speech_hidden.view(B, 1, T, F, 50).expand(B, K, T, F, 50).contiguous().view(-1, T, F, 50)
+    multi_mask = att(V5, q.view(-1, 50)).view(B, K, T, F)
+    pred = multi_mask * x.view(B, 1, T, F).expand(B, K, T, F)
+    mse = torch.nn.MSELoss()
+    loss = mse(pred, Y.to(dev)) + 0.5 * mse(torch.sum(multi_mask, 1), torch.ones(B, T, F, device=dev))
+    loss.backward()
+    # --- oracle
+    mask_r, _, _, _ = ref(feats, torch.from_numpy(np.array(idx)))
+    loss_r, _ = om.loss_label_ordered(mask_r, feats, Y)
+    loss_r.backward()
+    assert abs(float(loss) - float(loss_r)) / float(loss_r) < 1e-5
+    mods = {"mix": mix_hidden_layer_3d, "emb": emb_layer, "adj": adjust_layer}
+    for name, p in ref.named_parameters():
+        top, rest = name.split(".", 1)
+        mine = dict(mods[top].named_parameters())[rest]
+        assert _rel(mine.grad, p.grad) < 2e-3, (name, _rel(mine.grad, p.grad))
