@@ -30,14 +30,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_FILE = "profiles/r01_pmc.json"
+PMC_FILE = "profiles/r01_prof_c_pmc.json"
 
 
 def stft_grid_threads(n_sig, T):
-    """Launch grid (threads) of dl4ss_stft_fwd: 32-frame tiles, capped at 3 workgroups
-    per CU (stft.hip)."""
-    tiles = n_sig * ((T + 31) // 32)
-    return min(tiles, 256 * 3) * 256
+    """Launch grid (threads) of dl4ss_stft_fwd: one 256-thread workgroup per 32-frame
+    tile (stft.hip)."""
+    return n_sig * ((T + 31) // 32) * 256
 
 
 def stft_grids(B, K, T):

@@ -329,7 +329,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
           }
       }
       ld.commit(sin + (s & 1) * BC * J * 4);
+#ifndef RNN_EXP_NOPF
       if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
+#endif
       STAMP(0)
       __syncthreads();  // B1
       STAMP(1)
@@ -386,7 +388,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
         }
         // padded batch rows (bg >= B) still publish (zeros) so peers never wait on them
         put_granule(xg + (long long)(s & 1) * BC * H + cb * H + cj, (unsigned)(s + 1), hn);
+#ifdef RNN_EXP_NOSAVE
         if (cval) {
+          const long long bt = (long long)bg * T + t;
+          a.out[bt * 2 * H + d * H + cj] = hn;
+        }
+        if (false) {
+#else
+        if (cval) {
+#endif
           const long long bt = (long long)bg * T + t;
           float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;  // act rows are 4H wide for both cells
           actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
@@ -624,7 +634,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
           if (goff[g] >= 0) sdh[tid - NROLE + g * NROLE] = __uint_as_float((unsigned)v[g]);
       }
       ld.commit(sop + (s & 1) * BC * J * 8);
+#ifndef RNN_EXP_NOPF
       if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+#endif
       STAMP(0)
       __syncthreads();  // B1
       STAMP(1)
@@ -692,8 +704,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
         }
         const long long bt = (long long)bg * T + t;
         float* dgp = a.dG + (bt * 2 + d) * GH + cj;
+#ifndef RNN_EXP_NOSAVE
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) dgp[q * H] = dgi[q];
+#endif
         if (CELL == CELL_GRU) {
           float* dhp = a.dGh + (bt * 2 + d) * GH + cj;
 #pragma unroll

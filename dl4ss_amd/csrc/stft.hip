@@ -95,8 +95,9 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
 // Cooley-Tukey (two in-register radix-4x4 DFT16 + one LDS transpose); Z is then
 // staged in LDS and every thread emits consecutive output bins of the tile (the
 // tile is one contiguous range of the (signal, frame, bin) layout), so complex
-// and magnitude stores are fully coalesced.  One workgroup walks tiles in grid
-// stride with the next span's 16-B loads in flight during the current DFT.
+// and magnitude stores are fully coalesced.  The launch gives every tile its own
+// workgroup (3 resident per CU); a workgroup handed several tiles (grid stride)
+// keeps the next span's 16-B loads in flight during the current DFT.
 // ---------------------------------------------------------------------------
 constexpr int FPT = 32;                  // frames per tile
 constexpr int SPAN2 = HOPL * FPT + NFFT;  // 4352 samples
@@ -135,12 +136,11 @@ __device__ __forceinline__ void load_span(const float* __restrict__ x, int n_sam
 __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restrict__ x, int n_samples, int T,
                                                           int tiles_per_sig, int n_tiles, int flags,
                                                           float2* __restrict__ Xc, float* __restrict__ mag) {
-  __shared__ __attribute__((aligned(16))) float sx[SPAN2];
   __shared__ float sw[NFFT];
   __shared__ float2 stw[NFFT];
-  // transpose [pair][row][col ^ row] (XOR swizzle instead of padding keeps LDS at
-  // 52 KB: 3 workgroups per CU), then Z[pair][256]
+  // transpose [pair][row][col ^ row] (XOR swizzle instead of padding), then Z[pair][256]
   __shared__ __attribute__((aligned(16))) float2 sy[FPT / 2][NFFT];
+  __shared__ __attribute__((aligned(16))) float sx[SPAN2];
 
   const int tid = threadIdx.x;
   {
@@ -218,24 +218,12 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
       float2 X = par == 0 ? make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y))
                           : make_float2(0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x));
       if (conj) X.y = -X.y;
-#ifdef STFT_NT_STORES
-      if (want_c) {
-        __builtin_nontemporal_store(X.x, &xc[2 * it * NBIN].x);
-        __builtin_nontemporal_store(X.y, &xc[2 * it * NBIN].y);
-      }
-      if (want_m) {
-        float m = __builtin_amdgcn_sqrtf(X.x * X.x + X.y * X.y);
-        if (logm) m = __logf(m + 2.220446049250313e-16f);
-        __builtin_nontemporal_store(m, &xm[2 * it * NBIN]);
-      }
-#else
       if (want_c) xc[2 * it * NBIN] = X;
       if (want_m) {
         float m = __builtin_amdgcn_sqrtf(X.x * X.x + X.y * X.y);
         if (logm) m = __logf(m + 2.220446049250313e-16f);
         xm[2 * it * NBIN] = m;
       }
-#endif
     }
     if (tid < nfr) {  // Nyquist bin: Z[128] pairs with itself
       const int f = tid;
@@ -360,10 +348,12 @@ DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int
   if (n_sig == 0) return 0;
   const int T = 1 + n_samples / HOPL;
   const int tiles = (T + FPT - 1) / FPT;
-  // grid-stride launch sized to the resident capacity (3 workgroups per CU)
+  // one workgroup per tile: measured on MI355X (2048 x 4 s signals, complex + magnitude)
+  // 4.2-4.3 TB/s against 3.8-3.9 for a grid-stride launch sized to the resident
+  // capacity (768 workgroups walking 21 tiles each); the kernel still accepts any grid
   const long long n_tiles = n_sig * tiles;
   DL4SS_REQUIRE(n_tiles < (1LL << 31));
-  const long long grid = n_tiles < 256LL * 3 ? n_tiles : 256LL * 3;
+  const long long grid = n_tiles;
   hipLaunchKernelGGL(stft_fwd_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), x, n_samples, T, tiles,
                      (int)n_tiles, flags, reinterpret_cast<float2*>(X_c64), mag);
   DL4SS_CHECK_LAUNCH();

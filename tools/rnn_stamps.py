@@ -11,16 +11,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from dl4ss_amd import build as B  # noqa: E402
 
-LIB = os.path.join(ROOT, "dl4ss_amd", "libdl4ss_hip_stamps.so")
+# extra -D flags for experiment variants: RNN_DEFS="-DFOO -DBAR", library suffixed by RNN_TAG
+DEFS = os.environ.get("RNN_DEFS", "").split()
+LIB = os.path.join(ROOT, "dl4ss_amd", f"libdl4ss_hip_stamps{os.environ.get('RNN_TAG', '')}.so")
 
 
 def build_stamps():
     objs = []
-    os.makedirs("/tmp/stamps_obj", exist_ok=True)
+    od = f"/tmp/stamps_obj{os.environ.get('RNN_TAG', '')}"
+    os.makedirs(od, exist_ok=True)
     for f in sorted(os.listdir(B.CSRC)):
         if f.endswith(".hip"):
-            o = f"/tmp/stamps_obj/{f[:-4]}.o"
-            subprocess.run([B.HIPCC, *B.FLAGS, "-DRNN_STAMPS", "-I", B.CSRC, "-c", os.path.join(B.CSRC, f), "-o", o],
+            o = f"{od}/{f[:-4]}.o"
+            subprocess.run([B.HIPCC, *B.FLAGS, "-DRNN_STAMPS", *DEFS, "-I", B.CSRC, "-c", os.path.join(B.CSRC, f), "-o", o],
                            check=True)
             objs.append(o)
     subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", LIB], check=True)

@@ -38,7 +38,10 @@ def main(N=32000, iters=30):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1:  # python tools/stft_bench.py N_SIG {mag|complex} ITERS  (profiling runs)
+    if len(sys.argv) > 1 and sys.argv[1] == "sweep":  # python tools/stft_bench.py sweep  (size sweep)
+        for n in (512, 1024, 2048, 3072, 4096, 8192):
+            run(n, 32000, 20, True)
+    elif len(sys.argv) > 1:  # python tools/stft_bench.py N_SIG {mag|complex} ITERS  (profiling runs)
         run(int(sys.argv[1]), 32000, int(sys.argv[3]), sys.argv[2] == "complex")
     else:
         main()

@@ -41,7 +41,7 @@ def main(src, tag, out="profiles"):
         by = collections.defaultdict(list)
         for r in csv.DictReader(open(tr)):
             nm = short(r["Kernel_Name"])
-            if "stft" in nm or "gemm" in nm:
+            if "stft" in nm or "gemm" in nm or "rnn" in nm:
                 by[(nm, r.get("Grid_Size", r.get("Grid_Size_X", "?")))].append(
                     (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
         lines += ["", "## STFT / GEMM launches by grid size", "", "| kernel | grid | calls | avg us |",
