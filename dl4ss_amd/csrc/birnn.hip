@@ -66,6 +66,18 @@ __device__ __forceinline__ u64 stamp_now() {
 #define STAMP(i)
 #define STAMP_FLUSH
 #endif
+// Diagnostic build only (-DRNN_TRACE): per (workgroup, step) s_memrealtime (100 MHz, chip-wide)
+// of the publish (slot 0) and of the completed poll (slot 1) in a.stamps[(bid * T + s) * 2 + slot].
+#ifdef RNN_TRACE
+__device__ __forceinline__ u64 rtc_now() {
+  u64 t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define TRACE(slot, s) do { if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[((long long)blockIdx.x * a.T + (s)) * 4 + (slot)] = rtc_now(); } while (0)
+#else
+#define TRACE(slot, s) do { } while (0)
+#endif
 
 // Gate nonlinearities on the serial critical path: v_exp + v_rcp (1 ulp) instead of
 // the IEEE division / ocml tanh sequences (the cell update runs on one wave).
@@ -329,9 +341,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
           }
       }
       ld.commit(sin + (s & 1) * BC * J * 4);
-#ifndef RNN_EXP_NOPF
       if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
-#endif
       STAMP(0)
       __syncthreads();  // B1
       STAMP(1)
@@ -388,15 +398,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
         }
         // padded batch rows (bg >= B) still publish (zeros) so peers never wait on them
         put_granule(xg + (long long)(s & 1) * BC * H + cb * H + cj, (unsigned)(s + 1), hn);
-#ifdef RNN_EXP_NOSAVE
         if (cval) {
-          const long long bt = (long long)bg * T + t;
-          a.out[bt * 2 * H + d * H + cj] = hn;
-        }
-        if (false) {
-#else
-        if (cval) {
-#endif
           const long long bt = (long long)bg * T + t;
           float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;  // act rows are 4H wide for both cells
           actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
@@ -410,6 +412,319 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
     STAMP(4)
     // sh is rewritten only after the next gather's barrier (all matvec reads are
     // behind the barrier above); spart only after that barrier too.
+  }
+  STAMP_FLUSH
+}
+
+// --------------------------------------------------------------------------
+// Forward, bf16 MFMA mode with the PACKED hand-off (the throughput path).
+//
+// Measured on MI355X (tools/rnn_stamps.py, tools/rnn_trace.py; B = 32, H = 300):
+// the one-value-granule kernel above spends ~5k of its 6.7k cycles per step in the
+// hand-off.  Three changes, each timed:
+//  * h crosses workgroups already rounded to bf16 (the consumer rounds it anyway:
+//    results are bit-identical), three values per 8-B granule
+//      granule = { lo: v0 | v1 << 16, hi: v2 | tag << 16 },  16-bit tag = step + 1,
+//    two granules per 16-B store, 8 granules per (batch row, producer);
+//  * ONE wave polls, keeping two sweeps in flight (the older one is merged while
+//    the newer one travels): hand-off 2.3 -> 1.9 us;
+//  * a FAST copy written with plain stores and read with `sc1` loads: a plain store
+//    lands in the producer XCD's L2, which same-XCD consumers read directly, while an
+//    `sc1` store drops the line from L2 and the reader goes to the Infinity Fabric:
+//    hand-off 1.9 -> 0.96 us, step 2.68 -> 1.64 us.  A group's workgroups are placed
+//    on one XCD (group_of), but placement is speed only: every granule is ALSO
+//    published with an `sc1` store to a SAFE copy (the validated write-through form,
+//    MI355X_MICROARCH.md, Valid forms R2), and a consumer that has not completed a
+//    poll of the fast copy after FAST_SPINS sweeps switches to the safe copy for the
+//    rest of the launch.  Every value is validated by its own tag either way.
+// Waves: 0-3 MFMA tiles 0-3 + cell update + publish + saved-state stores;
+//        4 poll;  5-7 MFMA tiles 4-6 + per-step input prefetch.
+// Each MFMA tile runs two independent accumulator chains (even / odd k-steps).
+// --------------------------------------------------------------------------
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int PKU = 24;     // staged h slots per (row, producer): 8 granules x 3
+constexpr int WPOLL = 4;    // the polling wave
+constexpr unsigned FAST_SPINS = 256;  // sweeps of the fast copy before the safe copy is polled
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+
+template <int CELL, int BC>
+__global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
+  constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
+  constexpr int KSMAX = HMAX / 32;
+  constexpr int SHB = KSMAX * 32 + 8;  // bf16 row stride of the B image (k >= H stays zero)
+  const int H = a.H, T = a.T, J = a.J, NG = a.NG;
+  const int R = NGATE * J;
+  const int MT = (R + 15) / 16;
+  const int ngroups = 2 * a.nchunk;
+  int group, w;
+  group_of(blockIdx.x, NG, ngroups, group, w);
+  const int d = group / a.nchunk, chunk = group % a.nchunk;
+  const int b0 = chunk * BC;
+  const int j0 = w * J;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int GH = NGATE * H;
+  const int tile = wv < WPOLL ? wv : wv - 1;
+  const bool mv = wv != WPOLL && tile < MT;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  unsigned short* shb = reinterpret_cast<unsigned short*>(smem);                       // [16][SHB]
+  float* sgate = smem + 8 * SHB;                                                        // [BC][MT*16]
+  float* sin = sgate + BC * MT * 16;                                                    // [2][BC*32][4]
+  unsigned short* spub = reinterpret_cast<unsigned short*>(sin + 2 * BC * 32 * 4);      // [BC][PKU]
+
+  // ---- W_hh tile of this wave as bf16 A fragments: lane holds A[row tile*16 + (lane&15)][k]
+  bf16x8 afrag[KSMAX];
+  {
+    const int rl = tile * 16 + (lane & 15);
+    const int q = rl / J, u = rl % J;
+    const bool rv = mv && rl < R && j0 + u < H;
+    const float* wrow = a.Whh + ((long long)d * GH + q * H + j0 + u) * H;
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = ks * 32 + 8 * (lane >> 4) + j;
+        afrag[ks][j] = (short)bf16_rne((rv && k < H) ? wrow[k] : 0.0f);
+      }
+  }
+  for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;
+  for (int i = tid; i < BC * PKU; i += NT) spub[i] = 0;
+
+  // ---- cell lanes (waves 0-3): row cb = tid / 32, unit cu = tid % 32 (< J)
+  const int cb = tid >> 5, cu = tid & 31;
+  const bool ct = tid < BC * 32 && cu < J;
+  const int cj = j0 + cu;
+  const int bg = b0 + cb;
+  const bool cval = ct && cj < H && bg < a.B;
+  float bh[NGATE];
+#pragma unroll
+  for (int q = 0; q < NGATE; ++q) bh[q] = cval ? a.bhh[(long long)d * GH + q * H + cj] : 0.0f;
+  float hst = 0.0f, cst = 0.0f;
+
+  // granules of this group: [2 slots][fast, safe][BC][NG][8] x 8 B
+  const int slot_g = BC * NG * 8;
+  u64* xg = a.xbuf + (long long)group * 4 * slot_g;
+  const __amdgpu_buffer_rsrc_t xr = granule_rsrc(xg, (unsigned)(4 * slot_g * 8));
+
+  // ---- prefetch waves 5-7: input projection G[b][t][d][q*H + j] of every own (b, unit, gate)
+  constexpr int NPF = NT - (WPOLL + 1) * 64;  // 192 prefetch lanes
+  constexpr int NQ = (BC * 20 * 4 + NPF - 1) / NPF;
+  StepLoader<NQ> ld;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = tid - (WPOLL + 1) * 64 + q * NPF;  // item = gate * (BC*J) + cell
+    const int gate = i / (BC * J), cell = i % (BC * J);
+    const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
+    const bool on = wv > WPOLL && gate < NGATE;
+    ld.p[q] = (on && ib < a.B && ij < H) ? a.G + ((long long)ib * T * 2 + d) * GH + gate * H + ij : nullptr;
+    ld.stride[q] = 2 * GH;
+    ld.shift[q] = 0;
+    ld.dst[q] = on ? ((cell / J) * 32 + iu) * 4 + gate : -1;
+  }
+  if (wv > WPOLL) ld.issue(d == 0 ? 0 : T - 1, T);
+  __syncthreads();
+  STAMP_DECL
+
+  auto matvec = [&]() {  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
+    if (!mv) return;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const unsigned short* bp = shb + (lane & 15) * SHB + 8 * (lane >> 4);
+    bf16x8 bv[KSMAX];
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ks += 2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[ks], bv[ks], acc0, 0, 0, 0);
+      if (ks + 1 < KSMAX) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[ks + 1], bv[ks + 1], acc1, 0, 0, 0);
+    }
+    const int col = lane & 15;
+    if (col < BC) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sgate[col * MT * 16 + tile * 16 + (lane >> 4) * 4 + i] = acc0[i] + acc1[i];
+    }
+  };
+
+  if (wv == WPOLL) {
+    // ---- polling wave: 16-B unit idx = (b * NG + producer) * 4 + pair; lane holds
+    //      units lane + 64 g (idle lanes re-read unit 0: every load is unconditional,
+    //      so the compiler can keep a sweep in flight behind a counted vmcnt)
+    constexpr int GLK = BC;  // BC * NG * 4 <= 64 * BC  (NG <= 16, checked by the plan)
+    const int n16 = BC * NG * 4;
+    int loff[GLK], doff[GLK], dlim[GLK];
+#pragma unroll
+    for (int g = 0; g < GLK; ++g) {
+      const int idx = lane + 64 * g;
+      const bool on = idx < n16;
+      const int b = idx / (NG * 4), pw = (idx / 4) % NG, pp = idx % 4;
+      const int k0 = pw * J + 6 * pp;
+      loff[g] = on ? idx * 16 : 0;
+      doff[g] = on ? b * SHB + k0 : 0;
+      dlim[g] = on ? max(0, min(min(6, J - 6 * pp), H - k0)) : 0;
+    }
+#ifdef DBG_SAFE_ONLY  // diagnostic build (tools/variant_lib.py safe -DDBG_SAFE_ONLY): the fallback copy only
+    bool safe = true;
+#else
+    bool safe = false;  // sticky: once the fast copy stalls, the rest of the launch polls the safe copy
+#endif
+    for (int s = 0; s < T; ++s) {
+      if (s > 0) {
+        const unsigned tag = (unsigned)s & 0xFFFFu;
+        const int base = ((s - 1) & 1) * 2 * slot_g * 8;  // fast copy of the slot (bytes)
+        TRACE(2, s);
+        // two sweeps in flight: the older one is merged while the newer one travels;
+        // a pair is taken from the first sweep that shows both its tags.  Relaxed agent
+        // atomic 8-B loads (global_load_dwordx2 sc1): unlike the buffer intrinsics they
+        // are never hoisted out of the spin loop or merged by the compiler.
+        const u64* src = xg + (base >> 3) + (safe ? slot_g : 0);
+        u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
+        unsigned done = 0;
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) {
+          alo[g] = get_granule(src + (loff[g] >> 3));
+          ahi[g] = get_granule(src + (loff[g] >> 3) + 1);
+        }
+        unsigned spins = 0;
+        while (true) {
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            blo[g] = get_granule(src + (loff[g] >> 3));
+            bhi[g] = get_granule(src + (loff[g] >> 3) + 1);
+          }
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((unsigned)(alo[g] >> 48) == tag) & ((unsigned)(ahi[g] >> 48) == tag) & !((done >> g) & 1);
+            lo[g] = m ? alo[g] : lo[g];
+            hi[g] = m ? ahi[g] : hi[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+#ifdef RNN_TRACE
+          if (spins == 0) TRACE(3, s);
+#endif
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            alo[g] = get_granule(src + (loff[g] >> 3));
+            ahi[g] = get_granule(src + (loff[g] >> 3) + 1);
+          }
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((unsigned)(blo[g] >> 48) == tag) & ((unsigned)(bhi[g] >> 48) == tag) & !((done >> g) & 1);
+            lo[g] = m ? blo[g] : lo[g];
+            hi[g] = m ? bhi[g] : hi[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+          if (++spins > SPIN_LIMIT) {
+            atomicOr(a.status, 1);
+            return;
+          }
+          if (spins == FAST_SPINS && !safe) {  // the fast copy is not reaching this CU: poll the safe one
+            safe = true;
+            src += slot_g;
+          }
+        }
+        u32x4 v[GLK];
+#pragma unroll
+        for (int g = 0; g < GLK; ++g)
+          v[g] = u32x4{(unsigned)lo[g], (unsigned)(lo[g] >> 32), (unsigned)hi[g], (unsigned)(hi[g] >> 32)};
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) {
+          const u32x4 x = v[g];
+          unsigned* dst = reinterpret_cast<unsigned*>(shb + doff[g]);  // 4-B aligned: J, H, SHB even
+          const int nv = dlim[g];
+          if (nv > 0) dst[0] = x.x;
+          if (nv > 2) dst[1] = (x.y & 0xFFFFu) | (x.z << 16);
+          if (nv > 4) dst[2] = (x.z >> 16) | (x.w << 16);
+        }
+        TRACE(1, s);
+      }
+      STAMP(0)
+      __syncthreads();  // B1
+      STAMP(1)
+      STAMP(2)
+      __syncthreads();  // B2
+      STAMP(3)
+    }
+    STAMP_FLUSH
+    return;
+  }
+  if (wv > WPOLL) {
+    for (int s = 0; s < T; ++s) {
+      ld.commit(sin + (s & 1) * BC * 32 * 4);
+      if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
+      __syncthreads();  // B1
+      matvec();
+      __syncthreads();  // B2
+    }
+    return;
+  }
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? s : T - 1 - s;
+    STAMP(0)
+    __syncthreads();  // B1
+    STAMP(1)
+    matvec();
+    STAMP(2)
+    __syncthreads();  // B2
+    STAMP(3)
+    if (tid < BC * 32) {
+      float hn = 0.0f, st[4] = {0.f, 0.f, 0.f, 0.f};
+      if (cval) {
+        float hg[NGATE], gx[NGATE];
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) {
+          hg[q] = bh[q] + sgate[cb * MT * 16 + q * J + cu];
+          gx[q] = sin[(s & 1) * BC * 32 * 4 + tid * 4 + q];
+        }
+        if constexpr (CELL == CELL_LSTM) {
+          const float ig = fsig(gx[0] + hg[0]);
+          const float fg = fsig(gx[1] + hg[1]);
+          const float gg = ftanh(gx[2] + hg[2]);
+          const float og = fsig(gx[3] + hg[3]);
+          cst = fg * cst + ig * gg;
+          hn = og * ftanh(cst);
+          st[0] = ig; st[1] = fg; st[2] = gg; st[3] = og;
+        } else {
+          const float rg = fsig(gx[0] + hg[0]);
+          const float zg = fsig(gx[1] + hg[1]);
+          const float ng = ftanh(gx[2] + rg * hg[2]);
+          hn = (1.0f - zg) * ng + zg * hst;
+          st[0] = rg; st[1] = zg; st[2] = ng; st[3] = hg[2];
+        }
+      }
+      // stage bf16 h (padded rows / units >= H stage zeros) and publish: lanes 0-3 of
+      // each row read 6 staged values (LDS is in order within the wave) and store two
+      // tagged granules with one 16-B write-through store
+      if (ct) spub[cb * PKU + cu] = bf16_rne(hn);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (cu < 4) {
+        const unsigned* sp = reinterpret_cast<const unsigned*>(spub + cb * PKU + 6 * cu);
+        const unsigned w01 = sp[0], w23 = sp[1], w45 = sp[2];
+        const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
+        const u32x4 x = {w01, (w23 & 0xFFFFu) | (tag << 16), (w23 >> 16) | (w45 << 16), (w45 >> 16) | (tag << 16)};
+        const int off = ((s & 1) * 2 * slot_g + (cb * NG + w) * 8 + 2 * cu) * 8;
+#ifndef DBG_SAFE_ONLY
+        __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);               // fast: plain, stays in L2
+#endif
+        __builtin_amdgcn_raw_buffer_store_b128(x, xr, off + slot_g * 8, 0, 16);  // safe: sc1 write-through
+      }
+      if (tid == 0) TRACE(0, s);
+      if (cval) {
+        const long long bt = (long long)bg * T + t;
+        float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
+        actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
+        if constexpr (CELL == CELL_LSTM) a.cs[(bt * 2 + d) * H + cj] = cst;
+        a.hprev[bt * 2 * H + d * H + cj] = hst;
+        a.out[bt * 2 * H + d * H + cj] = hn;
+      }
+      hst = hn;
+    }
+    STAMP(4)
   }
   STAMP_FLUSH
 }
@@ -634,9 +949,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
           if (goff[g] >= 0) sdh[tid - NROLE + g * NROLE] = __uint_as_float((unsigned)v[g]);
       }
       ld.commit(sop + (s & 1) * BC * J * 8);
-#ifndef RNN_EXP_NOPF
       if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
-#endif
       STAMP(0)
       __syncthreads();  // B1
       STAMP(1)
@@ -704,10 +1017,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
         }
         const long long bt = (long long)bg * T + t;
         float* dgp = a.dG + (bt * 2 + d) * GH + cj;
-#ifndef RNN_EXP_NOSAVE
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) dgp[q * H] = dgi[q];
-#endif
         if (CELL == CELL_GRU) {
           float* dhp = a.dGh + (bt * 2 + d) * GH + cj;
 #pragma unroll
@@ -772,6 +1083,8 @@ struct Plan {
   int KP, KPL, HP, RP, RPL, KG, KGL;
   size_t smem_fwd, smem_bwd;        // fp32 VALU matvec
   size_t smem_fwd_mf, smem_bwd_mf;  // bf16 MFMA matvec
+  bool fwd_pk;                       // packed hand-off forward (rnn_fwd_pk_kernel) applies
+  size_t smem_fwd_pk;
 };
 
 bool make_plan(int cell, int B, int H, Plan& p) {
@@ -813,15 +1126,19 @@ bool make_plan(int cell, int B, int H, Plan& p) {
     const int SHB = HMAX + 8, MT = (R + 15) / 16, SDG = (4 * 20 + 31) / 32 * 32 + 8;
     p.smem_fwd_mf = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * J * 4);
     p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
+    p.fwd_pk = J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= 7;
+    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
     return true;
   }
   return false;
 }
 
 template <int CELL, int BC>
-void launch_fwd(const RnnArgs& a, bool mf, int grid, size_t smem, hipStream_t st) {
+void launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
   // compile-time k-slice lengths for the shipped H = 300 plans (LSTM J=20: 52, GRU J=20: 40)
-  if (mf)
+  if (mf && pk)
+    hipLaunchKernelGGL((rnn_fwd_pk_kernel<CELL, BC>), dim3(grid), dim3(NT), smem, st, a);
+  else if (mf)
     hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, true>), dim3(grid), dim3(NT), smem, st, a);
   else if (a.KPL == 52)
     hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 52, false>), dim3(grid), dim3(NT), smem, st, a);
@@ -845,24 +1162,24 @@ void launch_bwd(const RnnArgs& a, bool mf, int grid, size_t smem, hipStream_t st
 }
 
 template <int CELL>
-int dispatch(bool fwd, bool mf, int BC, const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
+int dispatch(bool fwd, bool mf, bool pk, int BC, const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
   switch (BC) {
-    case 1: fwd ? launch_fwd<CELL, 1>(a, mf, grid, smem, st) : launch_bwd<CELL, 1>(a, mf, grid, smem, st); break;
-    case 2: fwd ? launch_fwd<CELL, 2>(a, mf, grid, smem, st) : launch_bwd<CELL, 2>(a, mf, grid, smem, st); break;
-    case 4: fwd ? launch_fwd<CELL, 4>(a, mf, grid, smem, st) : launch_bwd<CELL, 4>(a, mf, grid, smem, st); break;
-    case 8: fwd ? launch_fwd<CELL, 8>(a, mf, grid, smem, st) : launch_bwd<CELL, 8>(a, mf, grid, smem, st); break;
+    case 1: fwd ? launch_fwd<CELL, 1>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 1>(a, mf, grid, smem, st); break;
+    case 2: fwd ? launch_fwd<CELL, 2>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 2>(a, mf, grid, smem, st); break;
+    case 4: fwd ? launch_fwd<CELL, 4>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 4>(a, mf, grid, smem, st); break;
+    case 8: fwd ? launch_fwd<CELL, 8>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 8>(a, mf, grid, smem, st); break;
     default: return (int)hipErrorInvalidValue;
   }
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
 
-#ifdef RNN_STAMPS
+#if defined(RNN_STAMPS) || defined(RNN_TRACE)
 u64* g_stamps = nullptr;
 #endif
 
 void fill_args(RnnArgs& a, const Plan& p, int B, int T, int H) {
-#ifdef RNN_STAMPS
+#if defined(RNN_STAMPS) || defined(RNN_TRACE)
   a.stamps = g_stamps;
 #endif
   a.B = B; a.T = T; a.H = H; a.J = p.J; a.NG = p.NG; a.nchunk = p.nchunk;
@@ -872,7 +1189,7 @@ void fill_args(RnnArgs& a, const Plan& p, int B, int T, int H) {
 
 }  // namespace
 
-#ifdef RNN_STAMPS
+#if defined(RNN_STAMPS) || defined(RNN_TRACE)
 DL4SS_API void dl4ss_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
 #endif
 
@@ -880,7 +1197,9 @@ DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
   Plan p;
   if (!make_plan(cell, B, H, p)) return -1;
   const long long groups = 2LL * p.nchunk;
-  const long long fwd = groups * 2 * p.BC * H * 8;
+  long long fwd = groups * 2 * p.BC * H * 8;
+  const long long fwd_pk = groups * 4 * p.BC * p.NG * 8 * 8;
+  if (fwd_pk > fwd) fwd = fwd_pk;
   const long long bwd = groups * 2 * p.NG * p.BC * H * 8;
   return fwd > bwd ? fwd : bwd;
 }
@@ -897,7 +1216,9 @@ DL4SS_API int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, cons
   DL4SS_REQUIRE(ws_bytes >= dl4ss_birnn_workspace_bytes(cell, B, H));
   hipStream_t st = as_stream(stream);
   const long long groups = 2LL * p.nchunk;
-  hipError_t e = hipMemsetAsync(workspace, 0, groups * 2 * p.BC * H * 8, st);
+  const bool mf = precision == 1;
+  const bool pk = mf && p.fwd_pk && T < 65535;
+  hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.BC * p.NG * 8 * 8 : groups * 2 * p.BC * H * 8, st);
   if (e != hipSuccess) return (int)e;
   RnnArgs a{};
   fill_args(a, p, B, T, H);
@@ -905,10 +1226,9 @@ DL4SS_API int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, cons
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
   a.status = status;
   const int grid = (int)(groups * p.NG);
-  const bool mf = precision == 1;
-  const size_t smem = mf ? p.smem_fwd_mf : p.smem_fwd;
-  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, mf, p.BC, a, grid, smem, st)
-                           : dispatch<CELL_GRU>(true, mf, p.BC, a, grid, smem, st);
+  const size_t smem = pk ? p.smem_fwd_pk : mf ? p.smem_fwd_mf : p.smem_fwd;
+  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, mf, pk, p.BC, a, grid, smem, st)
+                           : dispatch<CELL_GRU>(true, mf, pk, p.BC, a, grid, smem, st);
 }
 
 DL4SS_API int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, const float* dOut, const float* dOut_bcast,
@@ -934,6 +1254,6 @@ DL4SS_API int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, cons
   const int grid = (int)(groups * p.NG);
   const bool mf = precision == 1;
   const size_t smem = mf ? p.smem_bwd_mf : p.smem_bwd;
-  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, p.BC, a, grid, smem, st)
-                           : dispatch<CELL_GRU>(false, mf, p.BC, a, grid, smem, st);
+  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, false, p.BC, a, grid, smem, st)
+                           : dispatch<CELL_GRU>(false, mf, false, p.BC, a, grid, smem, st);
 }

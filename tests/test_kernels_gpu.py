@@ -192,9 +192,9 @@ def _manual_birnn(cell, G, whh, bhh, H, bf16=False):
 def test_birnn_bwd_dG_per_step(dev, cell, B, T, H, prec):
     """prec 0: exact fp32 recurrence vs fp64 (1e-5 abs on h, 1e-4 rel on dG).
     prec 1: bf16-operand MFMA recurrence vs an fp64 recurrence with the same operand
-    rounding (_Bf16MatVec); tolerance 1e-3 abs on h, 2e-3 rel on dG (fp32 vs fp64
-    accumulation can flip an operand's bf16 rounding, 2^-9 relative, which then
-    propagates through the recurrence)."""
+    rounding (_Bf16MatVec); tolerance 3e-3 abs on h, 2e-3 rel on dG (fp32 vs fp64
+    accumulation can flip an operand's bf16 rounding: one flip moves that h value by
+    2^-9 |h| <= 2e-3, which then propagates through the recurrence)."""
     ng = 4 if cell == "lstm" else 3
     NGH = ng * H
     g = torch.Generator().manual_seed(B * 31 + T)
@@ -205,7 +205,7 @@ def test_birnn_bwd_dG_per_step(dev, cell, B, T, H, prec):
     bl = bhh.clone().requires_grad_(True)
     out = _manual_birnn(cell, Gl, whh, bl, H, bf16=prec == 1)
     gout = torch.randn(out.shape, generator=g, dtype=torch.float64)
-    tol_h, tol_g = (1e-5, 1e-4) if prec == 0 else (1e-3, 2e-3)
+    tol_h, tol_g = (1e-5, 1e-4) if prec == 0 else (3e-3, 2e-3)
     (out * gout).sum().backward()
     cellid = 0 if cell == "lstm" else 1
     Gd = G.float().to(dev).contiguous()

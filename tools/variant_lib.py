@@ -1,0 +1,34 @@
+"""Experiment helper: build a variant of libdl4ss_hip.so with extra -D flags.
+
+  python tools/variant_lib.py TAG -DFOO -DBAR   ->  dl4ss_amd/libdl4ss_hip_TAG.so
+Use it with DL4SS_LIB=dl4ss_amd/libdl4ss_hip_TAG.so (never the shipped library)."""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from dl4ss_amd import build as B  # noqa: E402
+
+
+def main(tag, defs):
+    od = f"/tmp/variant_obj_{tag}"
+    os.makedirs(od, exist_ok=True)
+    srcs = sorted(f for f in os.listdir(B.CSRC) if f.endswith(".hip"))
+
+    def comp(f):
+        o = f"{od}/{f[:-4]}.o"
+        subprocess.run([B.HIPCC, *B.FLAGS, *B.FILE_FLAGS.get(f, []), *defs, "-I", B.CSRC, "-c",
+                        os.path.join(B.CSRC, f), "-o", o], check=True)
+        return o
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        objs = list(ex.map(comp, srcs))
+    lib = os.path.join(ROOT, "dl4ss_amd", f"libdl4ss_hip_{tag}.so")
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", lib], check=True)
+    print(lib)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2:])
