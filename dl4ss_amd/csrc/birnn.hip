@@ -1066,6 +1066,321 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
   STAMP_FLUSH
 }
 
+// --------------------------------------------------------------------------
+// BPTT, bf16 MFMA mode with the packed hand-off (the throughput path; see the
+// packed forward above for the measurements behind each choice).  What crosses
+// workgroups per step are the partial sums P_w[b][k] = sum_{own rows r} dgh[b][r]
+// W[r][k]; they are packed as 24-bit floats (fp32 rounded to 15 mantissa bits,
+// relative error <= 2^-16, far below the bf16 rounding of dgh itself), two per
+// tagged 8-B granule:
+//   granule = { lo: p0 | (p1 & 0xFF) << 24, hi: (p1 >> 8) | tag << 16 }
+// one 16-B store per 4 units (two granules), fast (plain) + safe (`sc1`) copies,
+// buffer [slot][copy][producer][b][HG granules], HG = H/2 rounded up to even.
+// Waves: 0-3 cell backward (rows b = tid/32) + MFMA W^T dgh + publish;
+//        4 polls the NG producers' partials of the own J units into LDS;
+//        5-7 per-step operand prefetch.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ unsigned pack24(float v) {
+  const unsigned u = __float_as_uint(v);
+  return (u + 0x80u) >> 8;  // round to nearest (ties away) on the dropped 8 bits
+}
+__device__ __forceinline__ float unpack24(unsigned r) { return __uint_as_float(r << 8); }
+
+template <int CELL, int BC>
+__global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
+  constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
+  constexpr int MTWMAX = (HMAX / 16 + 3) / 4;  // MFMA unit tiles per wave (5)
+  constexpr int KSRMAX = (4 * 20 + 31) / 32;   // MFMA K-steps over gate rows (3)
+  constexpr int SDG = KSRMAX * 32 + 8;         // bf16 row stride of the dgh B image
+  constexpr int WSPAN = MTWMAX * 16;           // output units per MFMA wave (80)
+  const int H = a.H, T = a.T, J = a.J, NG = a.NG;
+  const int R = NGATE * J;
+  const int ngroups = 2 * a.nchunk;
+  int group, w;
+  group_of(blockIdx.x, NG, ngroups, group, w);
+  const int d = group / a.nchunk, chunk = group % a.nchunk;
+  const int b0 = chunk * BC;
+  const int j0 = w * J;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int GH = NGATE * H;
+  const int AH = 4 * H;
+  const int HG = ((H + 1) / 2 + 1) & ~1;  // granules per (producer, row), even: 16-B aligned rows
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  unsigned short* sdgb = reinterpret_cast<unsigned short*>(smem);  // [16][SDG] bf16 dgh B image
+  float* sdh = smem + 8 * SDG;                                      // [NG][BC][J] gathered partials
+  float* wsc = sdh + ((NG * BC * J + 3) & ~3);                      // [4 waves][BC][WSPAN]
+  float* sop = wsc + 4 * BC * WSPAN;                                // [2][BC*32][8] per-step operands
+  for (int i = tid; i < 8 * SDG + NG * BC * J; i += NT) smem[i] = 0.0f;
+
+  // ---- W_hh^T tiles (waves 0-3): tile m = wv*MTWMAX + t, lane holds
+  //      A[k = m*16 + (lane&15)][r = ks*32 + 8(lane>>4) + j] = W[row(r)][k]
+  const bool mv = wv < 4;
+  bf16x8 afr[MTWMAX][KSRMAX];
+#pragma unroll
+  for (int t = 0; t < MTWMAX; ++t) {
+    const int k = (wv * MTWMAX + t) * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < KSRMAX; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rr = ks * 32 + 8 * (lane >> 4) + j;
+        const int q = rr / J, u = rr % J;
+        const bool ok = mv && k < H && rr < R && j0 + u < H;
+        afr[t][ks][j] = (short)bf16_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
+      }
+  }
+
+  // ---- cell lanes: row cb = tid / 32, unit cu = tid % 32 (< J)
+  const int cb = tid >> 5, cu = tid & 31;
+  const bool ct = tid < BC * 32 && cu < J;
+  const int cj = j0 + cu;
+  const int bg = b0 + cb;
+  const bool cval = ct && cj < H && bg < a.B;
+  float dc_next = 0.0f, dh_dir = 0.0f;
+  const float doutb = (cval && a.dOutB) ? a.dOutB[(long long)bg * 2 * H + d * H + cj] : 0.0f;
+
+  // partial-sum granules of this group: [2 slots][fast, safe][NG][BC][HG] x 8 B
+  const int copy_g = NG * BC * HG;
+  u64* xg = a.xbuf + (long long)group * 4 * copy_g;
+  const __amdgpu_buffer_rsrc_t xr = granule_rsrc(xg, (unsigned)(4 * copy_g * 8));
+
+  // ---- prefetch waves 5-7: per-step operands of every own (b, unit): 8 slots per cell
+  //   0 dOut, 1..4 act, 5 c (LSTM) / h_prev (GRU), 6 c_prev (LSTM), 7 unused
+  constexpr int NPF = NT - (WPOLL + 1) * 64;
+  constexpr int NQ = (BC * 20 * 8 + NPF - 1) / NPF;
+  StepLoader<NQ> ld;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = tid - (WPOLL + 1) * 64 + q * NPF;  // item = slot * (BC*J) + cell
+    const int slot = i / (BC * J), cell = i % (BC * J);
+    const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
+    const bool on = wv > WPOLL && slot < 8;
+    const bool valid = on && ib < a.B && ij < H;
+    const float* p = nullptr;
+    int stride = 2 * H, shift = 0;
+    if (valid) {
+      if (slot == 0) {
+        p = a.dOut + (long long)ib * T * 2 * H + d * H + ij;
+      } else if (slot <= 4) {
+        p = a.act + ((long long)ib * T * 2 + d) * AH + (slot - 1) * H + ij;
+        stride = 2 * AH;
+      } else if (CELL == CELL_LSTM && (slot == 5 || slot == 6)) {
+        p = a.cs + ((long long)ib * T * 2 + d) * H + ij;
+        shift = slot == 6 ? (d == 0 ? -1 : 1) : 0;
+      } else if (CELL == CELL_GRU && slot == 5) {
+        p = a.hprev + (long long)ib * T * 2 * H + d * H + ij;
+      }
+    }
+    ld.p[q] = p;
+    ld.stride[q] = stride;
+    ld.shift[q] = shift;
+    ld.dst[q] = on ? ((cell / J) * 32 + iu) * 8 + slot : -1;
+  }
+  if (wv > WPOLL) ld.issue(d == 0 ? T - 1 : 0, T);
+  __syncthreads();
+  STAMP_DECL
+
+  if (wv == WPOLL) {
+    // ---- polling wave: 16-B unit idx = (producer * BC + b) * (J/4) + quad
+    constexpr int GLK = (80 * BC + 63) / 64;  // NG <= 16, J <= 20
+    const int JQ = J / 4;
+    const int n16 = NG * BC * JQ;
+    int loff[GLK], doff[GLK];
+    bool on[GLK];
+#pragma unroll
+    for (int g = 0; g < GLK; ++g) {
+      const int idx = lane + 64 * g;
+      on[g] = idx < n16;
+      const int pb = idx / JQ, qd = idx % JQ;  // pb = producer * BC + b
+      loff[g] = on[g] ? pb * HG + (j0 >> 1) + 2 * qd : 0;  // granule offset within a copy
+      doff[g] = on[g] ? pb * J + 4 * qd : 0;               // sdh[(p * BC + b) * J + u]
+    }
+    bool safe = false;
+    for (int s = 0; s < T; ++s) {
+      if (s > 0) {
+        const unsigned tag = (unsigned)s & 0xFFFFu;
+        const u64* src = xg + ((s - 1) & 1) * 2 * copy_g + (safe ? copy_g : 0);
+        u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
+        unsigned done = 0;
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) {
+          alo[g] = get_granule(src + loff[g]);
+          ahi[g] = get_granule(src + loff[g] + 1);
+        }
+        unsigned spins = 0;
+        while (true) {
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            blo[g] = get_granule(src + loff[g]);
+            bhi[g] = get_granule(src + loff[g] + 1);
+          }
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((unsigned)(alo[g] >> 48) == tag) & ((unsigned)(ahi[g] >> 48) == tag) & !((done >> g) & 1);
+            lo[g] = m ? alo[g] : lo[g];
+            hi[g] = m ? ahi[g] : hi[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            alo[g] = get_granule(src + loff[g]);
+            ahi[g] = get_granule(src + loff[g] + 1);
+          }
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((unsigned)(blo[g] >> 48) == tag) & ((unsigned)(bhi[g] >> 48) == tag) & !((done >> g) & 1);
+            lo[g] = m ? blo[g] : lo[g];
+            hi[g] = m ? bhi[g] : hi[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+          if (++spins > SPIN_LIMIT) {
+            atomicOr(a.status, 2);
+            return;
+          }
+          if (spins == FAST_SPINS && !safe) {
+            safe = true;
+            src += copy_g;
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) {
+          if (on[g]) {
+            const unsigned l0 = (unsigned)lo[g], l1 = (unsigned)(lo[g] >> 32);
+            const unsigned h0 = (unsigned)hi[g], h1 = (unsigned)(hi[g] >> 32);
+            const float4 v = make_float4(unpack24(l0 & 0xFFFFFFu), unpack24((l0 >> 24) | ((l1 & 0xFFFFu) << 8)),
+                                         unpack24(h0 & 0xFFFFFFu), unpack24((h0 >> 24) | ((h1 & 0xFFFFu) << 8)));
+            *reinterpret_cast<float4*>(sdh + doff[g]) = v;  // 16-B aligned: J % 4 == 0
+          }
+        }
+      }
+      STAMP(0)
+      __syncthreads();  // B1
+      STAMP(1)
+      __syncthreads();  // B2
+      STAMP(3)
+      if (s + 1 == T) break;
+    }
+    STAMP_FLUSH
+    return;
+  }
+  if (wv > WPOLL) {
+    for (int s = 0; s < T; ++s) {
+      ld.commit(sop + (s & 1) * BC * 32 * 8);
+      if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+      __syncthreads();  // B1
+      __syncthreads();  // B2
+      if (s + 1 == T) break;
+    }
+    return;
+  }
+
+  // ---- waves 0-3: cell backward, then MFMA partials and their publish
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    STAMP(0)
+    __syncthreads();  // B1
+    STAMP(1)
+    if (tid < BC * 32) {
+      float dgi[NGATE], dgh[NGATE];
+#pragma unroll
+      for (int q = 0; q < NGATE; ++q) dgi[q] = dgh[q] = 0.0f;
+      if (cval) {
+        float dh_rec = 0.0f;
+        if (s > 0)
+          for (int p = 0; p < NG; ++p) dh_rec += sdh[(p * BC + cb) * J + cu];
+        const float* op = sop + (s & 1) * BC * 32 * 8 + tid * 8;
+        const float dout = op[0] + doutb;
+        const float act[4] = {op[1], op[2], op[3], op[4]};
+        const float c = op[5], cprev = op[6], hprev = op[5];
+        const float dh = dout + dh_rec + dh_dir;
+        if constexpr (CELL == CELL_LSTM) {
+          const float ig = act[0], fg = act[1], gg = act[2], og = act[3];
+          const float tc = ftanh(c);
+          const float dc = dc_next + dh * og * (1.0f - tc * tc);
+          dgi[0] = dc * gg * ig * (1.0f - ig);
+          dgi[1] = dc * cprev * fg * (1.0f - fg);
+          dgi[2] = dc * ig * (1.0f - gg * gg);
+          dgi[3] = dh * tc * og * (1.0f - og);
+          dc_next = dc * fg;
+#pragma unroll
+          for (int q = 0; q < NGATE; ++q) dgh[q] = dgi[q];
+        } else {
+          const float rg = act[0], zg = act[1], ng = act[2], hn = act[3];
+          const float dn = dh * (1.0f - zg);
+          const float dz = dh * (hprev - ng);
+          dh_dir = dh * zg;
+          const float dnp = dn * (1.0f - ng * ng);
+          const float dr = dnp * hn;
+          dgi[0] = dr * rg * (1.0f - rg);
+          dgi[1] = dz * zg * (1.0f - zg);
+          dgi[2] = dnp;
+          dgh[0] = dgi[0];
+          dgh[1] = dgi[1];
+          dgh[2] = dnp * rg;
+        }
+        const long long bt = (long long)bg * T + t;
+        float* dgp = a.dG + (bt * 2 + d) * GH + cj;
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) dgp[q * H] = dgi[q];
+        if (CELL == CELL_GRU) {
+          float* dhp = a.dGh + (bt * 2 + d) * GH + cj;
+#pragma unroll
+          for (int q = 0; q < NGATE; ++q) dhp[q * H] = dgh[q];
+        }
+      }
+      if (ct) {
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) sdgb[cb * SDG + q * J + cu] = bf16_rne(dgh[q]);
+      }
+    }
+    STAMP(2)
+    __syncthreads();  // B2
+    STAMP(3)
+    if (s + 1 == T) break;  // nothing flows past the sequence start
+    // ---- D[k][b] = sum_r W[r][k] dgh[b][r] per 16-unit tile, transposed through
+    //      wave-private LDS to [b][unit], packed four units per 16-B store
+    {
+      const unsigned short* bp = sdgb + (lane & 15) * SDG + 8 * (lane >> 4);
+      bf16x8 bv[KSRMAX];
+#pragma unroll
+      for (int ks = 0; ks < KSRMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
+      float* wsw = wsc + wv * BC * WSPAN;
+      const int col = lane & 15;
+#pragma unroll
+      for (int t2 = 0; t2 < MTWMAX; ++t2) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KSRMAX; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t2][ks], bv[ks], acc, 0, 0, 0);
+        if (col < BC) *reinterpret_cast<f32x4*>(wsw + col * WSPAN + t2 * 16 + 4 * (lane >> 4)) = acc;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      STAMP(4)
+      const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
+      constexpr int NQW = BC * WSPAN / 4;  // 16-B quads of this wave
+#pragma unroll
+      for (int e0 = 0; e0 < NQW; e0 += 64) {
+        const int e = e0 + lane;
+        const int bb = e / (WSPAN / 4), k = wv * WSPAN + 4 * (e % (WSPAN / 4));
+        if ((NQW % 64 == 0 || e < NQW) && k < H) {
+          const float4 v = *reinterpret_cast<const float4*>(wsw + bb * WSPAN + (k - wv * WSPAN));
+          const unsigned r0 = pack24(v.x), r1 = pack24(v.y), r2 = pack24(v.z), r3 = pack24(v.w);
+          const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
+          const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules, fast copy
+          __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);                // fast: plain
+          __builtin_amdgcn_raw_buffer_store_b128(x, xr, (off + copy_g) * 8, 0, 16);    // safe: sc1
+        }
+      }
+    }
+    STAMP(6)
+  }
+  STAMP_FLUSH
+}
+
 // compile-time (rows, k) per thread of the BPTT matvec: the shipped H = 300 plans
 // (LSTM R=80: 20 x 3, GRU R=60: 20 x 2) and the generic (guard-free, zero-padded) maxima
 void bwd_dims(int rpl, int kgl, int& rpln, int& kgln) {
@@ -1085,6 +1400,8 @@ struct Plan {
   size_t smem_fwd_mf, smem_bwd_mf;  // bf16 MFMA matvec
   bool fwd_pk;                       // packed hand-off forward (rnn_fwd_pk_kernel) applies
   size_t smem_fwd_pk;
+  bool bwd_pk;                       // packed hand-off BPTT (rnn_bwd_pk_kernel) applies
+  size_t smem_bwd_pk;
 };
 
 bool make_plan(int cell, int B, int H, Plan& p) {
@@ -1127,6 +1444,8 @@ bool make_plan(int cell, int B, int H, Plan& p) {
     p.smem_fwd_mf = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * J * 4);
     p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
     p.fwd_pk = J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= 7;
+    p.bwd_pk = J % 4 == 0 && H % 4 == 0 && NG <= 16;
+    p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((NG * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16) + 2 * BC * 32 * 8);
     p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
     return true;
   }
@@ -1148,10 +1467,12 @@ void launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipSt
     hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, false>), dim3(grid), dim3(NT), smem, st, a);
 }
 template <int CELL, int BC>
-void launch_bwd(const RnnArgs& a, bool mf, int grid, size_t smem, hipStream_t st) {
+void launch_bwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
   int rpln, kgln;
   bwd_dims(a.RPL, a.KGL, rpln, kgln);
-  if (mf)
+  if (mf && pk)
+    hipLaunchKernelGGL((rnn_bwd_pk_kernel<CELL, BC>), dim3(grid), dim3(NT), smem, st, a);
+  else if (mf)
     hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 0, 0, true>), dim3(grid), dim3(NT), smem, st, a);
   else if (rpln == 20 && kgln == 3)
     hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 20, 3, false>), dim3(grid), dim3(NT), smem, st, a);
@@ -1164,10 +1485,10 @@ void launch_bwd(const RnnArgs& a, bool mf, int grid, size_t smem, hipStream_t st
 template <int CELL>
 int dispatch(bool fwd, bool mf, bool pk, int BC, const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
   switch (BC) {
-    case 1: fwd ? launch_fwd<CELL, 1>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 1>(a, mf, grid, smem, st); break;
-    case 2: fwd ? launch_fwd<CELL, 2>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 2>(a, mf, grid, smem, st); break;
-    case 4: fwd ? launch_fwd<CELL, 4>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 4>(a, mf, grid, smem, st); break;
-    case 8: fwd ? launch_fwd<CELL, 8>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 8>(a, mf, grid, smem, st); break;
+    case 1: fwd ? launch_fwd<CELL, 1>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 1>(a, mf, pk, grid, smem, st); break;
+    case 2: fwd ? launch_fwd<CELL, 2>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 2>(a, mf, pk, grid, smem, st); break;
+    case 4: fwd ? launch_fwd<CELL, 4>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 4>(a, mf, pk, grid, smem, st); break;
+    case 8: fwd ? launch_fwd<CELL, 8>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 8>(a, mf, pk, grid, smem, st); break;
     default: return (int)hipErrorInvalidValue;
   }
   DL4SS_CHECK_LAUNCH();
@@ -1200,7 +1521,9 @@ DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
   long long fwd = groups * 2 * p.BC * H * 8;
   const long long fwd_pk = groups * 4 * p.BC * p.NG * 8 * 8;
   if (fwd_pk > fwd) fwd = fwd_pk;
-  const long long bwd = groups * 2 * p.NG * p.BC * H * 8;
+  long long bwd = groups * 2 * p.NG * p.BC * H * 8;
+  const long long bwd_pk = groups * 4LL * p.NG * p.BC * (((H + 1) / 2 + 1) & ~1) * 8;
+  if (bwd_pk > bwd) bwd = bwd_pk;
   return fwd > bwd ? fwd : bwd;
 }
 
@@ -1243,7 +1566,10 @@ DL4SS_API int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, cons
   DL4SS_REQUIRE(ws_bytes >= dl4ss_birnn_workspace_bytes(cell, B, H));
   hipStream_t st = as_stream(stream);
   const long long groups = 2LL * p.nchunk;
-  hipError_t e = hipMemsetAsync(workspace, 0, groups * 2 * p.NG * p.BC * H * 8, st);
+  const bool mf = precision == 1;
+  const bool pk = mf && p.bwd_pk && T < 65535;
+  const long long HG = ((H + 1) / 2 + 1) & ~1;
+  hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.NG * p.BC * HG * 8 : groups * 2 * p.NG * p.BC * H * 8, st);
   if (e != hipSuccess) return (int)e;
   RnnArgs a{};
   fill_args(a, p, B, T, H);
@@ -1252,8 +1578,7 @@ DL4SS_API int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, cons
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
   a.status = status;
   const int grid = (int)(groups * p.NG);
-  const bool mf = precision == 1;
-  const size_t smem = mf ? p.smem_bwd_mf : p.smem_bwd;
-  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, false, p.BC, a, grid, smem, st)
-                           : dispatch<CELL_GRU>(false, mf, false, p.BC, a, grid, smem, st);
+  const size_t smem = pk ? p.smem_bwd_pk : mf ? p.smem_bwd_mf : p.smem_bwd;
+  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, pk, p.BC, a, grid, smem, st)
+                           : dispatch<CELL_GRU>(false, mf, pk, p.BC, a, grid, smem, st);
 }
