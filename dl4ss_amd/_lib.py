@@ -24,6 +24,13 @@ SIGNATURES = {
     "dl4ss_istft": [P, LL, I, I, I, I, P, P],
     "dl4ss_mix_sources": [P, P, I, I, I, P, P, P, P],
     "dl4ss_gemm": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, P],
+    "dl4ss_gemm_bf16": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, P],
+    "dl4ss_f32_to_bf16": [P, P, LL, P],
+    "dl4ss_f32_to_bf16_2d": [P, LL, I, I, P, LL, P],
+    "dl4ss_colsum_bf16": [P, LL, I, I, P, P],
+    "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
+    "dl4ss_birnn_bwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P],
+    "dl4ss_mask_attn_loss_ex": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
     "dl4ss_birnn_workspace_bytes": [I, I, I],
     "dl4ss_birnn_fwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_bwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, LL, P, P],

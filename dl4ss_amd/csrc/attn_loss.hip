@@ -21,6 +21,7 @@
 // cost matrix per utterance, `pit_select` picks the lowest-index minimising
 // permutation, the GRAD pass uses it; label order (the reference) = identity.
 #include "common.h"
+#include <hip/hip_bf16.h>
 
 namespace {
 
@@ -49,7 +50,9 @@ struct AttnArgs {
   long long ys, yks;
   const int* perm;                // (B, K) target index per channel, null = identity
   float s1, s2;                   // loss scales: MSE term, sum-to-one term
-  float* dPre;                    // (B, T*F, E) GRAD pass output
+  float* dPre;                    // (B, T*F, E) GRAD pass output (fp32; null when dPreB is given)
+  unsigned* dPreB;                // GRAD pass bf16 output: row (b*T + t) of F*E values at stride ldpb (bf16)
+  long long ldpb;
   float* part_loss;               // (B, nblk, K*K + 1)
   float* part_dq;                 // (B, nblk, K, QW)
   float* mask_out;                // optional (B, K, T*F) [cRM: x2]
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
   __shared__ float sdl[GRAD ? TILE * K * NC : 1];  // dL/dlogit per tile row
   float dqa[2] = {0.f, 0.f};  // dq[j] for j = tid, tid + 256 (j < K*QW)
   const float* Vb = a.V + (long long)b * a.rows_per_b * E;
-  float* Db = GRAD ? a.dPre + (long long)b * a.rows_per_b * E : nullptr;
+  float* Db = (GRAD && a.dPre) ? a.dPre + (long long)b * a.rows_per_b * E : nullptr;
 
   for (int r0 = rbeg; r0 < rend; r0 += TILE) {
     const int nr = min(TILE, rend - r0);
@@ -256,7 +259,18 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
         }
       }
     }
-    if constexpr (GRAD) {
+    if (GRAD && a.dPreB) {
+      // bf16 dPre for the Linear's backward GEMMs: pairs (e, e+1) as one 4-B store into
+      // row (b*T + t) of the padded bf16 matrix (E, F*E offsets and ldpb are even)
+      __syncthreads();
+      for (int i = tid; i < nr * E / 2; i += NT) {
+        const int rl = (2 * i) / E, e = (2 * i) % E;
+        const int row = r0 + rl;
+        const int t = row / a.F, f = row - t * a.F;
+        __hip_bfloat162 v2 = __float22bfloat162_rn(make_float2(sv[2 * i], sv[2 * i + 1]));
+        a.dPreB[(((long long)b * a.T + t) * a.ldpb + (long long)f * E + e) >> 1] = *reinterpret_cast<unsigned*>(&v2);
+      }
+    } else if constexpr (GRAD) {
       __syncthreads();
       float* dst = Db + (long long)r0 * E;
       const int n = nr * E;
@@ -399,17 +413,36 @@ DL4SS_API int dl4ss_attn_nblk(int T, int F) {
 }
 
 // pass: 0 = COST (costs / masks only), 1 = GRAD (costs + dPre + dq partials)
+DL4SS_API int dl4ss_mask_attn_loss_ex(int pass, int crm, int B, int K, int T, int F, int E, const float* V,
+                                      const float* q, const float* X, long long x_bstride, const float* Y,
+                                      long long y_bstride, long long y_kstride, const int* perm, float s1, float s2,
+                                      float* dPre, void* dPre_bf16, long long dpre_bf16_ld, float* part_loss,
+                                      float* part_dq, float* mask_out, float* pred_out, void* stream);
+
 DL4SS_API int dl4ss_mask_attn_loss(int pass, int crm, int B, int K, int T, int F, int E, const float* V,
                                    const float* q, const float* X, long long x_bstride, const float* Y,
                                    long long y_bstride, long long y_kstride, const int* perm, float s1, float s2,
                                    float* dPre, float* part_loss, float* part_dq, float* mask_out,
                                    float* pred_out, void* stream) {
+  DL4SS_REQUIRE(pass == 0 || dPre);
+  return dl4ss_mask_attn_loss_ex(pass, crm, B, K, T, F, E, V, q, X, x_bstride, Y, y_bstride, y_kstride, perm, s1, s2,
+                                 dPre, nullptr, 0, part_loss, part_dq, mask_out, pred_out, stream);
+}
+
+DL4SS_API int dl4ss_mask_attn_loss_ex(int pass, int crm, int B, int K, int T, int F, int E, const float* V,
+                                      const float* q, const float* X, long long x_bstride, const float* Y,
+                                      long long y_bstride, long long y_kstride, const int* perm, float s1, float s2,
+                                      float* dPre, void* dPre_bf16, long long dpre_bf16_ld, float* part_loss,
+                                      float* part_dq, float* mask_out, float* pred_out, void* stream) {
   DL4SS_REQUIRE(B > 0 && K >= 1 && K <= 3 && T > 0 && F > 0 && V && q && X && Y && part_loss);
-  DL4SS_REQUIRE(pass == 0 || (dPre && part_dq));
+  DL4SS_REQUIRE(pass == 0 || ((dPre || dPre_bf16) && part_dq));
+  DL4SS_REQUIRE(!dPre_bf16 || (E % 2 == 0 && dpre_bf16_ld % 2 == 0 && dpre_bf16_ld >= (long long)F * E &&
+                               ((uintptr_t)dPre_bf16 & 3) == 0));
   AttnArgs a{};
   a.B = B; a.T = T; a.F = F; a.rows_per_b = T * F; a.nblk = dl4ss_attn_nblk(T, F);
   a.V = V; a.q = q; a.X = X; a.xs = x_bstride; a.Y = Y; a.ys = y_bstride; a.yks = y_kstride;
   a.perm = perm; a.s1 = s1; a.s2 = s2; a.dPre = dPre; a.part_loss = part_loss; a.part_dq = part_dq;
+  a.dPreB = reinterpret_cast<unsigned*>(dPre_bf16); a.ldpb = dpre_bf16_ld;
   a.mask_out = mask_out; a.pred_out = pred_out;
   return dispatch(E, K, crm, pass == 1, a, as_stream(stream));
 }

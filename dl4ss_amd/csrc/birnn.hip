@@ -118,6 +118,13 @@ struct RnnArgs {
   u64* xbuf;             // granules
   int* status;
   u64* stamps;           // diagnostic build only
+  // bf16 mode extras (packed kernels only; any may be null)
+  unsigned short* outb;    // fwd (B,T,2H) bf16(h)          -- next layer's / Linear's GEMM operand
+  unsigned short* hprevb;  // fwd (B,T,2H) bf16(h_{t-1})    -- dW_hh GEMM operand
+  unsigned short* dGb;     // bwd (B,T,2,NGATE*H) bf16(dG)  -- dW_ih / dX GEMM operand
+  unsigned short* dGhb;    // bwd GRU: bf16(dGh)            -- dW_hh GEMM operand
+  float* dbi;              // bwd: += sum_{b,t} dG   (bias_ih gradient, (2, NGATE*H))
+  float* dbh;              // bwd: += sum_{b,t} dGh  (bias_hh gradient)
 };
 
 __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& group, int& w) {
@@ -719,8 +726,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
         actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
         if constexpr (CELL == CELL_LSTM) a.cs[(bt * 2 + d) * H + cj] = cst;
-        a.hprev[bt * 2 * H + d * H + cj] = hst;
-        a.out[bt * 2 * H + d * H + cj] = hn;
+        const long long ho = bt * 2 * H + d * H + cj;
+        if (a.hprev) a.hprev[ho] = hst;
+        a.out[ho] = hn;
+        // bf16 copies, 16-B aligned rows for the GEMMs: out_bf16 (B*T, pad8(2H)) with the
+        // directions adjacent (the next layer's K), hprev_bf16 (B*T, 2 pad8(H)) with each
+        // direction's block 16-B aligned (the per-direction dW_hh operand)
+        const int hp8 = (H + 7) & ~7, op8 = (2 * H + 7) & ~7;
+        if (a.outb) a.outb[bt * op8 + d * H + cj] = bf16_rne(hn);
+        if (a.hprevb) a.hprevb[bt * 2 * hp8 + d * hp8 + cj] = bf16_rne(hst);
       }
       hst = hn;
     }
@@ -1279,6 +1293,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   }
 
   // ---- waves 0-3: cell backward, then MFMA partials and their publish
+  float sbi[NGATE], sbh[NGATE];  // this cell's bias-gradient sums over t
+#pragma unroll
+  for (int q = 0; q < NGATE; ++q) sbi[q] = sbh[q] = 0.0f;
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
     STAMP(0)
@@ -1322,14 +1339,29 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           dgh[1] = dgi[1];
           dgh[2] = dnp * rg;
         }
-        const long long bt = (long long)bg * T + t;
-        float* dgp = a.dG + (bt * 2 + d) * GH + cj;
+        const long long go = (long long)((bg * T + t) * 2 + d) * GH + cj;
+        if (a.dG) {
 #pragma unroll
-        for (int q = 0; q < NGATE; ++q) dgp[q * H] = dgi[q];
+          for (int q = 0; q < NGATE; ++q) a.dG[go + q * H] = dgi[q];
+        }
+        if (a.dGb) {
+#pragma unroll
+          for (int q = 0; q < NGATE; ++q) a.dGb[go + q * H] = bf16_rne(dgi[q]);
+        }
         if (CELL == CELL_GRU) {
-          float* dhp = a.dGh + (bt * 2 + d) * GH + cj;
+          if (a.dGh) {
 #pragma unroll
-          for (int q = 0; q < NGATE; ++q) dhp[q * H] = dgh[q];
+            for (int q = 0; q < NGATE; ++q) a.dGh[go + q * H] = dgh[q];
+          }
+          if (a.dGhb) {
+#pragma unroll
+            for (int q = 0; q < NGATE; ++q) a.dGhb[go + q * H] = bf16_rne(dgh[q]);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) {
+          sbi[q] += dgi[q];
+          sbh[q] += dgh[q];
         }
       }
       if (ct) {
@@ -1377,6 +1409,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       }
     }
     STAMP(6)
+  }
+  // fused bias gradients: one atomic per (cell, gate) for the whole sequence
+  if (cval) {
+#pragma unroll
+    for (int q = 0; q < NGATE; ++q) {
+      if (a.dbi) atomicAdd(a.dbi + d * GH + q * H + cj, sbi[q]);
+      if (a.dbh) atomicAdd(a.dbh + d * GH + q * H + cj, sbh[q]);
+    }
   }
   STAMP_FLUSH
 }
@@ -1527,12 +1567,24 @@ DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
   return fwd > bwd ? fwd : bwd;
 }
 
+DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
+                                 const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                                 void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream);
+
 DL4SS_API int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh, const float* b_hh,
                               float* out, float* hprev, float* act, float* cs, void* workspace,
                               long long ws_bytes, int* status, void* stream) {
+  DL4SS_REQUIRE(hprev);
+  return dl4ss_birnn_fwd_ex(cell, precision, B, T, H, G, W_hh, b_hh, out, hprev, act, cs, nullptr, nullptr, workspace,
+                            ws_bytes, status, stream);
+}
+
+DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
+                                 const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                                 void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
   DL4SS_REQUIRE(precision == 0 || precision == 1);
-  DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && out && hprev && act && workspace && status);
+  DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && out && act && workspace && status);
   DL4SS_REQUIRE(cell == CELL_GRU || cs);
   Plan p;
   DL4SS_REQUIRE(make_plan(cell, B, H, p));
@@ -1543,9 +1595,14 @@ DL4SS_API int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, cons
   const bool pk = mf && p.fwd_pk && T < 65535;
   hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.BC * p.NG * 8 * 8 : groups * 2 * p.BC * H * 8, st);
   if (e != hipSuccess) return (int)e;
+  // the bf16 copies, and dropping the fp32 h_{t-1} (only the GRU BPTT reads it), need the packed kernel
+  DL4SS_REQUIRE(pk || (!out_bf16 && !hprev_bf16 && hprev));
+  DL4SS_REQUIRE(hprev || cell == CELL_LSTM);
   RnnArgs a{};
   fill_args(a, p, B, T, H);
   a.G = G; a.Whh = W_hh; a.bhh = b_hh; a.out = out; a.hprev = hprev; a.act = act; a.cs = cs;
+  a.outb = reinterpret_cast<unsigned short*>(out_bf16);
+  a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
   a.status = status;
   const int grid = (int)(groups * p.NG);
@@ -1554,13 +1611,30 @@ DL4SS_API int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, cons
                            : dispatch<CELL_GRU>(true, mf, pk, p.BC, a, grid, smem, st);
 }
 
+DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, const float* dOut,
+                                 const float* dOut_bcast, const float* W_hh, const float* act, const float* cs,
+                                 const float* hprev, float* dG, float* dGh, void* dG_bf16, void* dGh_bf16,
+                                 float* db_ih, float* db_hh, void* workspace, long long ws_bytes, int* status,
+                                 void* stream);
+
 DL4SS_API int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, const float* dOut, const float* dOut_bcast,
                               const float* W_hh, const float* act, const float* cs, const float* hprev, float* dG,
                               float* dGh, void* workspace, long long ws_bytes, int* status, void* stream) {
+  DL4SS_REQUIRE(dG && (cell == CELL_LSTM || dGh));
+  return dl4ss_birnn_bwd_ex(cell, precision, B, T, H, dOut, dOut_bcast, W_hh, act, cs, hprev, dG, dGh, nullptr,
+                            nullptr, nullptr, nullptr, workspace, ws_bytes, status, stream);
+}
+
+DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, const float* dOut,
+                                 const float* dOut_bcast, const float* W_hh, const float* act, const float* cs,
+                                 const float* hprev, float* dG, float* dGh, void* dG_bf16, void* dGh_bf16,
+                                 float* db_ih, float* db_hh, void* workspace, long long ws_bytes, int* status,
+                                 void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
   DL4SS_REQUIRE(precision == 0 || precision == 1);
-  DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && dG && workspace && status);
-  DL4SS_REQUIRE(cell == CELL_GRU ? (dGh && hprev) : (cs != nullptr));
+  DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && workspace && status);
+  DL4SS_REQUIRE(dG || dG_bf16);
+  DL4SS_REQUIRE(cell == CELL_GRU ? ((dGh || dGh_bf16) && hprev) : (cs != nullptr));
   Plan p;
   DL4SS_REQUIRE(make_plan(cell, B, H, p));
   DL4SS_REQUIRE(ws_bytes >= dl4ss_birnn_workspace_bytes(cell, B, H));
@@ -1571,10 +1645,14 @@ DL4SS_API int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, cons
   const long long HG = ((H + 1) / 2 + 1) & ~1;
   hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.NG * p.BC * HG * 8 : groups * 2 * p.NG * p.BC * H * 8, st);
   if (e != hipSuccess) return (int)e;
+  // bf16 gradient copies, dropping the fp32 ones and the fused bias sums need the packed kernel
+  DL4SS_REQUIRE(pk || (!dG_bf16 && !dGh_bf16 && !db_ih && !db_hh && dG && (cell == CELL_LSTM || dGh)));
   RnnArgs a{};
   fill_args(a, p, B, T, H);
   a.Whh = W_hh; a.act = const_cast<float*>(act); a.cs = const_cast<float*>(cs);
   a.hprev = const_cast<float*>(hprev); a.dOut = dOut; a.dOutB = dOut_bcast; a.dG = dG; a.dGh = dGh;
+  a.dGb = reinterpret_cast<unsigned short*>(dG_bf16); a.dGhb = reinterpret_cast<unsigned short*>(dGh_bf16);
+  a.dbi = db_ih; a.dbh = db_hh;
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
   a.status = status;
   const int grid = (int)(groups * p.NG);

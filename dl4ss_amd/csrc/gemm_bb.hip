@@ -1,0 +1,384 @@
+// bf16-operand MFMA GEMM: C[M,N] (fp32) (+)= op(A) . op(B) (+ bias) (tanh), with
+// A and B already bf16 in HBM (the throughput path of the separation step).
+//
+// In bf16 mode every GEMM operand of the step is rounded to bf16 before the MFMA
+// anyway (gemm.hip rounds fp32 operands at the LDS store).  Here the PRODUCERS
+// write the bf16 copy (the BiRNN kernels write bf16 h / h_{t-1} / dG, the
+// attention kernel bf16 dPre, dl4ss_f32_to_bf16 the weights and the layer-0
+// features), so the products are bit-identical to gemm.hip's bf16 mode while the
+// operand bytes halve and no conversion sits in the load path.
+//
+// Tile 128 x 128 x 64, 256 threads = 4 waves in 2 x 2, each wave 64 x 64 =
+// 2 x 2 v_mfma_f32_32x32x16_bf16 accumulators.  Staging: every thread moves one
+// 8 x 8 bf16 block per k-tile (threads 0-127 of A, 128-255 of B): 8 x 16-B global
+// loads, and for a k-major operand (element (r,k) at G[k*ld + r]: the transposed
+// side of the weight gradients) an 8 x 8 16-bit transpose in registers
+// (v_perm_b32), then 8 x 16-B LDS stores into the [row][k] image (row stride 72
+// bf16 = 144 B: conflict-free ds_read_b128 fragments).  Pipeline: two LDS
+// buffers + a ring of three register blocks, so each k-tile's global loads are in
+// flight for two k-tiles of MFMAs before they are stored to LDS.
+// Tiles are mapped XCD-major and grouped (8 M-tiles x all N-tiles), as gemm.hip.
+// Split-K (grid.z) accumulates with fp32 atomics into C (weight gradients).
+#include "common.h"
+#include <hip/hip_bf16.h>
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, LDK = BK + 8;
+constexpr int NT = 256;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+enum { EPI_NONE = 0, EPI_TANH = 1 };
+
+// tanh for the Linear epilogue: 1 - 2 / (1 + e^{2x}) with v_exp + v_rcp (~1e-6 relative;
+// saturates cleanly: e^{2x} -> inf gives 1, -> 0 gives -1)
+__device__ __forceinline__ float ftanh_fast(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
+
+// One 8 x 8 block of one operand tile, staged in v[8] (16 B each).  KC: element (r,k)
+// at G[r*ld + k] (k contiguous); !KC: at G[k*ld + r].  Block (rb, kb): rows 8rb..+8,
+// k 8kb..+8.  Block index bi: KC -> rb = bi >> 3, kb = bi & 7 (a wave's 8 lanes of one
+// rb read 128 contiguous bytes); !KC -> kb = bi >> 4, rb = bi & 15 (16 lanes of one
+// k-row read 256 contiguous bytes).
+template <bool KC>
+__device__ __forceinline__ void block_coords(int bi, int& rb, int& kb) {
+  if (KC) { rb = bi >> 3; kb = bi & 7; }
+  else { kb = bi >> 4; rb = bi & 15; }
+}
+
+template <bool KC>
+__device__ __forceinline__ void load_block(uint4 (&v)[8], const unsigned short* __restrict__ G, long long ld, int r0,
+                                           int rmax, int k0, int kmax, bool vec, int rb, int kb) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int gr = KC ? r0 + 8 * rb + j : r0 + 8 * rb;
+    const int gk = KC ? k0 + 8 * kb : k0 + 8 * kb + j;
+    const unsigned short* p = KC ? G + (long long)gr * ld + gk : G + (long long)gk * ld + gr;
+    const bool full = KC ? (gr < rmax && gk + 8 <= kmax) : (gk < kmax && gr + 8 <= rmax);
+    if (vec && full) {
+      v[j] = *reinterpret_cast<const uint4*>(p);
+    } else {
+      unsigned e[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const bool in = KC ? (gr < rmax && gk + c < kmax) : (gk < kmax && gr + c < rmax);
+        e[c] = in ? p[c] : 0u;
+      }
+      v[j] = make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+    }
+  }
+}
+
+// write the block into the [row][k] LDS image (k-major blocks are transposed 8 x 8 in
+// registers: v[k] holds r = 0..7 of k-row k, two per dword)
+template <bool KC>
+__device__ __forceinline__ void store_block(const uint4 (&v)[8], unsigned short* __restrict__ s, int rb, int kb) {
+  if (KC) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *reinterpret_cast<uint4*>(s + (8 * rb + j) * LDK + 8 * kb) = v[j];
+  } else {
+    const unsigned* w = reinterpret_cast<const unsigned*>(v);  // w[4k + r/2]
+#pragma unroll
+    for (int r2 = 0; r2 < 4; ++r2) {
+      // v_perm_b32 selectors: 0x05040100 = lo16(src1) | lo16(src0) << 16 (even row 2 r2),
+      //                       0x07060302 = hi16(src1) | hi16(src0) << 16 (odd row 2 r2 + 1)
+      uint4 ev, od;
+      ev.x = __builtin_amdgcn_perm(w[4 * 1 + r2], w[4 * 0 + r2], 0x05040100u);
+      ev.y = __builtin_amdgcn_perm(w[4 * 3 + r2], w[4 * 2 + r2], 0x05040100u);
+      ev.z = __builtin_amdgcn_perm(w[4 * 5 + r2], w[4 * 4 + r2], 0x05040100u);
+      ev.w = __builtin_amdgcn_perm(w[4 * 7 + r2], w[4 * 6 + r2], 0x05040100u);
+      od.x = __builtin_amdgcn_perm(w[4 * 1 + r2], w[4 * 0 + r2], 0x07060302u);
+      od.y = __builtin_amdgcn_perm(w[4 * 3 + r2], w[4 * 2 + r2], 0x07060302u);
+      od.z = __builtin_amdgcn_perm(w[4 * 5 + r2], w[4 * 4 + r2], 0x07060302u);
+      od.w = __builtin_amdgcn_perm(w[4 * 7 + r2], w[4 * 6 + r2], 0x07060302u);
+      *reinterpret_cast<uint4*>(s + (8 * rb + 2 * r2) * LDK + 8 * kb) = ev;
+      *reinterpret_cast<uint4*>(s + (8 * rb + 2 * r2 + 1) * LDK + 8 * kb) = od;
+    }
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool ATOMIC>
+__global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
+                                                        long long lda, const unsigned short* __restrict__ B,
+                                                        long long ldb, float* __restrict__ C, long long ldc,
+                                                        const float* __restrict__ bias, float beta, int k_per_split,
+                                                        int grid_m, int grid_n, int vec) {
+  __shared__ __attribute__((aligned(16))) unsigned short sA[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short sB[2][BN * LDK];
+
+  const int ntiles = grid_m * grid_n;
+  const int per_xcd = (ntiles + 7) / 8;
+  const int tile = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  if (tile >= ntiles) return;
+  constexpr int GROUP = 8;
+  const int gsize = GROUP * grid_n;
+  const int first_m = (tile / gsize) * GROUP;
+  const int gm_here = min(grid_m - first_m, GROUP);
+  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  if (kbeg >= kend) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const bool isA = tid < 128;  // waves 0-1 stage A, waves 2-3 stage B (wave-uniform)
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  // staging: threads 0-127 stage A, 128-255 stage B; a ring of NS register blocks keeps
+  // the loads of k-tiles kt+1 .. kt+NS-1 in flight while tile kt is multiplied
+  constexpr int NS = 3;
+  uint4 v[NS][8];
+  int rb, kb;
+  if (isA) block_coords<A_KC>(tid & 127, rb, kb);
+  else block_coords<B_KC>(tid & 127, rb, kb);
+  const bool va = vec & 1, vb = vec & 2;
+  auto load = [&](uint4(&r)[8], int kt) {
+    const int k0 = kbeg + kt * BK;
+    if (isA) load_block<A_KC>(r, A, lda, m0, M, k0, kend, va, rb, kb);
+    else load_block<B_KC>(r, B, ldb, n0, N, k0, kend, vb, rb, kb);
+  };
+  auto store = [&](const uint4(&r)[8], int buf) {
+    if (isA) store_block<A_KC>(r, sA[buf], rb, kb);
+    else store_block<B_KC>(r, sB[buf], rb, kb);
+  };
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+#pragma unroll
+  for (int u = 0; u < NS; ++u)
+    if (u < nk) load(v[u], u);
+  store(v[0], 0);
+  __syncthreads();
+  const int fr = lane & 31, fk = 8 * (lane >> 5);
+  for (int kt0 = 0; kt0 < nk; kt0 += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int kt = kt0 + u;
+      if (kt < nk) {
+        const int cur = kt & 1;
+        const unsigned short* a = sA[cur];
+        const unsigned short* b = sB[cur];
+#ifndef GBB_NO_MFMA
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 16) {
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a + (wm + fr) * LDK + kk + fk);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + (wm + 32 + fr) * LDK + kk + fk);
+          const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(b + (wn + fr) * LDK + kk + fk);
+          const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(b + (wn + 32 + fr) * LDK + kk + fk);
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+        }
+#endif
+        if (kt + 1 < nk) store(v[(u + 1) % NS], cur ^ 1);  // tile kt+1 into the idle LDS buffer
+#ifndef GBB_NO_LOAD
+        if (kt + NS < nk) load(v[u], kt + NS);
+#endif              // v[u] (tile kt) was stored last iteration
+        __syncthreads();
+      }
+    }
+  }
+
+  // epilogue.  acc[i][j][r] holds (row wm + 32i + (r&3) + 8(r>>2) + 4(lane>>5), col
+  // wn + 32j + (lane&31)).  Non-atomic: each wave stages its 64 x 64 fp32 sub-tile in
+  // LDS (the operand buffers are free after the last barrier; 16 KB per wave, row
+  // stride 68 floats) and writes it back as 16-B stores, 16 lanes per 256-B row.
+  const bool add_bias = bias && blockIdx.z == 0;
+  if constexpr (ATOMIC) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn + 32 * j + (lane & 31);
+        if (col >= N) continue;
+        const float bv = add_bias ? bias[col] : 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < M) atomicAdd(C + (long long)row * ldc + col, acc[i][j][r] + bv);
+        }
+      }
+  } else {
+    constexpr int SLD = 68;
+    float* stage = reinterpret_cast<float*>(&sA[0][0]) + wave * 64 * SLD;  // 4 x 17 KB <= sA + sB
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          stage[(32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * SLD + 32 * j + (lane & 31)] = acc[i][j][r];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const int c4 = 4 * (lane & 15);  // this lane's 4 columns of the wave's 64
+    const int col = n0 + wn + c4;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (add_bias) {
+      bv.x = col < N ? bias[col] : 0.f;
+      bv.y = col + 1 < N ? bias[col + 1] : 0.f;
+      bv.z = col + 2 < N ? bias[col + 2] : 0.f;
+      bv.w = col + 3 < N ? bias[col + 3] : 0.f;
+    }
+    const bool vec_c = (ldc % 4 == 0) && ((((uintptr_t)C) & 15) == 0) && col + 4 <= N;
+#pragma unroll 4
+    for (int rr = 0; rr < 64; rr += 4) {
+      const int rl = rr + (lane >> 4);
+      const int row = m0 + wm + rl;
+      if (row >= M) continue;
+      float4 x = *reinterpret_cast<const float4*>(stage + rl * SLD + c4);
+      x.x += bv.x; x.y += bv.y; x.z += bv.z; x.w += bv.w;
+      float* cp = C + (long long)row * ldc + col;
+      if (vec_c) {
+        if (beta != 0.0f) {
+          const float4 o = *reinterpret_cast<const float4*>(cp);
+          x.x += beta * o.x; x.y += beta * o.y; x.z += beta * o.z; x.w += beta * o.w;
+        }
+        if (EPI == EPI_TANH) { x.x = ftanh_fast(x.x); x.y = ftanh_fast(x.y); x.z = ftanh_fast(x.z); x.w = ftanh_fast(x.w); }
+        *reinterpret_cast<float4*>(cp) = x;
+      } else {
+        const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (col + c >= N) break;
+          float y = xs[c];
+          if (beta != 0.0f) y += beta * cp[c];
+          if (EPI == EPI_TANH) y = ftanh_fast(y);
+          cp[c] = y;
+        }
+      }
+    }
+  }
+}
+
+template <bool A_KC, bool B_KC>
+int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
+           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, hipStream_t st) {
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  if (splitk < 1) splitk = 1;
+  int kps = (K + splitk - 1) / splitk;
+  kps = (kps + BK - 1) / BK * BK;
+  splitk = (K + kps - 1) / kps;
+  const int ntiles = gm * gn;
+  dim3 grid(8 * ((ntiles + 7) / 8), 1, splitk);
+  // 16-B vector loads need 16-B aligned rows (ld % 8 == 0) and base pointers
+  const int vec = ((lda % 8 == 0 && ((uintptr_t)A & 15) == 0) ? 1 : 0) |
+                  ((ldb % 8 == 0 && ((uintptr_t)B & 15) == 0) ? 2 : 0);
+  if (splitk > 1) {
+    if (epi != EPI_NONE || beta != 1.0f) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_NONE, true>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb,
+                       C, ldc, bias, beta, kps, gm, gn, vec);
+  } else if (epi == EPI_TANH) {
+    hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_TANH, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, bias, beta, kps, gm, gn, vec);
+  } else {
+    hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_NONE, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, bias, beta, kps, gm, gn, vec);
+  }
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, unsigned short* __restrict__ y, long long n) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    const float4 v = *reinterpret_cast<const float4*>(x + i);
+    __hip_bfloat162 lo2 = __float22bfloat162_rn(make_float2(v.x, v.y));
+    __hip_bfloat162 hi2 = __float22bfloat162_rn(make_float2(v.z, v.w));
+    const unsigned lo = *reinterpret_cast<unsigned*>(&lo2), hi = *reinterpret_cast<unsigned*>(&hi2);
+    *reinterpret_cast<uint2*>(y + i) = make_uint2(lo, hi);
+  } else {
+    for (long long j = i; j < n; ++j) {
+      const unsigned u = __float_as_uint(x[j]);
+      y[j] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    }
+  }
+}
+
+__global__ void f32_to_bf16_2d_kernel(const float* __restrict__ x, long long ldx, int rows, int cols,
+                                      unsigned short* __restrict__ y, long long ldy) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)rows * ldy) return;
+  const long long r = i / ldy, c = i - r * ldy;
+  unsigned short o = 0;
+  if (c < cols) {
+    const unsigned u = __float_as_uint(x[r * ldx + c]);
+    o = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  }
+  y[i] = o;
+}
+
+// out[n] += sum_m A[m*lda + n] for bf16 A (bias gradients from bf16 dPre)
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const unsigned short* __restrict__ A, long long lda, int M,
+                                                          int N, int rows_per_block, float* __restrict__ out) {
+  __shared__ float s[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int m0 = blockIdx.y * rows_per_block;
+  const int m1 = min(M, m0 + rows_per_block);
+  float acc = 0.f;
+  if (c < N)
+    for (int m = m0 + rl; m < m1; m += 4) acc += __uint_as_float((unsigned)A[(long long)m * lda + c] << 16);
+  s[rl][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rl == 0 && c < N) atomicAdd(out + c, s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
+}
+
+}  // namespace
+
+// y[r*ldy + c] = bf16(x[r*ldx + c]) for c < cols, 0 for cols <= c < ldy (row padding for 16-B rows)
+DL4SS_API int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy,
+                                   void* stream) {
+  DL4SS_REQUIRE(x && y && rows >= 0 && cols >= 0 && ldx >= cols && ldy >= cols);
+  if (rows == 0) return 0;
+  const long long n = (long long)rows * ldy;
+  hipLaunchKernelGGL(f32_to_bf16_2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), x,
+                     ldx, rows, cols, reinterpret_cast<unsigned short*>(y), ldy);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+DL4SS_API int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, void* stream) {
+  DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
+  if (M == 0 || N == 0) return 0;
+  const int rpb = 256;
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(cdiv(N, 64), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const unsigned short*>(A), lda, M, N, rpb, out);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+// C = op(A) op(B) (+ bias) (tanh) (+ beta C) with bf16 A, B (raw 16-bit words).
+// transA: A stored K x M (else M x K); transB: B stored N x K (else K x N).
+DL4SS_API int dl4ss_gemm_bf16(int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                              const void* B, long long ldb, float* C, long long ldc, const float* bias, int epilogue,
+                              float beta, int splitk, void* stream) {
+  DL4SS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && A && B && C);
+  if (M == 0 || N == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const auto* a = reinterpret_cast<const unsigned short*>(A);
+  const auto* b = reinterpret_cast<const unsigned short*>(B);
+  const bool a_kc = !transA, b_kc = transB;
+  if (a_kc && b_kc) return launch<true, true>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
+  if (a_kc && !b_kc) return launch<true, false>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
+  if (!a_kc && b_kc) return launch<false, true>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
+  return launch<false, false>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
+}
+
+// y = bf16(x), round to nearest even (the rounding gemm.hip applies at its LDS store).
+DL4SS_API int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream) {
+  DL4SS_REQUIRE(n >= 0 && (n == 0 || (x && y)));
+  if (n == 0) return 0;
+  DL4SS_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0);
+  const long long threads = (n + 3) / 4;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, as_stream(stream), x,
+                     reinterpret_cast<unsigned short*>(y), n);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}

@@ -165,6 +165,26 @@ class SepTrainer:
         self.s1 = 1.0 / (B * nch * T * F)
         self.s2 = 0.0 if (mode == "crm" or loss_channels) else sum_weight / (B * T * F)
         self.spk = torch.empty(B, K, device=dev, dtype=torch.int32)
+        # bf16 mode: every GEMM operand is produced directly as bf16 (gemm_bb.hip): the BiRNN
+        # kernels write bf16 h / h_{t-1} / dG (and fuse the bias gradients), the attention
+        # kernel writes bf16 dPre, the weights and the layer-0 features are converted once per
+        # step.  Rows are padded to multiples of 8 (16-B aligned operand rows).
+        self.fast = precision == "bf16" and self.rnn_precision == "bf16"
+        if self.fast:
+            bf = dict(device=dev, dtype=torch.bfloat16)
+            p8 = lambda n: (n + 7) // 8 * 8
+            self.p8 = p8
+            D0 = net.F
+            self.xb0 = torch.empty(BT, p8(D0), **bf)
+            self.outb = [torch.empty(BT, p8(2 * H), **bf) for _ in range(net.L)]
+            self.hprevb = [torch.empty(BT, 2 * p8(H), **bf) for _ in range(net.L)]
+            self.dGb = torch.empty(BT, 2 * NGH, **bf)
+            self.dGhb = torch.empty(BT, 2 * NGH, **bf) if net.cell == "gru" else None
+            self.dPreb = torch.empty(BT, p8(F * net.E), **bf)
+            self.wb_ih = [torch.empty(2 * NGH, p8(F if l == 0 else 2 * H), **bf) for l in range(net.L)]
+            self.wb_lin = torch.empty(F * net.E, p8(2 * H), **bf)
+            if net.cell == "lstm":  # the LSTM BPTT never reads the fp32 h_{t-1}
+                self.hprev = [None] * net.L
 
     # ------------------------------------------------------------------ features
     def features(self, raw, gains):
@@ -180,12 +200,47 @@ class SepTrainer:
                      out_mag=self.mag_src.view(B * K, self.T, self.F))
 
     # ------------------------------------------------------------------ forward
+    def _to_bf16_rows(self, x, out):
+        """out[:, :cols] = bf16(x), zero row padding (dl4ss_f32_to_bf16_2d)."""
+        _lib.call("dl4ss_f32_to_bf16_2d", _lib.ptr(x, True), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(out),
+                  out.stride(0), _lib.stream_ptr())
+
+    def _forward_fast(self, x):
+        net, B, T, H = self.net, self.B, self.T, self.net.H
+        BT = B * T
+        st = _lib.stream_ptr()
+        cell = CELLS[net.cell]
+        for l in range(net.L):
+            self._to_bf16_rows(net.cat_view("weight_ih", l), self.wb_ih[l])
+        self._to_bf16_rows(net.view("mix.Linear.weight"), self.wb_lin)
+        self._to_bf16_rows(x, self.xb0)
+        xb = self.xb0[:, :x.shape[1]]
+        for l in range(net.L):
+            D = xb.shape[1]
+            ops.gemm_bf16(xb, self.wb_ih[l][:, :D], transB=True, bias=net.cat_view("bias_ih", l), out=self.G)
+            hp = self.hprev[l]
+            _lib.call("dl4ss_birnn_fwd_ex", cell, 1, B, T, H, _lib.ptr(self.G), _lib.ptr(net.cat_view("weight_hh", l)),
+                      _lib.ptr(net.cat_view("bias_hh", l)), _lib.ptr(self.out[l]), _lib.ptr(hp), _lib.ptr(self.act[l]),
+                      _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.outb[l]), _lib.ptr(self.hprevb[l]),
+                      _lib.ptr(self.rnn_ws), self.ws_bytes, _lib.ptr(self.status), st)
+            xb = self.outb[l][:, :2 * H]
+        ops.gemm_bf16(xb, self.wb_lin[:, :2 * H], transB=True, bias=net.view("mix.Linear.bias"),
+                      epilogue=ops.EPI_TANH, out=self.V)
+
     def forward(self, feats=None):
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         x = (self.mag_mix if feats is None else feats).reshape(BT, -1)
         st = _lib.stream_ptr()
         cell = CELLS[net.cell]
+        if self.fast:
+            self._forward_fast(x)
+            wadj = net.view("adj.layer.weight") if net.adjust else None
+            _lib.call("dl4ss_query_fwd", _lib.ptr(self.out[-1]), B, T, 2 * H, _lib.ptr(self.spk),
+                      _lib.ptr(net.view("emb.layer.weight")), _lib.ptr(wadj), self.K, net.W, _lib.ptr(self.q),
+                      _lib.ptr(self.mean), st)
+            self._feats = x
+            return
         for l in range(net.L):
             ops.gemm(x, net.cat_view("weight_ih", l), transB=True, bias=net.cat_view("bias_ih", l), out=self.G,
                      precision=self.precision)
@@ -210,11 +265,14 @@ class SepTrainer:
 
     def attn(self, pass_, perm=None, mask_out=None, pred_out=None):
         X, xs, Y, ys, yks = self._attn_args()
-        _lib.call("dl4ss_mask_attn_loss", pass_, int(self.mode == "crm"), self.B, self.K, self.T, self.F, self.net.E,
-                  _lib.ptr(self.V), _lib.ptr(self.q), _lib.ptr(X), xs, _lib.ptr(Y), ys, yks, _lib.ptr(perm),
-                  self.s1, self.s2, _lib.ptr(self.V) if pass_ == 1 else None, _lib.ptr(self.part_loss),
-                  _lib.ptr(self.part_dq) if pass_ == 1 else None, _lib.ptr(mask_out), _lib.ptr(pred_out),
-                  _lib.stream_ptr())
+        grad = pass_ == 1
+        dpre = _lib.ptr(self.V) if grad and not self.fast else None
+        dpreb = _lib.ptr(self.dPreb) if grad and self.fast else None
+        _lib.call("dl4ss_mask_attn_loss_ex", pass_, int(self.mode == "crm"), self.B, self.K, self.T, self.F,
+                  self.net.E, _lib.ptr(self.V), _lib.ptr(self.q), _lib.ptr(X), xs, _lib.ptr(Y), ys, yks,
+                  _lib.ptr(perm), self.s1, self.s2, dpre, dpreb, self.dPreb.stride(0) if self.fast else 0,
+                  _lib.ptr(self.part_loss), _lib.ptr(self.part_dq) if grad else None, _lib.ptr(mask_out),
+                  _lib.ptr(pred_out), _lib.stream_ptr())
 
     def loss_and_grad(self):
         """Fused attention + loss + dPre (in place over V) + dq; returns loss (device)."""
@@ -230,6 +288,42 @@ class SepTrainer:
         return self.loss
 
     # ------------------------------------------------------------------ backward
+    def _backward_fast(self):
+        net, B, T, H = self.net, self.B, self.T, self.net.H
+        BT = B * T
+        NGH = _ngate(net.cell) * H
+        FE = self.F * net.E
+        g = net.grad
+        st = _lib.stream_ptr()
+        cell = CELLS[net.cell]
+        dPreb = self.dPreb[:, :FE]
+        hLb = self.outb[-1][:, :2 * H]
+        ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
+        _lib.call("dl4ss_colsum_bf16", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+                  _lib.ptr(net.view("mix.Linear.bias", g)), st)
+        dH = self.dH[0]
+        ops.gemm_bf16(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk="auto")
+        hp8 = self.p8(H)
+        for l in range(net.L - 1, -1, -1):
+            _lib.call("dl4ss_birnn_bwd_ex", cell, 1, B, T, H, _lib.ptr(dH),
+                      _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
+                      _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
+                      _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), None, None,
+                      _lib.ptr(self.dGb), _lib.ptr(self.dGhb), _lib.ptr(net.cat_view("bias_ih", l, g)),
+                      _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self.rnn_ws), self.ws_bytes,
+                      _lib.ptr(self.status), st)
+            xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
+            ops.gemm_bf16(self.dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0)
+            dGhb = self.dGhb if self.dGhb is not None else self.dGb
+            whh_g = net.cat_view("weight_hh", l, g)
+            for d in range(2):
+                ops.gemm_bf16(dGhb[:, d * NGH:(d + 1) * NGH], self.hprevb[l][:, d * hp8:d * hp8 + H], transA=True,
+                              out=whh_g[d * NGH:(d + 1) * NGH], splitk="auto", beta=1.0)
+            if l > 0:
+                dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
+                ops.gemm_bf16(self.dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")
+                dH = dH_next
+
     def backward(self):
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
@@ -244,6 +338,9 @@ class SepTrainer:
                   _lib.ptr(net.view("emb.layer.weight", g)),
                   _lib.ptr(net.view("adj.layer.weight", g)) if net.adjust else None,
                   _lib.ptr(self.dh_bcast) if net.adjust else None, st)
+        if self.fast:
+            self._backward_fast()
+            return
         dPre = self.V
         hL = self.out[-1].view(BT, 2 * H)
         # grads were zeroed above: weight gradients accumulate (beta 1) with split-K

@@ -137,6 +137,55 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
     return out
 
 
+def _mat_bf16(t, name):
+    if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
+        raise RuntimeError(f"{name}: expected a 2-D row-major bfloat16 CUDA matrix (unit inner stride)")
+    return t
+
+
+def gemm_bf16(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.0, out=None, splitk=1):
+    """out (fp32) = op(A) @ op(B) (+ bias) (tanh) (+ beta*out) with bf16 A and B
+    (dl4ss_gemm_bf16: the bf16-operand MFMA GEMM, gemm_bb.hip).  Layout and split-K
+    conventions as gemm()."""
+    _mat_bf16(A, "gemm_bf16(A)")
+    _mat_bf16(B, "gemm_bf16(B)")
+    M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
+    Kb, N = (B.shape[1], B.shape[0]) if transB else (B.shape[0], B.shape[1])
+    if K != Kb:
+        raise RuntimeError(f"gemm_bf16: inner dims differ ({K} vs {Kb})")
+    if out is None:
+        if beta != 0.0 or splitk not in (1, "auto"):
+            raise RuntimeError("gemm_bf16: accumulation needs an output tensor")
+        out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    _mat(out, "gemm_bf16(out)")
+    if tuple(out.shape) != (M, N):
+        raise RuntimeError(f"gemm_bf16: out shape {tuple(out.shape)} != {(M, N)}")
+    if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
+        raise RuntimeError("gemm_bf16: bias must be contiguous with N elements")
+    if splitk == "auto":
+        splitk = auto_splitk(M, N, K) if epilogue == EPI_NONE else 1
+        if splitk > 1 and beta == 0.0:
+            out.zero_()
+            beta = 1.0
+        elif splitk > 1 and beta != 1.0:
+            splitk = 1
+    _lib.call("dl4ss_gemm_bf16", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
+              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue,
+              float(beta), int(splitk), _lib.stream_ptr())
+    return out
+
+
+def to_bf16(x, out=None):
+    """bf16 copy (round to nearest even) of a contiguous fp32 CUDA tensor."""
+    _f32c(x, "to_bf16")
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    if out.dtype != torch.bfloat16 or not out.is_contiguous() or out.numel() != x.numel():
+        raise RuntimeError("to_bf16: out must be a contiguous bfloat16 tensor of the same size")
+    _lib.call("dl4ss_f32_to_bf16", _lib.ptr(x), _lib.ptr(out), x.numel(), _lib.stream_ptr())
+    return out
+
+
 def colsum(A, out):
     """out += A.sum(0) for a row-major matrix view A (M, N)."""
     _mat(A, "colsum")

@@ -72,6 +72,20 @@ int dl4ss_gemm(int transA, int transB, int M, int N, int K, const float* A, long
                long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta, int precision,
                int splitk, void* stream);
 
+/* bf16-operand form of dl4ss_gemm (precision bf16): A and B are raw bf16 words already
+ * rounded by their producers; C fp32.  Same layout, epilogue and split-K conventions;
+ * the products equal dl4ss_gemm(precision = BF16) on the fp32 originals. */
+int dl4ss_gemm_bf16(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
+                    long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta, int splitk,
+                    void* stream);
+/* y[i] = bf16(x[i]) (round to nearest even), n elements; x 16-B aligned, y 8-B aligned. */
+int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream);
+
+/* 2-D form with row padding: y[r*ldy + c] = bf16(x[r*ldx + c]) (c < cols), 0 up to ldy. */
+int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, void* stream);
+/* out[n] += sum_m A[m*lda + n] for a bf16 matrix A (bias gradient from bf16 dPre). */
+int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, void* stream);
+
 /* ---- persistent bidirectional LSTM / GRU recurrence ---------------------- */
 enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
 /* Granule workspace (bytes) needed by dl4ss_birnn_fwd / _bwd for (cell, B, H); -1 if unsupported. */
@@ -87,12 +101,30 @@ long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
 int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
                     const float* b_hh, float* out, float* hprev, float* act, float* cs, void* workspace,
                     long long ws_bytes, int* status, void* stream);
+/* dl4ss_birnn_fwd with bf16 extras (precision 1, packed-hand-off kernel only):
+ * out_bf16 (B*T rows of pad8(2H): [fwd | reverse] adjacent) receives bf16(h), the next
+ * layer's / the Linear's GEMM operand; hprev_bf16 (B*T rows of 2 pad8(H): each direction's
+ * block 16-B aligned) receives bf16(h_{t-1}), the W_hh weight-gradient operand
+ * (pad8(n) = n rounded up to a multiple of 8; pads are not written).  hprev may be NULL
+ * for LSTM (only the GRU BPTT reads the fp32 h_{t-1}). */
+int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
+                       const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                       void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream);
 /* BPTT of one layer: dOut (B,T,2H) (+ dOut_bcast (B,2H) at every t, may be NULL) ->
  * dG (B,T,2,NG*H) grad of the input projection (pre-activation) and, for GRU, dGh
  * grad of W_hh h + b_hh (for LSTM they coincide; dGh may be NULL). */
 int dl4ss_birnn_bwd(int cell, int precision, int B, int T, int H, const float* dOut, const float* dOut_bcast,
                     const float* W_hh, const float* act, const float* cs, const float* hprev, float* dG, float* dGh, void* workspace,
                     long long ws_bytes, int* status, void* stream);
+
+/* dl4ss_birnn_bwd with bf16 extras (precision 1, packed-hand-off kernel only): dG_bf16 /
+ * dGh_bf16 (B,T,2,NG*H) receive bf16 copies (the weight-gradient / dX GEMM operands),
+ * dG / dGh may then be NULL, and db_ih / db_hh (2, NG*H) are ACCUMULATED with the sums
+ * over (b,t) of dG / dGh (the bias gradients; fp32 atomics, one per cell and gate). */
+int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, const float* dOut, const float* dOut_bcast,
+                       const float* W_hh, const float* act, const float* cs, const float* hprev, float* dG,
+                       float* dGh, void* dG_bf16, void* dGh_bf16, float* db_ih, float* db_hh, void* workspace,
+                       long long ws_bytes, int* status, void* stream);
 
 /* ---- speaker-query mask attention + loss (fused forward/backward) -------- */
 /* Blocks per utterance used by the partial-sum buffers. */
@@ -110,6 +142,14 @@ int dl4ss_mask_attn_loss(int pass, int crm, int B, int K, int T, int F, int E, c
                          const float* X, long long x_bstride, const float* Y, long long y_bstride,
                          long long y_kstride, const int* perm, float s1, float s2, float* dPre, float* part_loss,
                          float* part_dq, float* mask_out, float* pred_out, void* stream);
+/* dl4ss_mask_attn_loss with a bf16 GRAD output: dPre_bf16 row (b*T + t) holds the F*E
+ * values of frame t at stride dpre_bf16_ld (even, >= F*E: 16-B rows for the Linear's
+ * backward GEMMs); dPre may then be NULL. */
+int dl4ss_mask_attn_loss_ex(int pass, int crm, int B, int K, int T, int F, int E, const float* V, const float* q,
+                            const float* X, long long x_bstride, const float* Y, long long y_bstride,
+                            long long y_kstride, const int* perm, float s1, float s2, float* dPre, void* dPre_bf16,
+                            long long dpre_bf16_ld, float* part_loss, float* part_dq, float* mask_out,
+                            float* pred_out, void* stream);
 /* PIT: per utterance the lowest-index permutation minimising the summed costs. */
 int dl4ss_pit_select(const float* part_loss, int B, int K, int nblk, int* perm, void* stream);
 /* loss_out[3] = {total, MSE term, weighted sum-to-one term}; dq = sum of partials. */

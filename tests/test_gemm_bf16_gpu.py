@@ -1,0 +1,75 @@
+"""bf16-operand GEMM (dl4ss_gemm_bf16, gemm_bb.hip) against dl4ss_gemm in bf16 mode on the
+fp32 originals: both round operands to bf16 (RNE) and accumulate the same 32x32x16 MFMA
+products in the same k order, so without split-K the results are bit-identical; with
+split-K only the fp32 atomic summation order differs (1e-5 relative), and the tanh
+epilogue uses v_exp/v_rcp (2e-6 absolute)."""
+import pytest
+import torch
+
+from dl4ss_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda")
+
+
+SHAPES = [(300, 200, 129), (8032 // 4, 600, 600), (130, 257, 1000), (64, 70, 8), (1, 1, 1), (515, 129, 77),
+          (250, 130, 136)]
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_bf16_bit_identical(dev, ta, tb, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(*((K, M) if ta else (M, K)), generator=g).to(dev)
+    B = torch.randn(*((N, K) if tb else (K, N)), generator=g).to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    ref = ops.gemm(A, B, transA=ta, transB=tb, bias=bias, precision="bf16")
+    ours = ops.gemm_bf16(ops.to_bf16(A), ops.to_bf16(B), transA=ta, transB=tb, bias=bias)
+    torch.cuda.synchronize()
+    assert torch.equal(ours, ref)
+
+
+def test_gemm_bf16_tanh_beta_splitk(dev):
+    g = torch.Generator(device="cpu").manual_seed(5)
+    A = torch.randn(700, 300, generator=g).to(dev)
+    B = torch.randn(450, 300, generator=g).to(dev)
+    Ab, Bb = ops.to_bf16(A), ops.to_bf16(B)
+    ref = ops.gemm(A, B, transB=True, epilogue=ops.EPI_TANH, precision="bf16")
+    ours = ops.gemm_bf16(Ab, Bb, transB=True, epilogue=ops.EPI_TANH)
+    assert (ours - ref).abs().max().item() < 2e-6  # v_exp/v_rcp tanh vs tanhf
+    C0 = torch.randn(700, 450, generator=g).to(dev)
+    ref = ops.gemm(A, B, transB=True, beta=0.5, out=C0.clone(), precision="bf16")
+    ours = ops.gemm_bf16(Ab, Bb, transB=True, beta=0.5, out=C0.clone())
+    assert torch.equal(ours, ref)
+    # weight-gradient form: long K, split-K atomics
+    X = torch.randn(5000, 300, generator=g).to(dev)
+    D = torch.randn(5000, 240, generator=g).to(dev)
+    ref = ops.gemm(D, X, transA=True, precision="bf16")
+    ours = ops.gemm_bf16(ops.to_bf16(D), ops.to_bf16(X), transA=True, out=torch.zeros(240, 300, device=dev),
+                         beta=1.0, splitk=4)
+    assert ((ours - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+def test_gemm_bf16_padded_rows(dev):
+    """operands as column slices of row-padded bf16 buffers (the producers' layout)"""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    A = torch.randn(333, 136, generator=g).to(dev)[:, :129]
+    B = torch.randn(260, 136, generator=g).to(dev)[:, :129]
+    ref = ops.gemm(A.contiguous(), B.contiguous(), transB=True, precision="bf16")
+    Ab = ops.to_bf16(A.contiguous())
+    Ap = torch.zeros(333, 136, device=dev, dtype=torch.bfloat16)
+    Ap[:, :129] = Ab
+    Bp = torch.zeros(260, 136, device=dev, dtype=torch.bfloat16)
+    Bp[:, :129] = ops.to_bf16(B.contiguous())
+    ours = ops.gemm_bf16(Ap[:, :129], Bp[:, :129], transB=True)
+    assert torch.equal(ours, ref)
+
+
+def test_to_bf16_matches_torch_rne(dev):
+    x = torch.randn(1003, device=dev) * 1e3
+    assert torch.equal(ops.to_bf16(x), x.to(torch.bfloat16))
