@@ -25,6 +25,7 @@ SIGNATURES = {
     "dl4ss_mix_sources": [P, P, I, I, I, P, P, P, P],
     "dl4ss_gemm": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, P],
     "dl4ss_gemm_bf16": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, P],
+    "dl4ss_gemm_bf16_batched": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P],
     "dl4ss_f32_to_bf16": [P, P, LL, P],
     "dl4ss_f32_to_bf16_2d": [P, LL, I, I, P, LL, P],
     "dl4ss_colsum_bf16": [P, LL, I, I, P, P],

@@ -45,18 +45,50 @@ __device__ __forceinline__ void block_coords(int bi, int& rb, int& kb) {
   else { kb = bi >> 4; rb = bi & 15; }
 }
 
-template <bool KC>
+// mask of dword i of a 16-B chunk whose first n elements (of 8) are valid
+__device__ __forceinline__ unsigned chunk_mask(int i, int n) {
+  return 2 * i + 1 < n ? 0xFFFFFFFFu : (2 * i < n ? 0x0000FFFFu : 0u);
+}
+
+// VEC: every row of the operand is 16-B aligned (ld % 8 == 0, aligned base), so a chunk
+// that starts inside the matrix never leaves its row: the eight 16-B loads are issued
+// unconditionally (out-of-range rows / k-rows re-read a valid address) and masked
+// afterwards -- straight-line code, so the compiler keeps them all in flight.
+template <bool KC, bool VEC>
 __device__ __forceinline__ void load_block(uint4 (&v)[8], const unsigned short* __restrict__ G, long long ld, int r0,
-                                           int rmax, int k0, int kmax, bool vec, int rb, int kb) {
+                                           int rmax, int k0, int kmax, int rb, int kb) {
+  if constexpr (VEC) {
+    if (KC) {
+      const int gk = k0 + 8 * kb;
+      const int nk = max(0, min(8, kmax - gk));
+      const int gkc = nk > 0 ? gk : 0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int gr = KC ? r0 + 8 * rb + j : r0 + 8 * rb;
-    const int gk = KC ? k0 + 8 * kb : k0 + 8 * kb + j;
-    const unsigned short* p = KC ? G + (long long)gr * ld + gk : G + (long long)gk * ld + gr;
-    const bool full = KC ? (gr < rmax && gk + 8 <= kmax) : (gk < kmax && gr + 8 <= rmax);
-    if (vec && full) {
-      v[j] = *reinterpret_cast<const uint4*>(p);
+      for (int j = 0; j < 8; ++j) {
+        const int gr = r0 + 8 * rb + j;
+        const bool rok = gr < rmax;
+        v[j] = *reinterpret_cast<const uint4*>(G + (long long)(rok ? gr : 0) * ld + gkc);
+        const int n = rok ? nk : 0;
+        v[j].x &= chunk_mask(0, n); v[j].y &= chunk_mask(1, n); v[j].z &= chunk_mask(2, n); v[j].w &= chunk_mask(3, n);
+      }
     } else {
+      const int gr = r0 + 8 * rb;
+      const int nr = max(0, min(8, rmax - gr));
+      const int grc = nr > 0 ? gr : 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int gk = k0 + 8 * kb + j;
+        const bool kok = gk < kmax;
+        v[j] = *reinterpret_cast<const uint4*>(G + (long long)(kok ? gk : 0) * ld + grc);
+        const int n = kok ? nr : 0;
+        v[j].x &= chunk_mask(0, n); v[j].y &= chunk_mask(1, n); v[j].z &= chunk_mask(2, n); v[j].w &= chunk_mask(3, n);
+      }
+    }
+  } else {  // unaligned rows: element-wise (correct, slow; producers pad rows to avoid it)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int gr = KC ? r0 + 8 * rb + j : r0 + 8 * rb;
+      const int gk = KC ? k0 + 8 * kb : k0 + 8 * kb + j;
+      const unsigned short* p = KC ? G + (long long)gr * ld + gk : G + (long long)gk * ld + gr;
       unsigned e[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -96,13 +128,66 @@ __device__ __forceinline__ void store_block(const uint4 (&v)[8], unsigned short*
   }
 }
 
-template <bool A_KC, bool B_KC, int EPI, bool ATOMIC>
+// The k-loop of one staging role: this thread stages blocks of ONE operand (KC layout)
+// and all threads run the same MFMAs and barriers.  Hoisting the (wave-uniform) role
+// out of the loop keeps each loop's loads straight-line code.
+template <bool KC, bool VEC>
+__device__ __forceinline__ void kloop(f32x16 (&acc)[2][2], const unsigned short* __restrict__ G, long long ld,
+                                      int r0, int rmax, int kbeg, int kend, unsigned short* sOwn, const unsigned short* sA,
+                                      const unsigned short* sB, int bi, int lane, int wm, int wn) {
+  constexpr int NS = 3;  // register ring: loads of k-tiles kt+1 .. kt+2 in flight during tile kt
+  constexpr int BUF = BM * LDK;
+  uint4 v[NS][8];
+  int rb, kb;
+  block_coords<KC>(bi, rb, kb);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+#pragma unroll
+  for (int u = 0; u < NS; ++u)
+    if (u < nk) load_block<KC, VEC>(v[u], G, ld, r0, rmax, kbeg + u * BK, kend, rb, kb);
+  store_block<KC>(v[0], sOwn, rb, kb);
+  __syncthreads();
+  const int fr = lane & 31, fk = 8 * (lane >> 5);
+  for (int kt0 = 0; kt0 < nk; kt0 += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int kt = kt0 + u;
+      if (kt < nk) {
+        const int cur = kt & 1;
+        const unsigned short* a = sA + cur * BUF;
+        const unsigned short* b = sB + cur * BUF;
+#ifndef GBB_NO_MFMA
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 16) {
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a + (wm + fr) * LDK + kk + fk);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + (wm + 32 + fr) * LDK + kk + fk);
+          const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(b + (wn + fr) * LDK + kk + fk);
+          const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(b + (wn + 32 + fr) * LDK + kk + fk);
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+        }
+#endif
+        if (kt + 1 < nk) store_block<KC>(v[(u + 1) % NS], sOwn + (cur ^ 1) * BUF, rb, kb);
+        if (kt + NS < nk) load_block<KC, VEC>(v[u], G, ld, r0, rmax, kbeg + (kt + NS) * BK, kend, rb, kb);
+        __syncthreads();
+      }
+    }
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool ATOMIC, bool VEC>
 __global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
                                                         long long lda, const unsigned short* __restrict__ B,
                                                         long long ldb, float* __restrict__ C, long long ldc,
                                                         const float* __restrict__ bias, float beta, int k_per_split,
-                                                        int grid_m, int grid_n, int vec) {
+                                                        int grid_m, int grid_n, long long sa, long long sb,
+                                                        long long sc) {
   __shared__ __attribute__((aligned(16))) unsigned short sA[2][BM * LDK];
+  // batch member blockIdx.y (strided batch: element offsets sa, sb, sc)
+  A += blockIdx.y * sa;
+  B += blockIdx.y * sb;
+  C += blockIdx.y * sc;
   __shared__ __attribute__((aligned(16))) unsigned short sB[2][BN * LDK];
 
   const int ntiles = grid_m * grid_n;
@@ -121,7 +206,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, con
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const bool isA = tid < 128;  // waves 0-1 stage A, waves 2-3 stage B (wave-uniform)
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -131,60 +215,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, con
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  // staging: threads 0-127 stage A, 128-255 stage B; a ring of NS register blocks keeps
-  // the loads of k-tiles kt+1 .. kt+NS-1 in flight while tile kt is multiplied
-  constexpr int NS = 3;
-  uint4 v[NS][8];
-  int rb, kb;
-  if (isA) block_coords<A_KC>(tid & 127, rb, kb);
-  else block_coords<B_KC>(tid & 127, rb, kb);
-  const bool va = vec & 1, vb = vec & 2;
-  auto load = [&](uint4(&r)[8], int kt) {
-    const int k0 = kbeg + kt * BK;
-    if (isA) load_block<A_KC>(r, A, lda, m0, M, k0, kend, va, rb, kb);
-    else load_block<B_KC>(r, B, ldb, n0, N, k0, kend, vb, rb, kb);
-  };
-  auto store = [&](const uint4(&r)[8], int buf) {
-    if (isA) store_block<A_KC>(r, sA[buf], rb, kb);
-    else store_block<B_KC>(r, sB[buf], rb, kb);
-  };
-
-  const int nk = (kend - kbeg + BK - 1) / BK;
-#pragma unroll
-  for (int u = 0; u < NS; ++u)
-    if (u < nk) load(v[u], u);
-  store(v[0], 0);
-  __syncthreads();
-  const int fr = lane & 31, fk = 8 * (lane >> 5);
-  for (int kt0 = 0; kt0 < nk; kt0 += NS) {
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const int kt = kt0 + u;
-      if (kt < nk) {
-        const int cur = kt & 1;
-        const unsigned short* a = sA[cur];
-        const unsigned short* b = sB[cur];
-#ifndef GBB_NO_MFMA
-#pragma unroll
-        for (int kk = 0; kk < BK; kk += 16) {
-          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a + (wm + fr) * LDK + kk + fk);
-          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + (wm + 32 + fr) * LDK + kk + fk);
-          const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(b + (wn + fr) * LDK + kk + fk);
-          const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(b + (wn + 32 + fr) * LDK + kk + fk);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
-        }
-#endif
-        if (kt + 1 < nk) store(v[(u + 1) % NS], cur ^ 1);  // tile kt+1 into the idle LDS buffer
-#ifndef GBB_NO_LOAD
-        if (kt + NS < nk) load(v[u], kt + NS);
-#endif              // v[u] (tile kt) was stored last iteration
-        __syncthreads();
-      }
-    }
-  }
+  // threads 0-127 stage A, 128-255 stage B (wave-uniform)
+  if (tid < 128)
+    kloop<A_KC, VEC>(acc, A, lda, m0, M, kbeg, kend, &sA[0][0], &sA[0][0], &sB[0][0], tid, lane, wm, wn);
+  else
+    kloop<B_KC, VEC>(acc, B, ldb, n0, N, kbeg, kend, &sB[0][0], &sA[0][0], &sB[0][0], tid - 128, lane, wm, wn);
 
   // epilogue.  acc[i][j][r] holds (row wm + 32i + (r&3) + 8(r>>2) + 4(lane>>5), col
   // wn + 32j + (lane&31)).  Non-atomic: each wave stages its 64 x 64 fp32 sub-tile in
@@ -259,28 +294,32 @@ __global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, con
 
 template <bool A_KC, bool B_KC>
 int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
-           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, hipStream_t st) {
+           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
+           long long sb, long long sc, hipStream_t st) {
   const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
   if (splitk < 1) splitk = 1;
   int kps = (K + splitk - 1) / splitk;
   kps = (kps + BK - 1) / BK * BK;
   splitk = (K + kps - 1) / kps;
   const int ntiles = gm * gn;
-  dim3 grid(8 * ((ntiles + 7) / 8), 1, splitk);
-  // 16-B vector loads need 16-B aligned rows (ld % 8 == 0) and base pointers
-  const int vec = ((lda % 8 == 0 && ((uintptr_t)A & 15) == 0) ? 1 : 0) |
-                  ((ldb % 8 == 0 && ((uintptr_t)B & 15) == 0) ? 2 : 0);
-  if (splitk > 1) {
-    if (epi != EPI_NONE || beta != 1.0f) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_NONE, true>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb,
-                       C, ldc, bias, beta, kps, gm, gn, vec);
-  } else if (epi == EPI_TANH) {
-    hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_TANH, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B,
-                       ldb, C, ldc, bias, beta, kps, gm, gn, vec);
+  dim3 grid(8 * ((ntiles + 7) / 8), batch, splitk);
+  // straight-line 16-B loads need 16-B aligned rows (ld % 8 == 0) and base pointers
+  const bool vec = lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ldb % 8 == 0 && ((uintptr_t)B & 15) == 0 &&
+                   (batch == 1 || (sa % 8 == 0 && sb % 8 == 0));
+  if (splitk > 1 && (epi != EPI_NONE || beta != 1.0f)) return (int)hipErrorInvalidValue;
+#define GBB_LAUNCH(EPI_, AT_, VEC_)                                                                             \
+  hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_, AT_, VEC_>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, C, \
+                     ldc, bias, beta, kps, gm, gn, sa, sb, sc)
+  if (vec) {
+    if (splitk > 1) GBB_LAUNCH(EPI_NONE, true, true);
+    else if (epi == EPI_TANH) GBB_LAUNCH(EPI_TANH, false, true);
+    else GBB_LAUNCH(EPI_NONE, false, true);
   } else {
-    hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_NONE, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B,
-                       ldb, C, ldc, bias, beta, kps, gm, gn, vec);
+    if (splitk > 1) GBB_LAUNCH(EPI_NONE, true, false);
+    else if (epi == EPI_TANH) GBB_LAUNCH(EPI_TANH, false, false);
+    else GBB_LAUNCH(EPI_NONE, false, false);
   }
+#undef GBB_LAUNCH
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
@@ -354,21 +393,33 @@ DL4SS_API int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, floa
   return 0;
 }
 
-// C = op(A) op(B) (+ bias) (tanh) (+ beta C) with bf16 A, B (raw 16-bit words).
-// transA: A stored K x M (else M x K); transB: B stored N x K (else K x N).
-DL4SS_API int dl4ss_gemm_bf16(int transA, int transB, int M, int N, int K, const void* A, long long lda,
-                              const void* B, long long ldb, float* C, long long ldc, const float* bias, int epilogue,
-                              float beta, int splitk, void* stream) {
-  DL4SS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && A && B && C);
+// Strided batch of dl4ss_gemm_bf16: member i uses A + i*strideA, B + i*strideB, C + i*strideC
+// (element offsets; the bias, if any, is shared).
+DL4SS_API int dl4ss_gemm_bf16_batched(int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                                      const void* B, long long ldb, float* C, long long ldc, const float* bias,
+                                      int epilogue, float beta, int splitk, int batch, long long strideA,
+                                      long long strideB, long long strideC, void* stream) {
+  DL4SS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && A && B && C && batch >= 1 && batch <= 65535);
   if (M == 0 || N == 0) return 0;
   hipStream_t st = as_stream(stream);
   const auto* a = reinterpret_cast<const unsigned short*>(A);
   const auto* b = reinterpret_cast<const unsigned short*>(B);
   const bool a_kc = !transA, b_kc = transB;
-  if (a_kc && b_kc) return launch<true, true>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
-  if (a_kc && !b_kc) return launch<true, false>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
-  if (!a_kc && b_kc) return launch<false, true>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
-  return launch<false, false>(M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, st);
+#define GBB_ARGS M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, batch, strideA, strideB, strideC, st
+  if (a_kc && b_kc) return launch<true, true>(GBB_ARGS);
+  if (a_kc && !b_kc) return launch<true, false>(GBB_ARGS);
+  if (!a_kc && b_kc) return launch<false, true>(GBB_ARGS);
+  return launch<false, false>(GBB_ARGS);
+#undef GBB_ARGS
+}
+
+// C = op(A) op(B) (+ bias) (tanh) (+ beta C) with bf16 A, B (raw 16-bit words).
+// transA: A stored K x M (else M x K); transB: B stored N x K (else K x N).
+DL4SS_API int dl4ss_gemm_bf16(int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                              const void* B, long long ldb, float* C, long long ldc, const float* bias, int epilogue,
+                              float beta, int splitk, void* stream) {
+  return dl4ss_gemm_bf16_batched(transA, transB, M, N, K, A, lda, B, ldb, C, ldc, bias, epilogue, beta, splitk, 1, 0,
+                                 0, 0, stream);
 }
 
 // y = bf16(x), round to nearest even (the rounding gemm.hip applies at its LDS store).

@@ -316,9 +316,9 @@ class SepTrainer:
             ops.gemm_bf16(self.dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0)
             dGhb = self.dGhb if self.dGhb is not None else self.dGb
             whh_g = net.cat_view("weight_hh", l, g)
-            for d in range(2):
-                ops.gemm_bf16(dGhb[:, d * NGH:(d + 1) * NGH], self.hprevb[l][:, d * hp8:d * hp8 + H], transA=True,
-                              out=whh_g[d * NGH:(d + 1) * NGH], splitk="auto", beta=1.0)
+            # both directions in one launch: member d = columns d*NGH of dGh, d*pad8(H) of h_{t-1}
+            ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
+                                  NGH, H, BT, transA=True, beta=1.0, splitk="auto")
             if l > 0:
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
                 ops.gemm_bf16(self.dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")

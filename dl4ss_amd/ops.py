@@ -137,6 +137,9 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
     return out
 
 
+GEMM_BF16_TARGET_WGS = 256  # measured best on MI355X (tools/gemm_bench_bf16.py sweep: 256/512/768)
+
+
 def _mat_bf16(t, name):
     if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
         raise RuntimeError(f"{name}: expected a 2-D row-major bfloat16 CUDA matrix (unit inner stride)")
@@ -163,7 +166,9 @@ def gemm_bf16(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, be
     if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
         raise RuntimeError("gemm_bf16: bias must be contiguous with N elements")
     if splitk == "auto":
-        splitk = auto_splitk(M, N, K) if epilogue == EPI_NONE else 1
+        # split-K adds fp32 atomic traffic (1.3 TB/s) on the output: split only as far as ~256
+        # workgroups (the sweep in tools/gemm_bench_bf16.py)
+        splitk = auto_splitk(M, N, K, target_wgs=GEMM_BF16_TARGET_WGS) if epilogue == EPI_NONE else 1
         if splitk > 1 and beta == 0.0:
             out.zero_()
             beta = 1.0
@@ -172,6 +177,23 @@ def gemm_bf16(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, be
     _lib.call("dl4ss_gemm_bf16", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
               _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue,
               float(beta), int(splitk), _lib.stream_ptr())
+    return out
+
+
+def gemm_bf16_batched(A, B, out, batch, strideA, strideB, strideC, M, N, K, transA=False, transB=False,
+                      beta=0.0, splitk=1):
+    """Strided batch of gemm_bf16 over raw views: member i reads A/B at element offsets
+    i*strideA / i*strideB from the given (first-member) views and writes out + i*strideC."""
+    _mat_bf16(A, "gemm_bf16_batched(A)")
+    _mat_bf16(B, "gemm_bf16_batched(B)")
+    _mat(out, "gemm_bf16_batched(out)")
+    if splitk == "auto":
+        splitk = auto_splitk(M, N, K, target_wgs=max(1, GEMM_BF16_TARGET_WGS // batch))
+        if splitk > 1 and beta == 0.0:
+            raise RuntimeError("gemm_bf16_batched: split-K accumulates (beta 1) into a zeroed output")
+    _lib.call("dl4ss_gemm_bf16_batched", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
+              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), None, EPI_NONE, float(beta),
+              int(splitk), int(batch), int(strideA), int(strideB), int(strideC), _lib.stream_ptr())
     return out
 
 

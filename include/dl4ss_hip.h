@@ -78,6 +78,11 @@ int dl4ss_gemm(int transA, int transB, int M, int N, int K, const float* A, long
 int dl4ss_gemm_bf16(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
                     long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta, int splitk,
                     void* stream);
+/* Strided batch (grid.y): member i uses A + i*strideA, B + i*strideB, C + i*strideC (elements). */
+int dl4ss_gemm_bf16_batched(int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                            const void* B, long long ldb, float* C, long long ldc, const float* bias, int epilogue,
+                            float beta, int splitk, int batch, long long strideA, long long strideB,
+                            long long strideC, void* stream);
 /* y[i] = bf16(x[i]) (round to nearest even), n elements; x 16-B aligned, y 8-B aligned. */
 int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream);
 

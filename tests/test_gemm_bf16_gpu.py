@@ -73,3 +73,19 @@ def test_gemm_bf16_padded_rows(dev):
 def test_to_bf16_matches_torch_rne(dev):
     x = torch.randn(1003, device=dev) * 1e3
     assert torch.equal(ops.to_bf16(x), x.to(torch.bfloat16))
+
+
+def test_gemm_bf16_batched_matches_members(dev):
+    """two column blocks of one matrix in one launch (the per-direction W_hh gradients)"""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    BT, NGH, H, hp8 = 700, 120, 30, 32
+    D = ops.to_bf16(torch.randn(BT, 2 * NGH, generator=g).to(dev))
+    Hb = torch.zeros(BT, 2 * hp8, device=dev, dtype=torch.bfloat16)
+    Hb[:, :H] = torch.randn(BT, H, generator=g).to(dev).to(torch.bfloat16)
+    Hb[:, hp8:hp8 + H] = torch.randn(BT, H, generator=g).to(dev).to(torch.bfloat16)
+    out = torch.zeros(2 * NGH, H, device=dev)
+    ops.gemm_bf16_batched(D[:, :NGH], Hb[:, :H], out[:NGH], 2, NGH, hp8, NGH * H, NGH, H, BT, transA=True, beta=1.0,
+                          splitk=3)
+    for d in range(2):
+        ref = ops.gemm_bf16(D[:, d * NGH:(d + 1) * NGH], Hb[:, d * hp8:d * hp8 + H], transA=True)
+        assert ((out[d * NGH:(d + 1) * NGH] - ref).abs().max() / ref.abs().max()).item() < 1e-5

@@ -11,6 +11,8 @@ from gemm_bench import SHAPES  # noqa: E402
 
 
 def main():
+    if len(sys.argv) > 1:
+        ops.GEMM_BF16_TARGET_WGS = int(sys.argv[1])
     dev = torch.device("cuda")
     total = 0.0
     for name, ta, tb, M, N, K, sk, epi in SHAPES:
