@@ -47,6 +47,9 @@ def main():
     lib.dl4ss_debug_set_stamps.argtypes = [ctypes.c_void_p]
     lib.dl4ss_debug_set_stamps(ctypes.c_void_p(stamps.data_ptr()))
     x = torch.randn(Bsz, T, 129, device=dev)
+    tr.spk.zero_()  # valid speaker ids for the query gather
+    if getattr(tr, "fast", False):
+        tr.dPreb.normal_()
     for rep in range(2):
         stamps.zero_()
         tr.forward(feats=x)

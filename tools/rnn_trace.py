@@ -45,10 +45,19 @@ def main():
     lib.dl4ss_debug_set_stamps.argtypes = [ctypes.c_void_p]
     lib.dl4ss_debug_set_stamps(ctypes.c_void_p(buf.data_ptr()))
     x = torch.randn(Bsz, T, 129, device=dev)
+    tr.spk.zero_()  # valid speaker ids for the query gather
+    bwd = "bwd" in sys.argv
     for _ in range(3):
         buf.zero_()
         tr.forward(feats=x)
         torch.cuda.synchronize()
+    if bwd:  # BPTT of the same layer (slot 3 = cell phase start after the first barrier)
+        tr.dq.normal_()
+        tr.dPreb.normal_()
+        for _ in range(2):
+            buf.zero_()
+            tr.backward()
+            torch.cuda.synchronize()
     tb = buf.view(grid, T, 4).cpu().double() * 10.0  # ns
     NG = 15
     ngroups = grid // NG
@@ -78,6 +87,12 @@ def main():
     q = lambda v, p: sorted(v)[int(p * (len(v) - 1))]
     print(f"step period (max publish to max publish) ns: median {st.median(step):.0f}  p10 {q(step, .1):.0f}  p90 {q(step, .9):.0f}")
     print(f"publish skew across producers ns: median {st.median(skew):.0f}  p90 {q(skew, .9):.0f}")
+    if bwd:
+        cp = [float(tb[m, s, 0] - tb[m, s, 3]) for m in range(grid) for s in range(2, T - 1)]
+        print(f"bwd cell start (after B1) -> own publish done ns: median {st.median(cp):.0f}  p90 {q(cp, .9):.0f}")
+        pc = [float(tb[m, s, 3] - tb[m, s, 1]) for m in range(grid) for s in range(2, T - 1)]
+        print(f"bwd poll complete -> cell start ns: median {st.median(pc):.0f}")
+        return
     print(f"first sweep round trip (poll start -> first re-poll) ns: median {st.median(rtt):.0f} p90 {q(rtt, .9):.0f}; "
           f"polls satisfied by the first sweep: {nospin}")
     print(f"poll start -> last producer publish ns: median {st.median(start_to_last):.0f}")
