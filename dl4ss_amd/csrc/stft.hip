@@ -7,9 +7,10 @@
 // output path (TDAA_beta/main_run_sstune_EvalVer.py:64-65, cRM_EvalVer.py:98-99).
 //
 // Design (HBM-bound, ~3.7 flop/B):
-//  * one 256-thread workgroup = 16 consecutive frames of one signal; the
-//    2304-sample span they cover is read once, coalesced, into LDS (reflect
-//    padding resolved at load time), so every sample crosses HBM once;
+//  * forward: one 256-thread workgroup = one 32-frame tile of one signal (see the
+//    forward section below: paired real-input DFTs); the iSTFT uses 16-frame
+//    tiles.  The sample span a tile covers is read once, coalesced, into LDS
+//    (reflect padding resolved at load time), so every sample crosses HBM once;
 //  * Hann window and the 256 twiddles W256^m live in LDS, computed once per
 //    workgroup with accurate sincospif;
 //  * each frame is a 256-pt real DFT done as 16 x 16 Cooley-Tukey: 16 lanes per
