@@ -41,7 +41,9 @@ constexpr int NROLE = 256;   // [0,256): cell + publish ; [256,512): gather
 constexpr int WMAX = 64;     // fwd weights per thread (generic path)
 constexpr int RPLMAX = 20;   // bwd rows per thread
 constexpr int KGLMAX = 6;    // bwd k per thread
-constexpr int HMAX = 320;    // largest hidden size (sizes the per-thread gather/publish offset arrays)
+constexpr int HMAX = 320;    // largest hidden size of the training kernels (sizes per-thread offset arrays)
+constexpr int HMAX_L = 640;  // largest hidden size of the forward-only (inference) instantiations: the
+                             // H = 600 speaker classifier of EvalVer.py:305-326 / GRID.py:178-199
 constexpr unsigned SPIN_LIMIT = 1u << 20;  // ~1 s of polling: a stuck hand-off exits, never hangs
 
 typedef unsigned long long u64;
@@ -190,11 +192,11 @@ __device__ __forceinline__ bool gather(const u64* src, const int (&off)[GM], uns
 //      throughput mode): wave m owns the 16-row tile m of W_hh (bf16 A fragments in
 //      registers for all K), h staged in LDS as bf16 [batch][k] (the B operand), one
 //      MFMA chain per wave -- no partial sums at all.
-template <int CELL, int BC, int KPL_T, bool MF>
+template <int CELL, int BC, int KPL_T, bool MF, int HM = HMAX>
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
   constexpr int WN = MF ? 1 : (KPL_T > 0 ? KPL_T : WMAX);  // fp32 weights per thread (compile-time)
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
-  constexpr int KSMAX = HMAX / 32;
+  constexpr int KSMAX = HM / 32;
   const int H = a.H, T = a.T, J = a.J;
   const int R = NGATE * J;
   const int ngroups = 2 * a.nchunk;
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 
   u64* xg = a.xbuf + (long long)group * 2 * BC * H;
   // gather role: granule offsets and LDS destinations, fixed for the whole launch
-  constexpr int GM = (BC * HMAX + NROLE - 1) / NROLE;
+  constexpr int GM = (BC * HM + NROLE - 1) / NROLE;
   int goff[GM], gdst[GM];
 #pragma unroll
   for (int g = 0; g < GM; ++g) {
@@ -1441,10 +1443,15 @@ struct Plan {
   bool fwd_pk;                       // packed hand-off forward (rnn_fwd_pk_kernel) applies
   size_t smem_fwd_pk;
   bool bwd_pk;                       // packed hand-off BPTT (rnn_bwd_pk_kernel) applies
+  bool big;                          // H > HMAX: forward-only instantiations (HM = HMAX_L)
   size_t smem_bwd_pk;
 };
 
-bool make_plan(int cell, int B, int H, Plan& p) {
+// mf: plan for the bf16 MFMA matvec (the fp32 VALU forward's per-thread weight limit
+// KPL <= WMAX does not apply).  H > HMAX is the forward-only large-H plan (HM = HMAX_L).
+bool make_plan(int cell, int B, int H, Plan& p, bool mf = true) {
+  if (H > HMAX_L) return false;
+  p.big = H > HMAX;
   const int ngate = cell == CELL_LSTM ? 4 : 3;
   for (int J = 20; J >= 4; --J) {
     const int R = ngate * J;
@@ -1452,7 +1459,7 @@ bool make_plan(int cell, int B, int H, Plan& p) {
     const int KP = NT / R;
     int KPL = (H + KP - 1) / KP;
     KPL = (KPL + 3) / 4 * 4;
-    if (KPL > WMAX) continue;
+    if (KPL > WMAX && !mf) continue;
     // bwd: RP row parts x KG k-groups <= NT
     int best_rp = -1, best_kg = 0;
     for (int RP = 1; RP <= 16; ++RP) {
@@ -1463,7 +1470,7 @@ bool make_plan(int cell, int B, int H, Plan& p) {
     }
     if (best_rp < 0) continue;
     const int NG = (H + J - 1) / J;
-    if (H > HMAX || J > 20) continue;  // gather/publish offset arrays are sized for H <= HMAX
+    if (J > 20) continue;  // gather/publish offset arrays are sized for J <= 20, H <= HMAX(_L)
     int BC = 0;
     for (int bc : {1, 2, 4, 8}) {
       const int nchunk = (B + bc - 1) / bc;
@@ -1480,11 +1487,11 @@ bool make_plan(int cell, int B, int H, Plan& p) {
     bwd_dims(p.RPL, p.KGL, rpln, kgln);
     p.smem_fwd = sizeof(float) * (BC * p.HP + KP * BC * R + 2 * BC * J * 4);
     p.smem_bwd = sizeof(float) * (BC * p.RP * rpln + NG * BC * J + 3 + p.RP * BC * p.KG * kgln + 2 * BC * J * 8);
-    const int SHB = HMAX + 8, MT = (R + 15) / 16, SDG = (4 * 20 + 31) / 32 * 32 + 8;
+    const int SHB = (p.big ? HMAX_L : HMAX) + 8, MT = (R + 15) / 16, SDG = (4 * 20 + 31) / 32 * 32 + 8;
     p.smem_fwd_mf = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * J * 4);
     p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
-    p.fwd_pk = J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= 7;
-    p.bwd_pk = J % 4 == 0 && H % 4 == 0 && NG <= 16;
+    p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= 7;
+    p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
     p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((NG * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16) + 2 * BC * 32 * 8);
     p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
     return true;
@@ -1494,6 +1501,13 @@ bool make_plan(int cell, int B, int H, Plan& p) {
 
 template <int CELL, int BC>
 void launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
+  if (a.H > HMAX) {  // forward-only large-H instantiations (the H = 600 classifier)
+    if (mf)
+      hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, true, HMAX_L>), dim3(grid), dim3(NT), smem, st, a);
+    else
+      hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, false, HMAX_L>), dim3(grid), dim3(NT), smem, st, a);
+    return;
+  }
   // compile-time k-slice lengths for the shipped H = 300 plans (LSTM J=20: 52, GRU J=20: 40)
   if (mf && pk)
     hipLaunchKernelGGL((rnn_fwd_pk_kernel<CELL, BC>), dim3(grid), dim3(NT), smem, st, a);
@@ -1554,17 +1568,29 @@ void fill_args(RnnArgs& a, const Plan& p, int B, int T, int H) {
 DL4SS_API void dl4ss_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
 #endif
 
-DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
-  Plan p;
-  if (!make_plan(cell, B, H, p)) return -1;
+static long long workspace_bytes(const Plan& p, int H) {
   const long long groups = 2LL * p.nchunk;
   long long fwd = groups * 2 * p.BC * H * 8;
   const long long fwd_pk = groups * 4 * p.BC * p.NG * 8 * 8;
   if (fwd_pk > fwd) fwd = fwd_pk;
+  if (p.big) return fwd;  // forward only
   long long bwd = groups * 2 * p.NG * p.BC * H * 8;
   const long long bwd_pk = groups * 4LL * p.NG * p.BC * (((H + 1) / 2 + 1) & ~1) * 8;
   if (bwd_pk > bwd) bwd = bwd_pk;
   return fwd > bwd ? fwd : bwd;
+}
+
+// the larger of the fp32 and bf16 plans' needs (either precision may use the buffer);
+// -1 when neither plan exists
+DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
+  long long best = -1;
+  for (bool mf : {false, true}) {
+    Plan p;
+    if (!make_plan(cell, B, H, p, mf)) continue;
+    const long long n = workspace_bytes(p, H);
+    if (n > best) best = n;
+  }
+  return best;
 }
 
 DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
@@ -1587,8 +1613,8 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && out && act && workspace && status);
   DL4SS_REQUIRE(cell == CELL_GRU || cs);
   Plan p;
-  DL4SS_REQUIRE(make_plan(cell, B, H, p));
-  DL4SS_REQUIRE(ws_bytes >= dl4ss_birnn_workspace_bytes(cell, B, H));
+  DL4SS_REQUIRE(make_plan(cell, B, H, p, precision == 1));
+  DL4SS_REQUIRE(ws_bytes >= workspace_bytes(p, H));
   hipStream_t st = as_stream(stream);
   const long long groups = 2LL * p.nchunk;
   const bool mf = precision == 1;
@@ -1635,9 +1661,10 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && workspace && status);
   DL4SS_REQUIRE(dG || dG_bf16);
   DL4SS_REQUIRE(cell == CELL_GRU ? ((dGh || dGh_bf16) && hprev) : (cs != nullptr));
+  DL4SS_REQUIRE(H <= HMAX);  // BPTT is built for the mask nets (H <= 320); the large-H plan is forward only
   Plan p;
-  DL4SS_REQUIRE(make_plan(cell, B, H, p));
-  DL4SS_REQUIRE(ws_bytes >= dl4ss_birnn_workspace_bytes(cell, B, H));
+  DL4SS_REQUIRE(make_plan(cell, B, H, p, precision == 1));
+  DL4SS_REQUIRE(ws_bytes >= workspace_bytes(p, H));
   hipStream_t st = as_stream(stream);
   const long long groups = 2LL * p.nchunk;
   const bool mf = precision == 1;

@@ -237,3 +237,45 @@ def test_birnn_bwd_dG_per_step(dev, cell, B, T, H, prec):
     # b_hh gradient (sum over b,t of dGh)
     dgh = (dGh if cell == "gru" else dG).cpu().double().view(B, T, 2, NGH).sum((0, 1))
     assert (dgh - bl.grad).abs().max() < tol_g * bl.grad.abs().max()
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+@pytest.mark.parametrize("B,T", [(1, 13), (4, 9), (32, 7)])
+def test_birnn_fwd_large_hidden(dev, cell, B, T, prec):
+    """Forward-only large-H plan (H = 600: the speaker classifier BiLSTM-3L of
+    EvalVer.py:305-326 / GRID.py:178-199; rnn_fwd_kernel<..., HMAX_L>).  prec 0: exact
+    fp32 recurrence vs fp64 (2e-5 abs); prec 1: bf16 MFMA matvec vs the fp64
+    recurrence with the same operand rounding (3e-3 abs).  BPTT at H > 320 is refused."""
+    H = 600
+    if prec == 0 and B == 32:
+        pytest.skip("the fp32 VALU plan at H = 600 needs 50 workgroups per group: B <= 16")
+    ng = 4 if cell == "lstm" else 3
+    NGH = ng * H
+    g = torch.Generator().manual_seed(B * 13 + T + prec)
+    G = torch.randn(B, T, 2, NGH, generator=g, dtype=torch.float64) * 0.5
+    whh = torch.randn(2, NGH, H, generator=g, dtype=torch.float64) / H ** 0.5
+    bhh = torch.randn(2, NGH, generator=g, dtype=torch.float64) * 0.1
+    ref = _manual_birnn(cell, G, whh, bhh, H, bf16=prec == 1)
+    cellid = 0 if cell == "lstm" else 1
+    Gd, whd, bhd = (t.float().to(dev).contiguous() for t in (G, whh, bhh))
+    o = torch.empty(B, T, 2 * H, device=dev)
+    hp = torch.empty_like(o)
+    act = torch.empty(B, T, 2, 4 * H, device=dev)
+    cs = torch.empty(B, T, 2, H, device=dev)
+    ws = _lib.query("dl4ss_birnn_workspace_bytes", cellid, B, H)
+    assert ws > 0
+    wsb = torch.empty((ws + 7) // 8, dtype=torch.int64, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("dl4ss_birnn_fwd", cellid, prec, B, T, H, _lib.ptr(Gd), _lib.ptr(whd), _lib.ptr(bhd), _lib.ptr(o),
+              _lib.ptr(hp), _lib.ptr(act), _lib.ptr(cs), _lib.ptr(wsb), ws, _lib.ptr(st), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert int(st.item()) == 0
+    err = (o.cpu().double() - ref).abs().max().item()
+    assert err < (2e-5 if prec == 0 else 3e-3), err
+    if B == 1 and prec == 1:
+        dG = torch.zeros(B * T, 2 * NGH, device=dev)
+        with pytest.raises(RuntimeError):
+            _lib.call("dl4ss_birnn_bwd", cellid, prec, B, T, H, _lib.ptr(o), None, _lib.ptr(whd), _lib.ptr(act),
+                      _lib.ptr(cs), _lib.ptr(hp), _lib.ptr(dG), _lib.ptr(dG), _lib.ptr(wsb), ws, _lib.ptr(st),
+                      _lib.stream_ptr())
