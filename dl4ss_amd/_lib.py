@@ -49,6 +49,10 @@ SIGNATURES = {
     "dl4ss_attn_dot_fwd": [P, P, I, I, I, I, I, P, P],
     "dl4ss_attn_dot_bwd": [P, P, I, P, P, I, I, I, I, P, P, P, P],
     "dl4ss_top_k_mask": [P, I, I, F, I, P, P, P, P],
+    "dl4ss_attn_dot_fwd_ex": [P, P, I, I, I, I, I, P, LL, P],
+    "dl4ss_classifier_select": [P, I, I, F, I, P, I, P, P, P, P],
+    "dl4ss_mask_split": [P, P, LL, P, P, P],
+    "dl4ss_time_mean": [P, I, I, I, P, P],
 }
 # entry points that return a value rather than a hipError_t
 RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,

@@ -9,6 +9,11 @@
 //   dl4ss_attn_dot_bwd  its backward: dV = dE q, dq = sum_r dE V, dE = dmask act'(e)
 //   dl4ss_top_k_mask    top_k_mask (EvalVer.py:390-405, Torch_multi/main_run.py:340-355)
 //                       on device: no sort, no host loop
+//   dl4ss_classifier_select  the speaker choice of the recursive extraction loop
+//                       (Torch_multi/main_run_multi_selfSS_recuReal_GRID.py:227-244,391-404):
+//                       sigmoid of the classifier logits, descending top-k order, first
+//                       not-yet-extracted speaker -- on device, no host round trip
+//   dl4ss_mask_split    pred = m X and residual (1 - m) X in one pass (GRID.py:433-444)
 #include "common.h"
 
 namespace {
@@ -32,7 +37,8 @@ constexpr float CRM_K = 10.0f;  // cRM_EvalVer.py:28
 
 template <int E>
 __global__ __launch_bounds__(256) void attn_dot_fwd_kernel(const float* __restrict__ V, const float* __restrict__ q,
-                                                           int q_stride, int R, int act, float* __restrict__ mask) {
+                                                           int q_stride, int R, int act, float* __restrict__ mask,
+                                                           long long mask_stride) {
   __shared__ float sq[E];
   const int b = blockIdx.y;
   if (threadIdx.x < E) sq[threadIdx.x] = q[(long long)b * q_stride + threadIdx.x];
@@ -43,7 +49,7 @@ __global__ __launch_bounds__(256) void attn_dot_fwd_kernel(const float* __restri
   float acc = 0.f;
 #pragma unroll
   for (int e = 0; e < E; ++e) acc = fmaf(vr[e], sq[e], acc);
-  mask[(long long)b * R + r] = act == 0 ? 1.0f / (1.0f + __expf(-acc)) : CRM_K * tanhf(acc);
+  mask[b * mask_stride + r] = act == 0 ? 1.0f / (1.0f + __expf(-acc)) : CRM_K * tanhf(acc);
 }
 
 // dE = dmask m (1-m); dV[b][r][:] = dE q[b]; per-block partial dq (fixed order, no atomics)
@@ -137,6 +143,76 @@ __global__ __launch_bounds__(256) void top_k_mask_kernel(const float* __restrict
   }
 }
 
+// One workgroup per row b: prob = sigmoid(logit) (the classifier head's F.sigmoid,
+// GRID.py:197); sort_index[b][0..top_k) = ids by descending prob (ties: lower id first,
+// -1 beyond N); chosen[b] = the first of them not in prev[0..n_prev)[b] when at least
+// one prob exceeds alpha (GRID.py:237-238: otherwise the loop has nothing to extract),
+// else -1.
+__global__ __launch_bounds__(256) void classifier_select_kernel(const float* __restrict__ logits, int N, float alpha,
+                                                                int top_k, const int* __restrict__ prev, int n_prev,
+                                                                float* __restrict__ prob, int* __restrict__ sort_index,
+                                                                int* __restrict__ chosen) {
+  extern __shared__ float sp[];  // [N] probabilities
+  __shared__ int s_cnt;
+  __shared__ int s_top[64];
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) s_cnt = 0;
+  if (threadIdx.x < 64) s_top[threadIdx.x] = -1;
+  __syncthreads();
+  int above = 0;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const float p = 1.0f / (1.0f + expf(-logits[(long long)b * N + i]));
+    sp[i] = p;
+    above += p > alpha ? 1 : 0;
+    if (prob) prob[(long long)b * N + i] = p;
+  }
+  atomicAdd(&s_cnt, above);
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const float pi = sp[i];
+    int rank = 0;
+    for (int j = 0; j < N; ++j) {
+      const float pj = sp[j];
+      rank += (pj > pi || (pj == pi && j < i)) ? 1 : 0;
+    }
+    if (rank < top_k) s_top[rank] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int pick = -1;
+    for (int r = 0; r < top_k; ++r) {
+      const int k = s_top[r];
+      if (sort_index) sort_index[(long long)b * top_k + r] = k;
+      if (pick >= 0 || k < 0 || s_cnt == 0) continue;
+      bool seen = false;
+      for (int p = 0; p < n_prev; ++p) seen |= prev[(long long)p * gridDim.x + b] == k;
+      if (!seen) pick = k;
+    }
+    if (chosen) chosen[b] = pick;
+  }
+}
+
+// pred = m x, resid = (1 - m) x (either output may be null); 4 elements per thread
+__global__ __launch_bounds__(256) void mask_split_kernel(const float* __restrict__ m, const float* __restrict__ x,
+                                                         long long n, float* __restrict__ pred,
+                                                         float* __restrict__ resid, bool vec) {
+  for (long long i = (blockIdx.x * 256LL + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * 1024) {
+    if (vec && i + 3 < n) {
+      const float4 a = *reinterpret_cast<const float4*>(m + i);
+      const float4 v = *reinterpret_cast<const float4*>(x + i);
+      if (pred) *reinterpret_cast<float4*>(pred + i) = make_float4(a.x * v.x, a.y * v.y, a.z * v.z, a.w * v.w);
+      if (resid)
+        *reinterpret_cast<float4*>(resid + i) =
+            make_float4((1.f - a.x) * v.x, (1.f - a.y) * v.y, (1.f - a.z) * v.z, (1.f - a.w) * v.w);
+    } else {
+      for (long long j = i; j < n && j < i + 4; ++j) {
+        if (pred) pred[j] = m[j] * x[j];
+        if (resid) resid[j] = (1.f - m[j]) * x[j];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 DL4SS_API int dl4ss_tanh_bwd(const float* v, const float* dv, float* dpre, long long n, void* stream) {
@@ -150,12 +226,40 @@ DL4SS_API int dl4ss_tanh_bwd(const float* v, const float* dv, float* dpre, long 
 
 DL4SS_API int dl4ss_attn_dot_nblk(int R) { return (int)cdiv(R, 256); }
 
-DL4SS_API int dl4ss_attn_dot_fwd(const float* V, const float* q, int q_stride, int Bq, int R, int E, int act,
-                                 float* mask, void* stream) {
+DL4SS_API int dl4ss_attn_dot_fwd_ex(const float* V, const float* q, int q_stride, int Bq, int R, int E, int act,
+                                    float* mask, long long mask_stride, void* stream) {
   DL4SS_REQUIRE(V && q && mask && Bq >= 0 && R >= 0 && E == 50 && q_stride >= E && (act == 0 || act == 1));
+  DL4SS_REQUIRE(mask_stride >= R);
   if (Bq == 0 || R == 0) return 0;
   hipLaunchKernelGGL(attn_dot_fwd_kernel<50>, dim3(cdiv(R, 256), Bq), dim3(256), 0, as_stream(stream), V, q, q_stride,
-                     R, act, mask);
+                     R, act, mask, mask_stride);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+DL4SS_API int dl4ss_attn_dot_fwd(const float* V, const float* q, int q_stride, int Bq, int R, int E, int act,
+                                 float* mask, void* stream) {
+  return dl4ss_attn_dot_fwd_ex(V, q, q_stride, Bq, R, E, act, mask, R, stream);
+}
+
+DL4SS_API int dl4ss_classifier_select(const float* logits, int B, int N, float alpha, int top_k, const int* prev,
+                                      int n_prev, float* prob, int* sort_index, int* chosen, void* stream) {
+  DL4SS_REQUIRE(logits && B >= 0 && N > 0 && N <= 8192 && top_k >= 1 && top_k <= 64 && n_prev >= 0);
+  DL4SS_REQUIRE(n_prev == 0 || prev);
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(classifier_select_kernel, dim3(B), dim3(256), sizeof(float) * N, as_stream(stream), logits, N,
+                     alpha, top_k, prev, n_prev, prob, sort_index, chosen);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+DL4SS_API int dl4ss_mask_split(const float* mask, const float* x, long long n, float* pred, float* resid,
+                               void* stream) {
+  DL4SS_REQUIRE(mask && x && n >= 0 && (pred || resid));
+  if (n == 0) return 0;
+  const bool vec = ((uintptr_t)mask | (uintptr_t)x | (uintptr_t)pred | (uintptr_t)resid) % 16 == 0;
+  const unsigned grid = (unsigned)min(16384LL, cdiv(n, 1024));
+  hipLaunchKernelGGL(mask_split_kernel, dim3(grid), dim3(256), 0, as_stream(stream), mask, x, n, pred, resid, vec);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

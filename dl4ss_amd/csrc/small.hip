@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) void query_fwd_kernel(const float* __restrict_
     for (int c = threadIdx.x; c < D; c += blockDim.x) smean[c] = mean[(long long)b * D + c];
   for (int i = threadIdx.x; i < K * W; i += blockDim.x) {
     const int k = i / W, o = i % W;
-    se[i] = emb[(long long)idx[b * K + k] * W + o];
+    const int id = idx[b * K + k];
+    se[i] = id >= 0 ? emb[(long long)id * W + o] : 0.0f;  // id -1: no speaker (zero query)
   }
   __syncthreads();
   for (int i = threadIdx.x; i < K * W; i += blockDim.x) {
@@ -180,6 +181,14 @@ DL4SS_API int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* id
   }
   const size_t smem = sizeof(float) * (D + K * W);
   hipLaunchKernelGGL(query_fwd_kernel, dim3(B), dim3(256), smem, st, mean_out, D, idx, emb, w_adj, K, W, q);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+DL4SS_API int dl4ss_time_mean(const float* h, int B, int T, int D, float* mean_out, void* stream) {
+  DL4SS_REQUIRE(h && mean_out && B >= 0 && T > 0 && D > 0);
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(256), 0, as_stream(stream), h, T, D, mean_out);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

@@ -163,7 +163,7 @@ int dl4ss_loss_finalize(const float* part_loss, int B, int K, int nblk, const in
 
 /* ---- speaker queries, reductions, optimizer ------------------------------ */
 /* q[b,k] = Emb[idx[b,k]] (+ W_adj [mean_t h[b]; Emb[idx[b,k]]]); h (B,T,D).
- * SPEECH_EMBEDDING + ADDJUST: EvalVer.py:348-377,606-608. w_adj may be NULL. */
+ * SPEECH_EMBEDDING + ADDJUST: EvalVer.py:348-377,606-608. w_adj may be NULL; an idx of -1 (no speaker) gives a zero query. */
 int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* idx, const float* emb, const float* w_adj, int K,
                     int W, float* q, float* mean_out, void* stream);
 /* d_emb (+=, scatter), d_wadj (+=), dh_bcast (B,D) = W_m^T sum_k dq / T. */
@@ -193,6 +193,26 @@ int dl4ss_attn_dot_bwd(const float* V, const float* q, int q_stride, const float
  * idx (B,top_k) the selected ids ascending (-1 padded), count (B); idx/count may be NULL. */
 int dl4ss_top_k_mask(const float* prob, int B, int N, float alpha, int top_k, float* mask, int* idx, int* count,
                      void* stream);
+/* dl4ss_attn_dot_fwd with an output row stride: mask[b * mask_stride + r] (K queries of one
+ * V (B,R,E) write a (B,K,R) mask without expanding V, the 414 MB copy of EvalVer.py:615-617). */
+int dl4ss_attn_dot_fwd_ex(const float* V, const float* q, int q_stride, int Bq, int R, int E, int act, float* mask,
+                          long long mask_stride, void* stream);
+
+/* ---- recursive extraction / speaker classifier ---- */
+/* Speaker choice of one recursion step (Torch_multi/main_run_multi_selfSS_recuReal_GRID.py:
+ * 227-244 top_k_mask with sort_index, 391-404 the seen-speaker filter), per row b:
+ * prob = sigmoid(logits) (GRID.py:197; may be NULL), sort_index (B,top_k) ids by descending
+ * prob (ties: lower id; -1 beyond N; may be NULL), chosen (B) = first id of sort_index not in
+ * prev (n_prev,B) (the ids chosen at earlier steps, -1 = none) if any prob > alpha, else -1
+ * (may be NULL).  top_k <= 64, N <= 8192. */
+int dl4ss_classifier_select(const float* logits, int B, int N, float alpha, int top_k, const int* prev, int n_prev,
+                            float* prob, int* sort_index, int* chosen, void* stream);
+/* pred = mask * x and resid = (1 - mask) * x, n elements (GRID.py:433-434 predict_multi_map,
+ * GRID.py:444 the residual spectrogram); pred or resid may be NULL. */
+int dl4ss_mask_split(const float* mask, const float* x, long long n, float* pred, float* resid, void* stream);
+/* mean over t of h (B,T,D) -> (B,D): the classifier's torch.mean(x, 1) (GRID.py:196,
+ * EvalVer.py:323) and ADDJUST's time mean (EvalVer.py:373). */
+int dl4ss_time_mean(const float* h, int B, int T, int D, float* mean_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -161,3 +161,37 @@ def test_golden_fixture_is_reproduced_by_oracle():
         np.testing.assert_allclose(S.real, g["re"][i], atol=1e-5)
         np.testing.assert_allclose(S.imag, g["im"][i], atol=1e-5)
         np.testing.assert_allclose(dsp.istft(S.T), g["y_rec"][i], atol=1e-6)
+
+
+def test_recursive_oracle_selection_known_answers():
+    """GRID.py:227-244 top_k_mask with sort_index and the seen-speaker filter (GRID.py:394-399)."""
+    from oracle import recursive as orc
+    prob = torch.tensor([[0.5, 0.9, 0.9, 0.2, 0.99], [0.1, 0.1, 0.2, 0.05, 0.3]])
+    final, sidx, cnt = orc.top_k_sort_index(prob, 0.5, 3)
+    assert sidx.tolist() == [[4, 1, 2], [4, 2, 0]]
+    assert cnt.tolist() == [3, 0]
+    assert final[0].tolist() == [0, 1, 1, 0, 1] and final[1].sum() == 0
+    assert orc.choose(sidx, cnt, [[4, 1], []]) == [2, -1]
+    assert orc.choose(sidx, cnt, [[4, 1, 2], []]) == [-1, -1]
+
+
+def test_recursive_oracle_two_steps_tiny():
+    """The loop on a tiny constant model: step 1 picks the classifier's top speaker, step 2
+    the best unseen one; final masks are computed on the original mixture."""
+    from oracle import recursive as orc
+    B, T, F, E, N = 1, 3, 4, 2, 5
+    emb = torch.randn(N, E, generator=torch.Generator().manual_seed(0))
+    V = torch.randn(B, T, F, E, generator=torch.Generator().manual_seed(1))
+    probs = [torch.tensor([[0.1, 0.8, 0.3, 0.9, 0.2]]), torch.tensor([[0.1, 0.2, 0.3, 0.95, 0.6]])]
+    calls = []
+
+    def cls(x):
+        calls.append(x.clone())
+        return probs[len(calls) - 1]
+
+    X = torch.rand(B, T, F) + 0.5
+    out = orc.recursive_extract(lambda x: (V, None), cls, emb, X)
+    assert out["spk"].tolist() == [[3, 4]]
+    m1 = torch.sigmoid(torch.einsum("btfe,e->btf", V, emb[3]))[0]
+    assert torch.allclose(calls[1][0], (1 - m1) * X[0])
+    assert torch.allclose(out["masks"][0, 1], torch.sigmoid(torch.einsum("btfe,e->btf", V, emb[4]))[0])

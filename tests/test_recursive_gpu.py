@@ -1,0 +1,135 @@
+"""Speaker classifier + recursive extraction (SURVEY R9 classifier, R17; GRID.py:178-199,
+227-244, 383-475) on the HIP path vs the oracle restatement (oracle/recursive.py).
+
+Bars: speaker ids (the chosen speaker of every step and the top-3 sort order) bit-exact;
+fp32: classifier probabilities 2e-5 abs, masks / predictions 1e-4 abs; bf16 (bf16 GEMM and
+recurrent-matvec operands): probabilities 1e-2 abs, masks 3e-2 abs, ids compared where the
+oracle's decision margin exceeds the bf16 error."""
+import numpy as np
+import pytest
+import torch
+
+from dl4ss_amd import engine, infer, synth
+from oracle import dsp
+from oracle import model as om
+from oracle import recursive as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _models(seed):
+    torch.manual_seed(seed)
+    mix = om.MixSpeech("gru", 129, 300, 2, 50)
+    cls = orc.Classifier(129, 600, 3, 101)
+    emb = torch.nn.Embedding(101, 50)
+    return mix, cls, emb
+
+
+def _feats(B, n, seed):
+    gen = synth.SyntheticMixtures(n_samples=n, k=2, seed=seed)
+    src, spk, u = gen.batch(B)
+    gains = synth.gains_for(u, 2)
+    out = []
+    for b in range(B):
+        srcs = [dsp.normalise_source(src[b, k], n) for k in range(2)]
+        _, m = dsp.mix_sources(srcs, gains[b])
+        out.append(dsp.magnitude(m))
+    return torch.from_numpy(np.array(out, dtype=np.float32))
+
+
+def _ours(dev, mix, cls, emb, B, T, precision):
+    net = engine.SepNet(cell="gru", num_layers=2, hidden=300, emb=50, num_labels=101, adjust=False, device=dev)
+    sd = {f"mix.{k}": v for k, v in mix.state_dict().items()}
+    sd["emb.layer.weight"] = emb.weight.detach()
+    net.load_state_dict(sd)
+    cnet = infer.ClassifierNet(129, 600, 3, 101, device=dev)
+    cnet.load_state_dict(cls.state_dict())
+    return infer.RecursiveExtractor(net, cnet, B, T, precision=precision)
+
+
+@pytest.mark.parametrize("B,n,seed", [(1, 128 * 39, 3), (2, 128 * 24, 5)])
+def test_recursive_fp32_matches_oracle(dev, B, n, seed):
+    mix, cls, emb = _models(seed)
+    X = _feats(B, n, seed)
+    T = X.shape[1]
+    with torch.no_grad():
+        ref = orc.recursive_extract(lambda x: mix(x), cls, emb.weight, X)
+    ex = _ours(dev, mix, cls, emb, B, T, "fp32")
+    out = ex.run(X.to(dev))
+    torch.cuda.synchronize()
+    assert torch.equal(out["spk"].cpu().long(), ref["spk"]), (out["spk"], ref["spk"])
+    for s in range(2):
+        assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < 2e-5
+        assert (out["step_pred"][s].cpu() - ref["step_pred"][:, s]).abs().max() < 1e-4
+    assert (out["masks"].cpu() - ref["masks"]).abs().max() < 1e-4
+    # top-3 order of the first step (GRID.py:235 sort_index)
+    _, sidx, _ = orc.top_k_sort_index(ref["probs"][0], -0.3, 3)
+    assert torch.equal(out["sort_index"][0].cpu().long(), sidx)
+
+
+def test_recursive_bf16_close(dev):
+    B, n, seed = 1, 128 * 39, 11
+    mix, cls, emb = _models(seed)
+    X = _feats(B, n, seed)
+    T = X.shape[1]
+    with torch.no_grad():
+        ref = orc.recursive_extract(lambda x: mix(x), cls, emb.weight, X)
+    out = _ours(dev, mix, cls, emb, B, T, "bf16").run(X.to(dev))
+    torch.cuda.synchronize()
+    for s in range(2):
+        assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < 1e-2
+    p = ref["probs"][0][0].sort(descending=True).values
+    if float(p[0] - p[1]) > 2e-2:  # decision margin above the bf16 error
+        assert int(out["spk"][0, 0]) == int(ref["spk"][0, 0])
+        assert (out["masks"][:, 0].cpu() - ref["masks"][:, 0]).abs().max() < 3e-2
+
+
+def test_classifier_select_and_test_mode(dev):
+    """Classifier probabilities + the test-mode top_k_mask selection (EvalVer.py:436-442)."""
+    B, n = 3, 128 * 20
+    _, cls, _ = _models(21)
+    X = _feats(B, n, 21)
+    T = X.shape[1]
+    with torch.no_grad():
+        p_ref = cls(X)
+    cnet = infer.ClassifierNet(129, 600, 3, 101, device=dev)
+    cnet.load_state_dict(cls.state_dict())
+    cf = infer.ClassifierForward(cnet, B, T, "fp32")
+    mask, idx, cnt = infer.select_speakers(cf, X.to(dev), alpha=-0.5, top_k=2)
+    torch.cuda.synchronize()
+    assert (cf.prob.cpu() - p_ref).abs().max() < 2e-5
+    assert torch.equal(mask.cpu(), om.top_k_mask(p_ref, -0.5, 2))
+    assert (cnt.cpu() == 2).all()
+    for b in range(B):
+        assert idx[b].cpu().tolist() == sorted(np.where(mask[b].cpu().numpy() == 1)[0].tolist())
+
+
+def test_classifier_select_kernel_edge_cases(dev):
+    """Ties (lower id first), the seen-speaker filter, nothing above alpha -> -1, top_k > N."""
+    from dl4ss_amd import _lib
+    logits = torch.tensor([[0.0, 2.0, 2.0, -1.0, 5.0],      # order 4, 1, 2, 0, 3
+                           [-9.0, -9.0, -8.0, -9.5, -7.0],  # all probs < 0.5
+                           [1.0, 1.0, 1.0, 1.0, 1.0]], device=dev)
+    B, N = logits.shape
+    prev = torch.tensor([[4, -1, 0], [1, -1, -1]], dtype=torch.int32, device=dev)  # (n_prev, B)
+    sidx = torch.empty(B, 3, dtype=torch.int32, device=dev)
+    ch = torch.empty(B, dtype=torch.int32, device=dev)
+    prob = torch.empty(B, N, device=dev)
+    _lib.call("dl4ss_classifier_select", _lib.ptr(logits), B, N, 0.5, 3, _lib.ptr(prev), 2, _lib.ptr(prob),
+              _lib.ptr(sidx), _lib.ptr(ch), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert sidx.cpu().tolist() == [[4, 1, 2], [4, 2, 0], [0, 1, 2]]
+    assert ch.cpu().tolist() == [2, -1, 1]  # row 0: 4 and 1 seen; row 1: none above 0.5; row 2: 0 seen
+    assert (prob.cpu() - torch.sigmoid(logits.cpu())).abs().max() < 1e-6
+    sidx6 = torch.empty(B, 6, dtype=torch.int32, device=dev)
+    _lib.call("dl4ss_classifier_select", _lib.ptr(logits), B, N, -1.0, 6, None, 0, None, _lib.ptr(sidx6), None,
+              _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert sidx6[:, 5].cpu().tolist() == [-1, -1, -1]
