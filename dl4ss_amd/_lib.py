@@ -53,6 +53,8 @@ SIGNATURES = {
     "dl4ss_classifier_select": [P, I, I, F, I, P, I, P, P, P, P],
     "dl4ss_mask_split": [P, P, LL, P, P, P],
     "dl4ss_time_mean": [P, I, I, I, P, P],
+    "dl4ss_bss_corr": [P, I, I, I, I, P, P],
+    "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
 }
 # entry points that return a value rather than a hipError_t
 RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,

@@ -5,9 +5,10 @@
 (dl4ss_istft_apply); ``write_batch_output`` writes the reference's
 ``batch_output/`` wav naming (PCM16 via the stdlib ``wave`` module).
 
-``cal`` needs BSS-eval SDR (``separation.bss_eval_sources``), a dependency the
-reference does not vendor: parity unpinned, listed as the
-next row; it raises until that row is built.
+``cal`` scores a ``batch_output/`` directory with BSS-eval SDR (bss_test.py:12-61): the
+reference's ``separation.bss_eval_sources`` is not vendored (SURVEY section 8c item 3);
+this build runs BSS_EVAL v3 on the GPU (``dl4ss_amd.bss``), parity unpinned against the
+reference's copy and pinned against the restatement in ``oracle/bss_eval.py``.
 """
 import os
 import wave
@@ -53,6 +54,40 @@ def write_batch_output(path, waves_pred, names, mix_wav=None, clean=None, rate=8
             _write_wav(os.path.join(path, f"{b}_True_mix.wav"), mix_wav[b], rate)
 
 
+def _read_wav(path):
+    """PCM16 -> float64 in [-1, 1) (soundfile.read's default scaling, bss_test.py:30-36)."""
+    with wave.open(path, "rb") as w:
+        if w.getsampwidth() != 2:
+            raise ValueError(f"{path}: only 16-bit PCM wavs are written by this build")
+        return np.frombuffer(w.readframes(w.getnframes()), dtype="<i2").astype(np.float64) / 32768.0
+
+
 def cal(path, aim_mix_number):
-    raise NotImplementedError("bss_test.cal needs BSS-eval SDR (separation.bss_eval_sources, not vendored by the "
-                              "reference): SURVEY section 8f row f2, not built yet")
+    """bss_test.py:12-61 (``add_slience_channel = 0``): per mixture index, the ``realTrue``
+    wavs are the references and the ``pre`` wavs the estimates (sorted file order); one
+    estimate against two references is repeated; returns the concatenated SDR arrays."""
+    from dl4ss_amd import bss
+
+    path = path if path.endswith(os.sep) else path + os.sep
+    wavs = sorted(l for l in os.listdir(path) if l[-3:] == "wav")
+    mix_number = len(set(l.split("_")[0] for l in wavs))
+    print("num of mixed :", mix_number)
+    sdr_sum = np.array([])
+    for idx in range(mix_number):
+        aim, pre = [], []
+        for l in wavs:
+            if l.split("_")[0] != str(idx):
+                continue
+            if "realTrue" in l:
+                aim.append(_read_wav(path + l))
+            if "pre" in l:
+                pre.append(_read_wav(path + l))
+        aim, pre = np.array(aim), np.array(pre)
+        if pre.shape[0] == 1 and aim.shape[0] == 2:
+            pre = pre.repeat(2, 0)
+        sdr, sir, sar, perm = bss.bss_eval_sources(torch.from_numpy(aim).float(), torch.from_numpy(pre).float())
+        result = (sdr[0], sir[0], sar[0], perm[0])
+        print(result)
+        sdr_sum = np.append(sdr_sum, result[0])
+    print("SDR here:", sdr_sum.mean())
+    return sdr_sum

@@ -214,6 +214,15 @@ int dl4ss_mask_split(const float* mask, const float* x, long long n, float* pred
  * EvalVer.py:323) and ADDJUST's time mean (EvalVer.py:373). */
 int dl4ss_time_mean(const float* h, int B, int T, int D, float* mean_out, void* stream);
 
+/* ---- BSS-eval (replaces the un-vendored separation.bss_eval_sources of
+ *      Torch_multi/bss_test.py:5,55 -- BSS_EVAL v3, 512-tap distortion filters) ---- */
+/* R (M,P,P,L) fp64: R[m][a][b][l] = sum_n x[m][a][n] x[m][b][n+l], l < L, x (M,P,N) fp32
+ * (the K references then the estimates of mixture m). */
+int dl4ss_bss_corr(const float* x, int M, int P, int N, int L, double* R, void* stream);
+/* From R: the Gram matrix of the delayed references G (M, K L, K L) (may be NULL), its
+ * diagonal blocks Gd (M, K, L, L) (may be NULL) and D (M, K L, P-K) = <delayed refs, est>. */
+int dl4ss_bss_gram(const double* R, int M, int P, int K, int L, double* G, double* Gd, double* D, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
