@@ -54,6 +54,7 @@ SIGNATURES = {
     "dl4ss_mask_split": [P, P, LL, P, P, P],
     "dl4ss_time_mean": [P, I, I, I, P, P],
     "dl4ss_bss_corr": [P, I, I, I, I, P, P],
+    "dl4ss_mix_sources_ex": [P, P, P, I, I, I, P, P, P, P],
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
 }
 # entry points that return a value rather than a hipError_t

@@ -13,26 +13,29 @@
 
 namespace {
 
-// one workgroup per source: fp64 mean and max|x - mean|
-__global__ __launch_bounds__(256) void source_stats_kernel(const float* __restrict__ raw, int N,
-                                                           float2* __restrict__ stats) {
-  const float* x = raw + (long long)blockIdx.x * N;
+// one workgroup per source: fp64 mean and max|x - mean| over its first len samples (a
+// shorter wav of a list file is normalised over its own length, then zero-padded:
+// predata_fromList_cRM_123.py:186-198)
+__global__ __launch_bounds__(256) void source_stats_kernel(const float* __restrict__ raw, int NS,
+                                                           const int* __restrict__ lens, float2* __restrict__ stats) {
+  const float* x = raw + (long long)blockIdx.x * NS;
+  const int N = lens ? min(max(lens[blockIdx.x], 0), NS) : NS;
   __shared__ double sd[4];
   __shared__ float sm[4];
   double s = 0.0;
   for (int i = threadIdx.x * 4; i < N; i += 1024) {
-    if (i + 3 < N) {
+    if (i + 3 < N && (NS & 3) == 0) {
       const float4 v = *reinterpret_cast<const float4*>(x + i);
       s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
     } else {
-      for (int k = i; k < N; ++k) s += x[k];
+      for (int k = i; k < N && k < i + 4; ++k) s += x[k];
     }
   }
   s = wave_sum_d(s);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   if (l == 0) sd[w] = s;
   __syncthreads();
-  const double mean = (sd[0] + sd[1] + sd[2] + sd[3]) / N;
+  const double mean = N > 0 ? (sd[0] + sd[1] + sd[2] + sd[3]) / N : 0.0;
   const float meanf = (float)mean;
   float m = 0.f;
   for (int i = threadIdx.x; i < N; i += 256) m = fmaxf(m, fabsf(x[i] - meanf));
@@ -47,8 +50,9 @@ __global__ __launch_bounds__(256) void source_stats_kernel(const float* __restri
 
 // grid (ceil(N/1024), B): normalise, gain, write sources and their sum
 __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw, const float2* __restrict__ stats,
-                                                  const float* __restrict__ gains, int K, int N,
-                                                  float* __restrict__ out_src, float* __restrict__ out_mix) {
+                                                  const float* __restrict__ gains, const int* __restrict__ lens,
+                                                  int K, int N, float* __restrict__ out_src,
+                                                  float* __restrict__ out_mix) {
   const int b = blockIdx.y;
   const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= N) return;
@@ -59,7 +63,8 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
     const float g = gains[src] * st.y;
     const float* x = raw + src * N;
     float* o = out_src + ((long long)b * K + k) * N;
-    if (i + 3 < N && ((N & 3) == 0)) {
+    const int len = lens ? min(max(lens[src], 0), N) : N;  // zero beyond the source's own length
+    if (i + 3 < len && ((N & 3) == 0)) {
       float4 v = *reinterpret_cast<const float4*>(x + i);
       v.x = (v.x - st.x) * g; v.y = (v.y - st.x) * g; v.z = (v.z - st.x) * g; v.w = (v.w - st.x) * g;
       *reinterpret_cast<float4*>(o + i) = v;
@@ -67,7 +72,7 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
     } else {
       float* a = &acc.x;
       for (int q = 0; q < 4 && i + q < N; ++q) {
-        const float v = (x[i + q] - st.x) * g;
+        const float v = i + q < len ? (x[i + q] - st.x) * g : 0.0f;
         o[i + q] = v;
         a[q] += v;
       }
@@ -84,15 +89,20 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
 
 }  // namespace
 
-DL4SS_API int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws,
-                                float* out_src, float* out_mix, void* stream) {
+DL4SS_API int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gains, int B, int K, int N,
+                                   float* stats_ws, float* out_src, float* out_mix, void* stream) {
   DL4SS_REQUIRE(raw && gains && out_src && out_mix && stats_ws && B >= 0 && K >= 1 && N > 0);
   if (B == 0) return 0;
-  hipLaunchKernelGGL(source_stats_kernel, dim3(B * K), dim3(256), 0, as_stream(stream), raw, N,
+  hipLaunchKernelGGL(source_stats_kernel, dim3(B * K), dim3(256), 0, as_stream(stream), raw, N, lengths,
                      reinterpret_cast<float2*>(stats_ws));
   DL4SS_CHECK_LAUNCH();
   hipLaunchKernelGGL(mix_kernel, dim3(cdiv(N, 1024), B), dim3(256), 0, as_stream(stream), raw,
-                     reinterpret_cast<const float2*>(stats_ws), gains, K, N, out_src, out_mix);
+                     reinterpret_cast<const float2*>(stats_ws), gains, lengths, K, N, out_src, out_mix);
   DL4SS_CHECK_LAUNCH();
   return 0;
+}
+
+DL4SS_API int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws,
+                                float* out_src, float* out_mix, void* stream) {
+  return dl4ss_mix_sources_ex(raw, nullptr, gains, B, K, N, stats_ws, out_src, out_mix, stream);
 }

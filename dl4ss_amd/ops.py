@@ -61,9 +61,10 @@ def istft(S, conj=False, out=None):
     return out
 
 
-def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None):
+def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=None):
     """raw (B, K, N) fp32 sources, gains (B, K) fp32 -> (scaled sources (B, K, N),
-    mixture (B, N)) -- normalise, gain, sum."""
+    mixture (B, N)) -- normalise, gain, sum.  lengths (B, K) int32: each
+    source's own length (normalised over it, zero beyond; list-file wavs)."""
     _f32c(raw, "mix_sources")
     _f32c(gains, "mix_sources(gains)")
     B, K, N = raw.shape
@@ -75,8 +76,10 @@ def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None):
         out_mix = torch.empty(B, N, device=raw.device, dtype=torch.float32)
     if stats_ws is None:
         stats_ws = torch.empty(B * K * 2, device=raw.device, dtype=torch.float32)
-    _lib.call("dl4ss_mix_sources", _lib.ptr(raw), _lib.ptr(gains), B, K, N, _lib.ptr(stats_ws), _lib.ptr(out_src),
-              _lib.ptr(out_mix), _lib.stream_ptr())
+    if lengths is not None and (lengths.dtype != torch.int32 or tuple(lengths.shape) != (B, K)):
+        raise RuntimeError("mix_sources: lengths must be (B, K) int32")
+    _lib.call("dl4ss_mix_sources_ex", _lib.ptr(raw), _lib.ptr(lengths), _lib.ptr(gains), B, K, N, _lib.ptr(stats_ws),
+              _lib.ptr(out_src), _lib.ptr(out_mix), _lib.stream_ptr())
     return out_src, out_mix
 
 

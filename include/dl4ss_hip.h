@@ -59,6 +59,11 @@ int dl4ss_istft_apply(const float* X_mix_c64, const float* aux, long long n_sig,
  * fromList_cRM_123 gain variants: gains are computed by the caller). */
 int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws, float* out_src,
                       float* out_mix, void* stream);
+/* As dl4ss_mix_sources, with per-source valid lengths (B*K int32; NULL = N): mean and peak
+ * over the first lengths[s] samples, zero beyond -- a list-file wav shorter than MAX_LEN
+ * (TDAA_beta/predata_fromList_cRM_123.py:186-201: crop, normalise, then zero-pad). */
+int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gains, int B, int K, int N,
+                         float* stats_ws, float* out_src, float* out_mix, void* stream);
 
 /* ---- dense contractions (MFMA) ------------------------------------------ */
 enum { DL4SS_EPI_NONE = 0, DL4SS_EPI_TANH = 1 };
