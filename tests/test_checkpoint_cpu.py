@@ -1,0 +1,56 @@
+"""Reference checkpoint compatibility: the per-module params/param_* files of
+EvalVer.py:677-690 (saved here in torch's legacy non-zip format, as torch-0.3 wrote them)
+load into SepNet / ClassifierNet through the weights_only loader, and save back."""
+import torch
+
+from dl4ss_amd import checkpoint, engine, infer
+from oracle import model as om
+from oracle import recursive as orc
+
+
+def test_load_reference_module_files(tmp_path):
+    torch.manual_seed(0)
+    ref = om.SepModel(cell="lstm", num_layers=4)
+    files = {}
+    for kind, mod in (("hidden3d", ref.mix), ("emblayer", ref.emb), ("adjlayer", ref.adj)):
+        p = str(tmp_path / f"param_mixdotadjust4lstmdot_WSJ0_{kind}_125")
+        torch.save(mod.state_dict(), p, _use_new_zipfile_serialization=False)
+        files[kind] = p
+    net = engine.SepNet(cell="lstm", num_layers=4, device="cpu", seed=3)
+    checkpoint.load_reference_params(net, **files)
+    for name, t in ref.state_dict().items():
+        assert torch.equal(net.view(name), t), name
+    out = checkpoint.save_reference_params(net, str(tmp_path / "out"), "x", 5)
+    net2 = engine.SepNet(cell="lstm", num_layers=4, device="cpu", seed=9)
+    checkpoint.load_reference_params(net2, **out)
+    assert torch.equal(net.flat, net2.flat)
+
+
+def test_load_reference_classifier_drops_cnn_keys(tmp_path):
+    torch.manual_seed(1)
+    cls = orc.Classifier(129, 600, 3, 101)
+    sd = dict(cls.state_dict())
+    sd["cnn.weight"] = torch.zeros(3)  # EvalVer.py:547-549 pops keys containing 'cnn'
+    p = str(tmp_path / "param_speech_2mix3lstm_best")
+    torch.save(sd, p, _use_new_zipfile_serialization=False)
+    cnet = infer.ClassifierNet(device="cpu")
+    checkpoint.load_reference_classifier(cnet, p)
+    for k, v in cls.state_dict().items():
+        assert torch.equal(cnet.view(k), v), k
+
+
+def test_strict_key_and_shape_errors(tmp_path):
+    p = str(tmp_path / "bad")
+    torch.save({"layer.weight_ih_l9": torch.zeros(2, 2)}, p)
+    net = engine.SepNet(cell="gru", num_layers=2, device="cpu", adjust=False)
+    try:
+        checkpoint.load_reference_params(net, hidden3d=p)
+        raise AssertionError("expected KeyError")
+    except KeyError:
+        pass
+    torch.save({"layer.weight": torch.zeros(5, 5)}, p)
+    try:
+        checkpoint.load_reference_params(net, emblayer=p)
+        raise AssertionError("expected ValueError")
+    except ValueError:
+        pass
