@@ -55,6 +55,8 @@ SIGNATURES = {
     "dl4ss_time_mean": [P, I, I, I, P, P],
     "dl4ss_bss_corr": [P, I, I, I, I, P, P],
     "dl4ss_mix_sources_ex": [P, P, P, I, I, I, P, P, P, P],
+    "dl4ss_gemm_bf16_set_tile": [I],
+    "dl4ss_gemm_bf16_lt": [I, I, I, I, I, P, LL, P, LL, P, LL, F, I, LL, LL, LL, P, LL, P],
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
 }
 # entry points that return a value rather than a hipError_t

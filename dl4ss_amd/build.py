@@ -22,6 +22,8 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-at
 # per-file extras: the STFT's radix-4x4 butterflies run 1.2-1.5x faster as scalar fp32
 # than SLP-packed into v_pk_add_f32 (the packing needs a v_mov per pair of operands)
 FILE_FLAGS = {"stft.hip": ["-fno-slp-vectorize"]}
+# hipBLASLt for the plain (epilogue-free) backward GEMMs (gemm_lt.hip)
+LINK = ["-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _newer(src, dst, deps):
@@ -56,7 +58,7 @@ def build(verbose=False, jobs=None):
             if verbose:
                 print("compiled", os.path.basename(obj), file=sys.stderr)
     if todo or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB, *LINK]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

@@ -24,8 +24,7 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64, LDK = BK + 8;
-constexpr int NT = 256;
+constexpr int BK = 64, LDK = BK + 8;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 enum { EPI_NONE = 0, EPI_TANH = 1 };
@@ -36,13 +35,13 @@ __device__ __forceinline__ float ftanh_fast(float x) { return 1.0f - 2.0f * __bu
 
 // One 8 x 8 block of one operand tile, staged in v[8] (16 B each).  KC: element (r,k)
 // at G[r*ld + k] (k contiguous); !KC: at G[k*ld + r].  Block (rb, kb): rows 8rb..+8,
-// k 8kb..+8.  Block index bi: KC -> rb = bi >> 3, kb = bi & 7 (a wave's 8 lanes of one
-// rb read 128 contiguous bytes); !KC -> kb = bi >> 4, rb = bi & 15 (16 lanes of one
-// k-row read 256 contiguous bytes).
-template <bool KC>
+// k 8kb..+8.  Block index bi (tile of ROWS rows): KC -> rb = bi >> 3, kb = bi & 7 (a
+// wave's 8 lanes of one rb read 128 contiguous bytes); !KC -> kb = bi / (ROWS/8),
+// rb = bi % (ROWS/8) (ROWS/8 lanes of one k-row read 2 ROWS contiguous bytes).
+template <bool KC, int ROWS>
 __device__ __forceinline__ void block_coords(int bi, int& rb, int& kb) {
   if (KC) { rb = bi >> 3; kb = bi & 7; }
-  else { kb = bi >> 4; rb = bi & 15; }
+  else { kb = bi / (ROWS / 8); rb = bi % (ROWS / 8); }
 }
 
 // mask of dword i of a 16-B chunk whose first n elements (of 8) are valid
@@ -128,23 +127,49 @@ __device__ __forceinline__ void store_block(const uint4 (&v)[8], unsigned short*
   }
 }
 
-// The k-loop of one staging role: this thread stages blocks of ONE operand (KC layout)
-// and all threads run the same MFMAs and barriers.  Hoisting the (wave-uniform) role
-// out of the loop keeps each loop's loads straight-line code.
-template <bool KC, bool VEC>
-__device__ __forceinline__ void kloop(f32x16 (&acc)[2][2], const unsigned short* __restrict__ G, long long ld,
-                                      int r0, int rmax, int kbeg, int kend, unsigned short* sOwn, const unsigned short* sA,
-                                      const unsigned short* sB, int bi, int lane, int wm, int wn) {
-  constexpr int NS = 3;  // register ring: loads of k-tiles kt+1 .. kt+2 in flight during tile kt
-  constexpr int BUF = BM * LDK;
+// Tile configurations (all k-tiles BK = 64, waves of WM x WN = (WM/32) x (WN/32)
+// v_mfma_f32_32x32x16_bf16 blocks, WN = 64):
+//   TILE_128x128: 4 waves (64 x 64 each), 256 threads, 2 workgroups per CU (73.7 KB LDS)
+//   TILE_256x128: 8 waves (64 x 64 each), 512 threads, 1 per CU (110.6 KB)
+//   TILE_256x256: 8 waves (128 x 64 each), 512 threads, 1 per CU (147.5 KB)
+// The larger tiles halve (256x256) or cut by a quarter (256x128) the operand bytes per
+// MFMA that every workgroup pulls through L2 -- the 128 x 128 tile needs ~2x the per-CU
+// L2 bandwidth at full MFMA rate.  Staging: threads [0, BM) stage A blocks, [BM, BM+BN)
+// B blocks, the rest (256x128: 128 threads) only run MFMAs; all share the barriers.
+template <int BM_, int BN_, int WM_, int WN_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int TI = WM / 32, TJ = WN / 32;
+  static constexpr int WAVES_N = BN / WN;
+  static constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  static constexpr int NS = TI * TJ > 4 ? 2 : 3;  // register ring depth (VGPR budget at 512 threads)
+  static_assert(WN == 64, "the epilogue maps 16 lanes x 4 columns onto a 64-wide wave tile");
+};
+typedef Tile<128, 128, 64, 64> T128x128;
+typedef Tile<256, 128, 64, 64> T256x128;
+typedef Tile<256, 256, 128, 64> T256x256;
+
+// The k-loop of one staging role: this thread stages blocks of ONE operand (KC layout,
+// ROWS-row tile) -- or none (STAGE false) -- and all threads run the same MFMAs and
+// barriers.  Hoisting the (wave-uniform) role out of the loop keeps each loop's loads
+// straight-line code.
+template <class TC, bool STAGE, bool KC, bool VEC, int ROWS>
+__device__ __forceinline__ void kloop(f32x16 (&acc)[TC::TI][TC::TJ], const unsigned short* __restrict__ G, long long ld,
+                                      int r0, int rmax, int kbeg, int kend, unsigned short* sOwn,
+                                      const unsigned short* sA, const unsigned short* sB, int bi, int lane, int wm,
+                                      int wn) {
+  constexpr int NS = TC::NS;  // register ring: loads of k-tiles kt+1 .. kt+NS-1 in flight during tile kt
+  constexpr int BUF_A = TC::BM * LDK, BUF_B = TC::BN * LDK, BUF_OWN = ROWS * LDK;
   uint4 v[NS][8];
-  int rb, kb;
-  block_coords<KC>(bi, rb, kb);
+  int rb = 0, kb = 0;
+  block_coords<KC, ROWS>(bi, rb, kb);
   const int nk = (kend - kbeg + BK - 1) / BK;
+  if constexpr (STAGE) {
 #pragma unroll
-  for (int u = 0; u < NS; ++u)
-    if (u < nk) load_block<KC, VEC>(v[u], G, ld, r0, rmax, kbeg + u * BK, kend, rb, kb);
-  store_block<KC>(v[0], sOwn, rb, kb);
+    for (int u = 0; u < NS; ++u)
+      if (u < nk) load_block<KC, VEC>(v[u], G, ld, r0, rmax, kbeg + u * BK, kend, rb, kb);
+    store_block<KC>(v[0], sOwn, rb, kb);
+  }
   __syncthreads();
   const int fr = lane & 31, fk = 8 * (lane >> 5);
   for (int kt0 = 0; kt0 < nk; kt0 += NS) {
@@ -153,42 +178,44 @@ __device__ __forceinline__ void kloop(f32x16 (&acc)[2][2], const unsigned short*
       const int kt = kt0 + u;
       if (kt < nk) {
         const int cur = kt & 1;
-        const unsigned short* a = sA + cur * BUF;
-        const unsigned short* b = sB + cur * BUF;
+        const unsigned short* a = sA + cur * BUF_A;
+        const unsigned short* b = sB + cur * BUF_B;
 #ifndef GBB_NO_MFMA
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 16) {
-          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(a + (wm + fr) * LDK + kk + fk);
-          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(a + (wm + 32 + fr) * LDK + kk + fk);
-          const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(b + (wn + fr) * LDK + kk + fk);
-          const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(b + (wn + 32 + fr) * LDK + kk + fk);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+          bf16x8 af[TC::TI], bfr[TC::TJ];
+#pragma unroll
+          for (int i = 0; i < TC::TI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a + (wm + 32 * i + fr) * LDK + kk + fk);
+#pragma unroll
+          for (int j = 0; j < TC::TJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(b + (wn + 32 * j + fr) * LDK + kk + fk);
+#pragma unroll
+          for (int i = 0; i < TC::TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TC::TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
 #endif
-        if (kt + 1 < nk) store_block<KC>(v[(u + 1) % NS], sOwn + (cur ^ 1) * BUF, rb, kb);
-        if (kt + NS < nk) load_block<KC, VEC>(v[u], G, ld, r0, rmax, kbeg + (kt + NS) * BK, kend, rb, kb);
+        if constexpr (STAGE) {
+          if (kt + 1 < nk) store_block<KC>(v[(u + 1) % NS], sOwn + (cur ^ 1) * BUF_OWN, rb, kb);
+          if (kt + NS < nk) load_block<KC, VEC>(v[u], G, ld, r0, rmax, kbeg + (kt + NS) * BK, kend, rb, kb);
+        }
         __syncthreads();
       }
     }
   }
 }
 
-template <bool A_KC, bool B_KC, int EPI, bool ATOMIC, bool VEC>
-__global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
-                                                        long long lda, const unsigned short* __restrict__ B,
-                                                        long long ldb, float* __restrict__ C, long long ldc,
-                                                        const float* __restrict__ bias, float beta, int k_per_split,
-                                                        int grid_m, int grid_n, long long sa, long long sb,
-                                                        long long sc) {
+template <class TC, bool A_KC, bool B_KC, int EPI, bool ATOMIC, bool VEC>
+__global__ __launch_bounds__(TC::NT, TC::NT == 256 ? 2 : 1) void gemm_bb_kernel(
+    int M, int N, int K, const unsigned short* __restrict__ A, long long lda, const unsigned short* __restrict__ B,
+    long long ldb, float* __restrict__ C, long long ldc, const float* __restrict__ bias, float beta, int k_per_split,
+    int grid_m, int grid_n, long long sa, long long sb, long long sc) {
+  constexpr int BM = TC::BM, BN = TC::BN, TI = TC::TI, TJ = TC::TJ;
   __shared__ __attribute__((aligned(16))) unsigned short sA[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short sB[2][BN * LDK];
   // batch member blockIdx.y (strided batch: element offsets sa, sb, sc)
   A += blockIdx.y * sa;
   B += blockIdx.y * sb;
   C += blockIdx.y * sc;
-  __shared__ __attribute__((aligned(16))) unsigned short sB[2][BN * LDK];
 
   const int ntiles = grid_m * grid_n;
   const int per_xcd = (ntiles + 7) / 8;
@@ -205,32 +232,35 @@ __global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, con
   if (kbeg >= kend) return;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = (wave / TC::WAVES_N) * TC::WM, wn = (wave % TC::WAVES_N) * TC::WN;
 
-  f32x16 acc[2][2];
+  f32x16 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  // threads 0-127 stage A, 128-255 stage B (wave-uniform)
-  if (tid < 128)
-    kloop<A_KC, VEC>(acc, A, lda, m0, M, kbeg, kend, &sA[0][0], &sA[0][0], &sB[0][0], tid, lane, wm, wn);
+  // threads [0, BM) stage A, [BM, BM + BN) stage B, the rest only compute (wave-uniform)
+  if (tid < BM)
+    kloop<TC, true, A_KC, VEC, BM>(acc, A, lda, m0, M, kbeg, kend, &sA[0][0], &sA[0][0], &sB[0][0], tid, lane, wm, wn);
+  else if (tid < BM + BN)
+    kloop<TC, true, B_KC, VEC, BN>(acc, B, ldb, n0, N, kbeg, kend, &sB[0][0], &sA[0][0], &sB[0][0], tid - BM, lane, wm,
+                                   wn);
   else
-    kloop<B_KC, VEC>(acc, B, ldb, n0, N, kbeg, kend, &sB[0][0], &sA[0][0], &sB[0][0], tid - 128, lane, wm, wn);
+    kloop<TC, false, true, VEC, BM>(acc, A, lda, m0, M, kbeg, kend, &sA[0][0], &sA[0][0], &sB[0][0], 0, lane, wm, wn);
 
   // epilogue.  acc[i][j][r] holds (row wm + 32i + (r&3) + 8(r>>2) + 4(lane>>5), col
-  // wn + 32j + (lane&31)).  Non-atomic: each wave stages its 64 x 64 fp32 sub-tile in
-  // LDS (the operand buffers are free after the last barrier; 16 KB per wave, row
-  // stride 68 floats) and writes it back as 16-B stores, 16 lanes per 256-B row.
+  // wn + 32j + (lane&31)).  Non-atomic: each wave stages one 32-row block (i) of its
+  // sub-tile at a time in LDS (the operand buffers are free after the last barrier;
+  // 32 x 68 fp32 per wave) and writes it back as 16-B stores, 16 lanes per 256-B row.
   const bool add_bias = bias && blockIdx.z == 0;
   if constexpr (ATOMIC) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < TJ; ++j) {
         const int col = n0 + wn + 32 * j + (lane & 31);
         if (col >= N) continue;
         const float bv = add_bias ? bias[col] : 0.0f;
@@ -242,16 +272,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, con
       }
   } else {
     constexpr int SLD = 68;
-    float* stage = reinterpret_cast<float*>(&sA[0][0]) + wave * 64 * SLD;  // 4 x 17 KB <= sA + sB
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          stage[(32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * SLD + 32 * j + (lane & 31)] = acc[i][j][r];
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
+    float* stage = reinterpret_cast<float*>(&sA[0][0]) + wave * 32 * SLD;  // 8.7 KB per wave
     const int c4 = 4 * (lane & 15);  // this lane's 4 columns of the wave's 64
     const int col = n0 + wn + c4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -262,64 +283,99 @@ __global__ __launch_bounds__(NT, 2) void gemm_bb_kernel(int M, int N, int K, con
       bv.w = col + 3 < N ? bias[col + 3] : 0.f;
     }
     const bool vec_c = (ldc % 4 == 0) && ((((uintptr_t)C) & 15) == 0) && col + 4 <= N;
-#pragma unroll 4
-    for (int rr = 0; rr < 64; rr += 4) {
-      const int rl = rr + (lane >> 4);
-      const int row = m0 + wm + rl;
-      if (row >= M) continue;
-      float4 x = *reinterpret_cast<const float4*>(stage + rl * SLD + c4);
-      x.x += bv.x; x.y += bv.y; x.z += bv.z; x.w += bv.w;
-      float* cp = C + (long long)row * ldc + col;
-      if (vec_c) {
-        if (beta != 0.0f) {
-          const float4 o = *reinterpret_cast<const float4*>(cp);
-          x.x += beta * o.x; x.y += beta * o.y; x.z += beta * o.z; x.w += beta * o.w;
-        }
-        if (EPI == EPI_TANH) { x.x = ftanh_fast(x.x); x.y = ftanh_fast(x.y); x.z = ftanh_fast(x.z); x.w = ftanh_fast(x.w); }
-        *reinterpret_cast<float4*>(cp) = x;
-      } else {
-        const float xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if (col + c >= N) break;
-          float y = xs[c];
-          if (beta != 0.0f) y += beta * cp[c];
-          if (EPI == EPI_TANH) y = ftanh_fast(y);
-          cp[c] = y;
+    for (int i = 0; i < TI; ++i) {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          stage[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * SLD + 32 * j + (lane & 31)] = acc[i][j][r];
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll 4
+      for (int rr = 0; rr < 32; rr += 4) {
+        const int rl = rr + (lane >> 4);
+        const int row = m0 + wm + 32 * i + rl;
+        if (row >= M) continue;
+        float4 x = *reinterpret_cast<const float4*>(stage + rl * SLD + c4);
+        x.x += bv.x; x.y += bv.y; x.z += bv.z; x.w += bv.w;
+        float* cp = C + (long long)row * ldc + col;
+        if (vec_c) {
+          if (beta != 0.0f) {
+            const float4 o = *reinterpret_cast<const float4*>(cp);
+            x.x += beta * o.x; x.y += beta * o.y; x.z += beta * o.z; x.w += beta * o.w;
+          }
+          if (EPI == EPI_TANH) { x.x = ftanh_fast(x.x); x.y = ftanh_fast(x.y); x.z = ftanh_fast(x.z); x.w = ftanh_fast(x.w); }
+          *reinterpret_cast<float4*>(cp) = x;
+        } else {
+          const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (col + c >= N) break;
+            float y = xs[c];
+            if (beta != 0.0f) y += beta * cp[c];
+            if (EPI == EPI_TANH) y = ftanh_fast(y);
+            cp[c] = y;
+          }
         }
       }
     }
   }
 }
 
-template <bool A_KC, bool B_KC>
-int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
-           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
-           long long sb, long long sc, hipStream_t st) {
-  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
-  if (splitk < 1) splitk = 1;
-  int kps = (K + splitk - 1) / splitk;
-  kps = (kps + BK - 1) / BK * BK;
-  splitk = (K + kps - 1) / kps;
-  const int ntiles = gm * gn;
-  dim3 grid(8 * ((ntiles + 7) / 8), batch, splitk);
-  // straight-line 16-B loads need 16-B aligned rows (ld % 8 == 0) and base pointers
-  const bool vec = lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ldb % 8 == 0 && ((uintptr_t)B & 15) == 0 &&
-                   (batch == 1 || (sa % 8 == 0 && sb % 8 == 0));
-  if (splitk > 1 && (epi != EPI_NONE || beta != 1.0f)) return (int)hipErrorInvalidValue;
-#define GBB_LAUNCH(EPI_, AT_, VEC_)                                                                             \
-  hipLaunchKernelGGL((gemm_bb_kernel<A_KC, B_KC, EPI_, AT_, VEC_>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, C, \
-                     ldc, bias, beta, kps, gm, gn, sa, sb, sc)
+// tile choice: 0 = automatic (gemm_tile_for), else a forced TILE_* (tuning: tools/gemm_bench_bf16.py)
+enum { TILE_AUTO = 0, TILE_128x128 = 1, TILE_256x128 = 2, TILE_256x256 = 3 };
+int g_tile_override = TILE_AUTO;
+
+int gemm_tile_for(int M, int N, int K, int splitk, int batch) {
+  (void)M; (void)N; (void)K; (void)splitk; (void)batch;
+  return TILE_128x128;
+}
+
+template <class TC, bool A_KC, bool B_KC>
+void launch_tile(bool vec, int splitk, int epi, dim3 grid, int M, int N, int K, const unsigned short* A, long long lda,
+                 const unsigned short* B, long long ldb, float* C, long long ldc, const float* bias, float beta,
+                 int kps, int gm, int gn, long long sa, long long sb, long long sc, hipStream_t st) {
+#define GBB_LAUNCH(EPI_, AT_, VEC_)                                                                                 \
+  hipLaunchKernelGGL((gemm_bb_kernel<TC, A_KC, B_KC, EPI_, AT_, VEC_>), grid, dim3(TC::NT), 0, st, M, N, K, A, lda, B, \
+                     ldb, C, ldc, bias, beta, kps, gm, gn, sa, sb, sc)
   if (vec) {
     if (splitk > 1) GBB_LAUNCH(EPI_NONE, true, true);
     else if (epi == EPI_TANH) GBB_LAUNCH(EPI_TANH, false, true);
     else GBB_LAUNCH(EPI_NONE, false, true);
-  } else {
+  } else if constexpr (TC::NT == 256) {  // unaligned operands: the 128 x 128 tile only
     if (splitk > 1) GBB_LAUNCH(EPI_NONE, true, false);
     else if (epi == EPI_TANH) GBB_LAUNCH(EPI_TANH, false, false);
     else GBB_LAUNCH(EPI_NONE, false, false);
   }
 #undef GBB_LAUNCH
+}
+
+template <bool A_KC, bool B_KC>
+int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
+           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
+           long long sb, long long sc, hipStream_t st) {
+  if (splitk < 1) splitk = 1;
+  // straight-line 16-B loads need 16-B aligned rows (ld % 8 == 0) and base pointers
+  const bool vec = lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ldb % 8 == 0 && ((uintptr_t)B & 15) == 0 &&
+                   (batch == 1 || (sa % 8 == 0 && sb % 8 == 0));
+  int tc = g_tile_override ? g_tile_override : gemm_tile_for(M, N, K, splitk, batch);
+  if (!vec) tc = TILE_128x128;
+  const int BMt = tc == TILE_128x128 ? 128 : 256, BNt = tc == TILE_256x256 ? 256 : 128;
+  const int gm = (M + BMt - 1) / BMt, gn = (N + BNt - 1) / BNt;
+  int kps = (K + splitk - 1) / splitk;
+  kps = (kps + BK - 1) / BK * BK;
+  splitk = (K + kps - 1) / kps;
+  const int ntiles = gm * gn;
+  dim3 grid(8 * ((ntiles + 7) / 8), batch, splitk);
+  if (splitk > 1 && (epi != EPI_NONE || beta != 1.0f)) return (int)hipErrorInvalidValue;
+#define GBB_ARGS vec, splitk, epi, grid, M, N, K, A, lda, B, ldb, C, ldc, bias, beta, kps, gm, gn, sa, sb, sc, st
+  if (tc == TILE_256x256) launch_tile<T256x256, A_KC, B_KC>(GBB_ARGS);
+  else if (tc == TILE_256x128) launch_tile<T256x128, A_KC, B_KC>(GBB_ARGS);
+  else launch_tile<T128x128, A_KC, B_KC>(GBB_ARGS);
+#undef GBB_ARGS
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
@@ -370,6 +426,13 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const unsigned short* 
 }
 
 }  // namespace
+
+// tuning knob (tools/gemm_bench_bf16.py): force a tile configuration (0 = automatic)
+DL4SS_API int dl4ss_gemm_bf16_set_tile(int tile) {
+  DL4SS_REQUIRE(tile >= TILE_AUTO && tile <= TILE_256x256);
+  g_tile_override = tile;
+  return 0;
+}
 
 // y[r*ldy + c] = bf16(x[r*ldx + c]) for c < cols, 0 for cols <= c < ldy (row padding for 16-B rows)
 DL4SS_API int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy,

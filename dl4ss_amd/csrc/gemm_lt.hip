@@ -1,0 +1,106 @@
+// Plain bf16-operand GEMMs through hipBLASLt: the weight-gradient and input-gradient
+// contractions of the backward pass (dW_lin, dH, dW_ih, dW_hh, dX), which carry no fused
+// epilogue.  The fused forward GEMMs (input projection + bias, Linear + bias + tanh) stay on
+// the hand-written MFMA kernel (gemm_bb.hip).
+//
+// Semantics are those of dl4ss_gemm_bf16_batched (row-major C[M,N] = op(A) op(B) + beta C,
+// A stored M x K or K x M (transA), B stored K x N or N x K (transB), bf16 operands, fp32
+// C and accumulation).  hipBLASLt is column-major, so the call computes the transposed
+// product C^T = op(B)^T op(A)^T on the same memory.  One hipBLASLt handle per device
+// (std::call_once); the heuristic's first algorithm is cached per problem (mutex-guarded),
+// so a step's repeated shapes pay the query once.  The workspace is the caller's.
+#include "common.h"
+
+#include <hipblaslt/hipblaslt.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace {
+
+struct LtKey {
+  int ta, tb, M, N, K, batch, beta0;
+  long long lda, ldb, ldc, sa, sb, sc, ws;
+  bool operator<(const LtKey& o) const {
+    return std::tie(ta, tb, M, N, K, batch, beta0, lda, ldb, ldc, sa, sb, sc, ws) <
+           std::tie(o.ta, o.tb, o.M, o.N, o.K, o.batch, o.beta0, o.lda, o.ldb, o.ldc, o.sa, o.sb, o.sc, o.ws);
+  }
+};
+
+struct LtPlan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+  size_t ws = 0;
+};
+
+constexpr int MAX_DEV = 16;
+hipblasLtHandle_t g_handle[MAX_DEV] = {};
+std::once_flag g_once[MAX_DEV];
+std::mutex g_mu;
+std::map<std::pair<int, LtKey>, LtPlan> g_plans;
+
+hipblasLtMatrixLayout_t layout(hipDataType t, uint64_t rows, uint64_t cols, int64_t ld, int batch, int64_t stride) {
+  hipblasLtMatrixLayout_t l = nullptr;
+  if (hipblasLtMatrixLayoutCreate(&l, t, rows, cols, ld) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+  if (batch > 1) {
+    int32_t b = batch;
+    hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &b, sizeof(b));
+    hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &stride, sizeof(stride));
+  }
+  return l;
+}
+
+}  // namespace
+
+DL4SS_API int dl4ss_gemm_bf16_lt(int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                                 const void* B, long long ldb, float* C, long long ldc, float beta, int batch,
+                                 long long strideA, long long strideB, long long strideC, void* workspace,
+                                 long long ws_bytes, void* stream) {
+  DL4SS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && A && B && C && batch >= 1 && ws_bytes >= 0);
+  DL4SS_REQUIRE(ws_bytes == 0 || workspace);
+  if (M == 0 || N == 0) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return (int)hipErrorInvalidDevice;
+  std::call_once(g_once[dev], [dev] { hipblasLtCreate(&g_handle[dev]); });
+  if (!g_handle[dev]) return (int)hipErrorNotInitialized;
+  const LtKey key{transA, transB, M, N, K, batch, beta == 0.0f, lda, ldb, ldc, strideA, strideB, strideC, ws_bytes};
+  LtPlan plan;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_plans.find({dev, key});
+    if (it != g_plans.end()) {
+      plan = it->second;
+    } else {
+      // column-major view: first operand op(B)^T (N x K), second op(A)^T (K x M), C^T (N x M)
+      const hipblasOperation_t opx = transB ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+      const hipblasOperation_t opy = transA ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+      if (hipblasLtMatmulDescCreate(&plan.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS)
+        return (int)hipErrorInvalidValue;
+      hipblasLtMatmulDescSetAttribute(plan.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opx, sizeof(opx));
+      hipblasLtMatmulDescSetAttribute(plan.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opy, sizeof(opy));
+      plan.la = transB ? layout(HIP_R_16BF, K, N, ldb, batch, strideB) : layout(HIP_R_16BF, N, K, ldb, batch, strideB);
+      plan.lb = transA ? layout(HIP_R_16BF, M, K, lda, batch, strideA) : layout(HIP_R_16BF, K, M, lda, batch, strideA);
+      plan.lc = layout(HIP_R_32F, N, M, ldc, batch, strideC);
+      if (!plan.la || !plan.lb || !plan.lc) return (int)hipErrorInvalidValue;
+      hipblasLtMatmulPreference_t pref = nullptr;
+      hipblasLtMatmulPreferenceCreate(&pref);
+      uint64_t wsmax = (uint64_t)ws_bytes;
+      hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsmax, sizeof(wsmax));
+      hipblasLtMatmulHeuristicResult_t res[1];
+      int nres = 0;
+      const hipblasStatus_t hs = hipblasLtMatmulAlgoGetHeuristic(g_handle[dev], plan.desc, plan.la, plan.lb, plan.lc,
+                                                                 plan.lc, pref, 1, res, &nres);
+      hipblasLtMatmulPreferenceDestroy(pref);
+      if (hs != HIPBLAS_STATUS_SUCCESS || nres < 1) return (int)hipErrorNotSupported;
+      plan.algo = res[0].algo;
+      plan.ws = res[0].workspaceSize;
+      g_plans[{dev, key}] = plan;
+    }
+  }
+  const float alpha = 1.0f;
+  const hipblasStatus_t s = hipblasLtMatmul(g_handle[dev], plan.desc, &alpha, B, plan.la, A, plan.lb, &beta, C,
+                                            plan.lc, C, plan.lc, &plan.algo, workspace, plan.ws, as_stream(stream));
+  return s == HIPBLAS_STATUS_SUCCESS ? 0 : (int)hipErrorLaunchFailure;
+}

@@ -16,6 +16,7 @@ reference / oracle state dict loads directly) and all gradients in a second
 flat buffer: one all-reduce and one Adam launch per step.
 """
 import math
+import os
 
 import torch
 
@@ -170,6 +171,8 @@ class SepTrainer:
         # kernel writes bf16 dPre, the weights and the layer-0 features are converted once per
         # step.  Rows are padded to multiples of 8 (16-B aligned operand rows).
         self.fast = precision == "bf16" and self.rnn_precision == "bf16"
+        # bf16 mode: the plain backward GEMMs through hipBLASLt (DL4SS_GEMM_LT=0: the hand-written kernel)
+        self.use_lt = self.fast and os.environ.get("DL4SS_GEMM_LT", "1") != "0"
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
             p8 = lambda n: (n + 7) // 8 * 8
@@ -298,11 +301,18 @@ class SepTrainer:
         cell = CELLS[net.cell]
         dPreb = self.dPreb[:, :FE]
         hLb = self.outb[-1][:, :2 * H]
-        ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
+        lt = self.use_lt  # plain (epilogue-free) GEMMs through hipBLASLt, else the hand-written kernel
+        if lt:
+            ops.gemm_bf16_lt(dPreb, hLb, net.view("mix.Linear.weight", g), transA=True, beta=1.0)
+        else:
+            ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
         _lib.call("dl4ss_colsum_bf16", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                   _lib.ptr(net.view("mix.Linear.bias", g)), st)
         dH = self.dH[0]
-        ops.gemm_bf16(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk="auto")
+        if lt:
+            ops.gemm_bf16_lt(dPreb, self.wb_lin[:, :2 * H], dH)
+        else:
+            ops.gemm_bf16(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk="auto")
         hp8 = self.p8(H)
         for l in range(net.L - 1, -1, -1):
             _lib.call("dl4ss_birnn_bwd_ex", cell, 1, B, T, H, _lib.ptr(dH),
@@ -313,15 +323,24 @@ class SepTrainer:
                       _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self.rnn_ws), self.ws_bytes,
                       _lib.ptr(self.status), st)
             xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
-            ops.gemm_bf16(self.dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0)
             dGhb = self.dGhb if self.dGhb is not None else self.dGb
             whh_g = net.cat_view("weight_hh", l, g)
-            # both directions in one launch: member d = columns d*NGH of dGh, d*pad8(H) of h_{t-1}
-            ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
-                                  NGH, H, BT, transA=True, beta=1.0, splitk="auto")
-            if l > 0:
+            if l > 0:  # the input gradient first: it is all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
-                ops.gemm_bf16(self.dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")
+                if lt:
+                    ops.gemm_bf16_lt(self.dGb, self.wb_ih[l][:, :2 * H], dH_next)
+                else:
+                    ops.gemm_bf16(self.dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")
+            # both directions' dW_hh in one launch: member d = columns d*NGH of dGh, d*pad8(H) of h_{t-1}
+            if lt:
+                ops.gemm_bf16_lt(self.dGb, xb, net.cat_view("weight_ih", l, g), transA=True, beta=1.0)
+                ops.gemm_bf16_lt(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], transA=True, beta=1.0, batch=2,
+                                 strideA=NGH, strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT)
+            else:
+                ops.gemm_bf16(self.dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0)
+                ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
+                                      NGH, H, BT, transA=True, beta=1.0, splitk="auto")
+            if l > 0:
                 dH = dH_next
 
     def backward(self):

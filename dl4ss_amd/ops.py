@@ -143,6 +143,11 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
 GEMM_BF16_TARGET_WGS = 256  # measured best on MI355X (tools/gemm_bench_bf16.py sweep: 256/512/768)
 
 
+def gemm_bf16_set_tile(tile):
+    """Force the bf16 GEMM tile configuration (0 automatic, 1 128x128, 2 256x128, 3 256x256)."""
+    _lib.call("dl4ss_gemm_bf16_set_tile", int(tile))
+
+
 def _mat_bf16(t, name):
     if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
         raise RuntimeError(f"{name}: expected a 2-D row-major bfloat16 CUDA matrix (unit inner stride)")
@@ -180,6 +185,31 @@ def gemm_bf16(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, be
     _lib.call("dl4ss_gemm_bf16", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
               _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue,
               float(beta), int(splitk), _lib.stream_ptr())
+    return out
+
+
+LT_WS_BYTES = 32 << 20  # hipBLASLt workspace cap (allocated once per device)
+_lt_ws = {}
+
+
+def gemm_bf16_lt(A, B, out, transA=False, transB=False, beta=0.0, batch=1, strideA=0, strideB=0, strideC=0,
+                 M=None, N=None, K=None):
+    """out (fp32) = op(A) @ op(B) + beta*out with bf16 A, B through hipBLASLt
+    (dl4ss_gemm_bf16_lt): the plain backward GEMMs.  Layout conventions as gemm_bf16; with
+    batch > 1 the member offsets are raw element strides from the given first-member views."""
+    _mat_bf16(A, "gemm_bf16_lt(A)")
+    _mat_bf16(B, "gemm_bf16_lt(B)")
+    _mat(out, "gemm_bf16_lt(out)")
+    if M is None:
+        M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
+        N = B.shape[0] if transB else B.shape[1]
+    dev = A.device
+    ws = _lt_ws.get(dev)
+    if ws is None:
+        ws = _lt_ws[dev] = torch.empty(LT_WS_BYTES, dtype=torch.uint8, device=dev)
+    _lib.call("dl4ss_gemm_bf16_lt", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
+              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), float(beta), int(batch),
+              int(strideA), int(strideB), int(strideC), _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
     return out
 
 

@@ -90,6 +90,16 @@ int dl4ss_gemm_bf16_batched(int transA, int transB, int M, int N, int K, const v
                             long long strideC, void* stream);
 /* y[i] = bf16(x[i]) (round to nearest even), n elements; x 16-B aligned, y 8-B aligned. */
 int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream);
+/* Plain bf16-operand GEMM (no epilogue) through hipBLASLt: the backward pass's weight /
+ * input gradients (dW_lin, dH, dW_ih, dW_hh, dX of EvalVer.py:673's autograd).  Semantics
+ * of dl4ss_gemm_bf16_batched with epilogue NONE and no split-K; workspace (may be NULL when
+ * ws_bytes is 0) is the caller's. */
+int dl4ss_gemm_bf16_lt(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
+                       long long ldb, float* C, long long ldc, float beta, int batch, long long strideA,
+                       long long strideB, long long strideC, void* workspace, long long ws_bytes, void* stream);
+/* Tuning knob of dl4ss_gemm_bf16[_batched]: force a tile configuration for later calls
+ * (0 automatic, 1 = 128x128 / 4 waves, 2 = 256x128 / 8 waves, 3 = 256x256 / 8 waves). */
+int dl4ss_gemm_bf16_set_tile(int tile);
 
 /* 2-D form with row padding: y[r*ldy + c] = bf16(x[r*ldx + c]) (c < cols), 0 up to ldy. */
 int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, void* stream);

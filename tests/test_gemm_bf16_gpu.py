@@ -20,10 +20,18 @@ SHAPES = [(300, 200, 129), (8032 // 4, 600, 600), (130, 257, 1000), (64, 70, 8),
           (250, 130, 136)]
 
 
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "t128x128", "t256x128", "t256x256"])
+def tile(request):
+    """every tile configuration of gemm_bb.hip (forced through dl4ss_gemm_bf16_set_tile)"""
+    ops.gemm_bf16_set_tile(request.param)
+    yield request.param
+    ops.gemm_bf16_set_tile(0)
+
+
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_gemm_bf16_bit_identical(dev, ta, tb, M, N, K):
+def test_gemm_bf16_bit_identical(dev, ta, tb, M, N, K, tile):
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)
     A = torch.randn(*((K, M) if ta else (M, K)), generator=g).to(dev)
     B = torch.randn(*((N, K) if tb else (K, N)), generator=g).to(dev)
@@ -34,7 +42,7 @@ def test_gemm_bf16_bit_identical(dev, ta, tb, M, N, K):
     assert torch.equal(ours, ref)
 
 
-def test_gemm_bf16_tanh_beta_splitk(dev):
+def test_gemm_bf16_tanh_beta_splitk(dev, tile):
     g = torch.Generator(device="cpu").manual_seed(5)
     A = torch.randn(700, 300, generator=g).to(dev)
     B = torch.randn(450, 300, generator=g).to(dev)
@@ -55,7 +63,7 @@ def test_gemm_bf16_tanh_beta_splitk(dev):
     assert ((ours - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
-def test_gemm_bf16_padded_rows(dev):
+def test_gemm_bf16_padded_rows(dev, tile):
     """operands as column slices of row-padded bf16 buffers (the producers' layout)"""
     g = torch.Generator(device="cpu").manual_seed(9)
     A = torch.randn(333, 136, generator=g).to(dev)[:, :129]
@@ -75,7 +83,7 @@ def test_to_bf16_matches_torch_rne(dev):
     assert torch.equal(ops.to_bf16(x), x.to(torch.bfloat16))
 
 
-def test_gemm_bf16_batched_matches_members(dev):
+def test_gemm_bf16_batched_matches_members(dev, tile):
     """two column blocks of one matrix in one launch (the per-direction W_hh gradients)"""
     g = torch.Generator(device="cpu").manual_seed(11)
     BT, NGH, H, hp8 = 700, 120, 30, 32
@@ -86,6 +94,37 @@ def test_gemm_bf16_batched_matches_members(dev):
     out = torch.zeros(2 * NGH, H, device=dev)
     ops.gemm_bf16_batched(D[:, :NGH], Hb[:, :H], out[:NGH], 2, NGH, hp8, NGH * H, NGH, H, BT, transA=True, beta=1.0,
                           splitk=3)
+    for d in range(2):
+        ref = ops.gemm_bf16(D[:, d * NGH:(d + 1) * NGH], Hb[:, d * hp8:d * hp8 + H], transA=True)
+        assert ((out[d * NGH:(d + 1) * NGH] - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("ta,tb", [(True, False), (False, False), (False, True), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(2400, 600, 8032), (8032, 600, 2400), (300, 129, 77), (1, 5, 3)])
+def test_gemm_bf16_lt_matches_kernel(dev, ta, tb, M, N, K):
+    """hipBLASLt path (the plain backward GEMMs) vs the hand-written bf16 kernel on the same
+    bf16 operands: same products, different fp32 summation order (1e-5 of the max)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = ops.to_bf16(torch.randn(*((K, M) if ta else (M, K)), generator=g).to(dev))
+    B = ops.to_bf16(torch.randn(*((N, K) if tb else (K, N)), generator=g).to(dev))
+    C0 = torch.randn(M, N, generator=g).to(dev)
+    ref = ops.gemm_bf16(A, B, transA=ta, transB=tb, out=C0.clone(), beta=0.5)
+    ours = ops.gemm_bf16_lt(A, B, C0.clone(), transA=ta, transB=tb, beta=0.5)
+    torch.cuda.synchronize()
+    assert ((ours - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+def test_gemm_bf16_lt_batched(dev):
+    """both W_hh gradient directions in one strided-batch call (the engine's dW_hh)"""
+    g = torch.Generator(device="cpu").manual_seed(12)
+    BT, NGH, H, hp8 = 700, 120, 30, 32
+    D = ops.to_bf16(torch.randn(BT, 2 * NGH, generator=g).to(dev))
+    Hb = torch.zeros(BT, 2 * hp8, device=dev, dtype=torch.bfloat16)
+    Hb[:, :H] = torch.randn(BT, H, generator=g).to(dev).to(torch.bfloat16)
+    Hb[:, hp8:hp8 + H] = torch.randn(BT, H, generator=g).to(dev).to(torch.bfloat16)
+    out = torch.zeros(2 * NGH, H, device=dev)
+    ops.gemm_bf16_lt(D[:, :NGH], Hb[:, :H], out[:NGH], transA=True, beta=1.0, batch=2, strideA=NGH, strideB=hp8,
+                     strideC=NGH * H, M=NGH, N=H, K=BT)
     for d in range(2):
         ref = ops.gemm_bf16(D[:, d * NGH:(d + 1) * NGH], Hb[:, d * hp8:d * hp8 + H], transA=True)
         assert ((out[d * NGH:(d + 1) * NGH] - ref).abs().max() / ref.abs().max()).item() < 1e-5

@@ -13,6 +13,8 @@ from gemm_bench import SHAPES  # noqa: E402
 def main():
     if len(sys.argv) > 1:
         ops.GEMM_BF16_TARGET_WGS = int(sys.argv[1])
+    tile = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    ops.gemm_bf16_set_tile(tile)
     dev = torch.device("cuda")
     total = 0.0
     for name, ta, tb, M, N, K, sk, epi in SHAPES:
@@ -36,7 +38,8 @@ def main():
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / it
         total += ms
-        print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "us": round(ms * 1e3, 1),
+        print(json.dumps({"gemm": name, "tile": tile, "wgs": ops.GEMM_BF16_TARGET_WGS, "M": M, "N": N, "K": K,
+                          "us": round(ms * 1e3, 1),
                           "TFLOP/s": round(2.0 * M * N * K / (ms * 1e-3) / 1e12, 1)}), flush=True)
     print(json.dumps({"operands": "bf16", "sum_us_one_each": round(total * 1e3, 1)}))
 

@@ -26,7 +26,7 @@ def build_stamps():
             subprocess.run([B.HIPCC, *B.FLAGS, "-DRNN_STAMPS", *DEFS, "-I", B.CSRC, "-c", os.path.join(B.CSRC, f), "-o", o],
                            check=True)
             objs.append(o)
-    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", LIB], check=True)
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", LIB, *B.LINK], check=True)
 
 
 def main():

@@ -27,7 +27,7 @@ def build():
             subprocess.run([B.HIPCC, *B.FLAGS, *B.FILE_FLAGS.get(f, []), "-DRNN_TRACE", *sys.argv[2:], "-I", B.CSRC,
                             "-c", os.path.join(B.CSRC, f), "-o", o], check=True)
             objs.append(o)
-    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", LIB], check=True)
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", LIB, *B.LINK], check=True)
 
 
 def main():

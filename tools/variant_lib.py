@@ -26,7 +26,7 @@ def main(tag, defs):
     with cf.ThreadPoolExecutor(8) as ex:
         objs = list(ex.map(comp, srcs))
     lib = os.path.join(ROOT, "dl4ss_amd", f"libdl4ss_hip_{tag}.so")
-    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", lib], check=True)
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", lib, *B.LINK], check=True)
     print(lib)
 
 
