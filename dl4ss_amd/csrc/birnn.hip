@@ -87,6 +87,26 @@ __device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.
 __device__ __forceinline__ float ftanh(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f; }
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+// Sum of the NG producers' dh partials p[i * stride] (BPTT cell phase): for NG <= 16 all
+// loads are issued at once and added as a pairwise tree.  (A runtime-bound loop compiled to
+// an 8-wide unrolled body plus a remainder loop with one LDS round trip per iteration:
+// ~800 of the cell phase's ~1500 cycles per step at NG = 15.)
+__device__ __forceinline__ float sum_partials(const float* p, int stride, int NG) {
+  if (NG > 16) {
+    float a = 0.0f;
+    for (int i = 0; i < NG; ++i) a += p[i * stride];
+    return a;
+  }
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = i < NG ? p[i * stride] : 0.0f;
+#pragma unroll
+  for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+    for (int i = 0; i < w; ++i) v[i] += v[i + w];
+  return v[0];
+}
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
   unsigned u = __float_as_uint(f);
@@ -990,8 +1010,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
     // ---- cell backward for (b, u): LDS operands only, global stores only
     if (ct) {
       float dh_rec = 0.0f;
-      if (s > 0)
-        for (int p = 0; p < NG; ++p) dh_rec += sdh[(p * BC + cb) * J + cu];
+      if (s > 0) dh_rec = sum_partials(sdh + cb * J + cu, BC * J, NG);
       const float* op = sop + (s & 1) * BC * J * 8 + tid * 8;
       const float dout = op[0] + doutb;
       const float act[4] = {op[1], op[2], op[3], op[4]};
@@ -1296,8 +1315,32 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 
   // ---- waves 0-3: cell backward, then MFMA partials and their publish
   float sbi[NGATE], sbh[NGATE];  // this cell's bias-gradient sums over t
+  float pgi[NGATE], pgh[NGATE];  // this step's dG / dGh, stored after the publish
+  int pt = 0;
 #pragma unroll
-  for (int q = 0; q < NGATE; ++q) sbi[q] = sbh[q] = 0.0f;
+  for (int q = 0; q < NGATE; ++q) sbi[q] = sbh[q] = pgi[q] = pgh[q] = 0.0f;
+  auto store_dg = [&]() {
+    if (!cval) return;
+    const long long go = (long long)((bg * T + pt) * 2 + d) * GH + cj;
+    if (a.dG) {
+#pragma unroll
+      for (int q = 0; q < NGATE; ++q) a.dG[go + q * H] = pgi[q];
+    }
+    if (a.dGb) {
+#pragma unroll
+      for (int q = 0; q < NGATE; ++q) a.dGb[go + q * H] = bf16_rne(pgi[q]);
+    }
+    if (CELL == CELL_GRU) {
+      if (a.dGh) {
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) a.dGh[go + q * H] = pgh[q];
+      }
+      if (a.dGhb) {
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) a.dGhb[go + q * H] = bf16_rne(pgh[q]);
+      }
+    }
+  };
   for (int s = 0; s < T; ++s) {
     const int t = d == 0 ? T - 1 - s : s;
     STAMP(0)
@@ -1309,8 +1352,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       for (int q = 0; q < NGATE; ++q) dgi[q] = dgh[q] = 0.0f;
       if (cval) {
         float dh_rec = 0.0f;
-        if (s > 0)
-          for (int p = 0; p < NG; ++p) dh_rec += sdh[(p * BC + cb) * J + cu];
+        if (s > 0) dh_rec = sum_partials(sdh + cb * J + cu, BC * J, NG);
         const float* op = sop + (s & 1) * BC * 32 * 8 + tid * 8;
         const float dout = op[0] + doutb;
         const float act[4] = {op[1], op[2], op[3], op[4]};
@@ -1341,29 +1383,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           dgh[1] = dgi[1];
           dgh[2] = dnp * rg;
         }
-        const long long go = (long long)((bg * T + t) * 2 + d) * GH + cj;
-        if (a.dG) {
-#pragma unroll
-          for (int q = 0; q < NGATE; ++q) a.dG[go + q * H] = dgi[q];
-        }
-        if (a.dGb) {
-#pragma unroll
-          for (int q = 0; q < NGATE; ++q) a.dGb[go + q * H] = bf16_rne(dgi[q]);
-        }
-        if (CELL == CELL_GRU) {
-          if (a.dGh) {
-#pragma unroll
-            for (int q = 0; q < NGATE; ++q) a.dGh[go + q * H] = dgh[q];
-          }
-          if (a.dGhb) {
-#pragma unroll
-            for (int q = 0; q < NGATE; ++q) a.dGhb[go + q * H] = bf16_rne(dgh[q]);
-          }
-        }
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
           sbi[q] += dgi[q];
           sbh[q] += dgh[q];
+          pgi[q] = dgi[q];
+          pgh[q] = dgh[q];
         }
       }
       if (ct) {
@@ -1371,13 +1396,18 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         for (int q = 0; q < NGATE; ++q) sdgb[cb * SDG + q * J + cu] = bf16_rne(dgh[q]);
       }
     }
+    pt = t;
     STAMP(2)
     __syncthreads();  // B2
     STAMP(3)
-    if (s + 1 == T) break;  // nothing flows past the sequence start
+    if (s + 1 == T) {  // nothing flows past the sequence start
+      store_dg();
+      break;
+    }
     // ---- D[k][b] = sum_r W[r][k] dgh[b][r] per 16-unit tile, transposed through
     //      wave-private LDS to [b][unit], packed four units per 16-B store
     {
+#ifndef BWD_REG_PUBLISH  // transpose each tile through wave-private LDS: 2 store rounds (measured faster)
       const unsigned short* bp = sdgb + (lane & 15) * SDG + 8 * (lane >> 4);
       bf16x8 bv[KSRMAX];
 #pragma unroll
@@ -1409,7 +1439,40 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, (off + copy_g) * 8, 0, 16);    // safe: sc1
         }
       }
+#else
+      // the 16 x 16 accumulator lane holds 4 consecutive units 4(lane>>4) + i of batch column
+      // lane & 15: one packed quad, published straight from the registers (every tile's MFMA
+      // chain issued first, then the stores) -- no LDS round trip on the critical path
+      const unsigned short* bp = sdgb + (lane & 15) * SDG + 8 * (lane >> 4);
+      bf16x8 bv[KSRMAX];
+#pragma unroll
+      for (int ks = 0; ks < KSRMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
+      f32x4 acc[MTWMAX];
+#pragma unroll
+      for (int t2 = 0; t2 < MTWMAX; ++t2) acc[t2] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KSRMAX; ++ks)
+#pragma unroll
+        for (int t2 = 0; t2 < MTWMAX; ++t2)
+          acc[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t2][ks], bv[ks], acc[t2], 0, 0, 0);
+      STAMP(4)
+      const int col = lane & 15;
+      const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
+#pragma unroll
+      for (int t2 = 0; t2 < MTWMAX; ++t2) {
+        const int k = (wv * MTWMAX + t2) * 16 + 4 * (lane >> 4);
+        if (col < BC && k < H) {
+          const unsigned r0 = pack24(acc[t2][0]), r1 = pack24(acc[t2][1]), r2 = pack24(acc[t2][2]),
+                         r3 = pack24(acc[t2][3]);
+          const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
+          const int off = (((s & 1) * 2 * NG + w) * BC + col) * HG + (k >> 1);  // granules, fast copy
+          __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);                // fast: plain
+          __builtin_amdgcn_raw_buffer_store_b128(x, xr, (off + copy_g) * 8, 0, 16);    // safe: sc1
+        }
+      }
+#endif
     }
+    store_dg();  // this step's dG / dGh, after the publish (off the critical path)
     STAMP(6)
   }
   // fused bias gradients: one atomic per (cell, gate) for the whole sequence
