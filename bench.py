@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--no-stft-standalone", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=24)
     ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the RCCL process group even at world size 1 (exercises the DP path)")
     return ap.parse_args()
 
 
@@ -123,7 +125,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=dev)
@@ -287,7 +289,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args, N, K)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg is not None:
         import torch.distributed as dist
 
         dist.destroy_process_group()

@@ -24,9 +24,11 @@ def allreduce_mean_(flat, pg=None):
     """grad <- mean over ranks of the per-rank grads.  Every rank's loss is a mean
     over its own equal-sized shard, so the mean of the per-rank gradients is the
     gradient of the global-batch mean loss (the single-GPU reference's objective)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return flat
     n = world(pg)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=pg)  # also at world size 1 (bench --dist)
     if n > 1:
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=pg)
         flat.mul_(1.0 / n)
     return flat
 
