@@ -44,6 +44,7 @@ constexpr int KGLMAX = 6;    // bwd k per thread
 constexpr int HMAX = 320;    // largest hidden size of the training kernels (sizes per-thread offset arrays)
 constexpr int HMAX_L = 640;  // largest hidden size of the forward-only (inference) instantiations: the
                              // H = 600 speaker classifier of EvalVer.py:305-326 / GRID.py:178-199
+constexpr int DL4SS_RNN_WS_ZEROED = 0x100;  // precision flag: workspace already zero (no memset)
 constexpr unsigned SPIN_LIMIT = 1u << 20;  // ~1 s of polling: a stuck hand-off exits, never hangs
 
 typedef unsigned long long u64;
@@ -1672,6 +1673,8 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
                                  const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
                                  void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
+  const bool prezeroed = precision & DL4SS_RNN_WS_ZEROED;  // the caller zeroed the workspace (one fill per step)
+  precision &= ~DL4SS_RNN_WS_ZEROED;
   DL4SS_REQUIRE(precision == 0 || precision == 1);
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && out && act && workspace && status);
   DL4SS_REQUIRE(cell == CELL_GRU || cs);
@@ -1682,8 +1685,10 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
   const long long groups = 2LL * p.nchunk;
   const bool mf = precision == 1;
   const bool pk = mf && p.fwd_pk && T < 65535;
-  hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.BC * p.NG * 8 * 8 : groups * 2 * p.BC * H * 8, st);
-  if (e != hipSuccess) return (int)e;
+  if (!prezeroed) {
+    hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.BC * p.NG * 8 * 8 : groups * 2 * p.BC * H * 8, st);
+    if (e != hipSuccess) return (int)e;
+  }
   // the bf16 copies, and dropping the fp32 h_{t-1} (only the GRU BPTT reads it), need the packed kernel
   DL4SS_REQUIRE(pk || (!out_bf16 && !hprev_bf16 && hprev));
   DL4SS_REQUIRE(hprev || cell == CELL_LSTM);
@@ -1720,6 +1725,8 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
                                  float* db_ih, float* db_hh, void* workspace, long long ws_bytes, int* status,
                                  void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
+  const bool prezeroed = precision & DL4SS_RNN_WS_ZEROED;
+  precision &= ~DL4SS_RNN_WS_ZEROED;
   DL4SS_REQUIRE(precision == 0 || precision == 1);
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && workspace && status);
   DL4SS_REQUIRE(dG || dG_bf16);
@@ -1733,8 +1740,11 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   const bool mf = precision == 1;
   const bool pk = mf && p.bwd_pk && T < 65535;
   const long long HG = ((H + 1) / 2 + 1) & ~1;
-  hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.NG * p.BC * HG * 8 : groups * 2 * p.NG * p.BC * H * 8, st);
-  if (e != hipSuccess) return (int)e;
+  if (!prezeroed) {
+    hipError_t e =
+        hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.NG * p.BC * HG * 8 : groups * 2 * p.NG * p.BC * H * 8, st);
+    if (e != hipSuccess) return (int)e;
+  }
   // bf16 gradient copies, dropping the fp32 ones and the fused bias sums need the packed kernel
   DL4SS_REQUIRE(pk || (!dG_bf16 && !dGh_bf16 && !db_ih && !db_hh && dG && (cell == CELL_LSTM || dGh)));
   RnnArgs a{};

@@ -409,20 +409,72 @@ __global__ void f32_to_bf16_2d_kernel(const float* __restrict__ x, long long ldx
   y[i] = o;
 }
 
-// out[n] += sum_m A[m*lda + n] for bf16 A (bias gradients from bf16 dPre)
-__global__ __launch_bounds__(256) void colsum_bf16_kernel(const unsigned short* __restrict__ A, long long lda, int M,
-                                                          int N, int rows_per_block, float* __restrict__ out) {
-  __shared__ float s[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+// Several row-padded fp32 -> bf16 conversions in one launch (the step's bf16 weight copies):
+// segment i converts rows x cols of x[i] (row stride ldx) into y[i] (row stride ldy, zero
+// padding beyond cols).
+constexpr int CVT_MAX = 8;
+struct CvtSegs {
+  const float* x[CVT_MAX];
+  unsigned short* y[CVT_MAX];
+  long long ldx[CVT_MAX], ldy[CVT_MAX], start[CVT_MAX + 1];  // element prefix over rows * ldy
+  int cols[CVT_MAX];
+  int n;
+};
+__global__ __launch_bounds__(256) void f32_to_bf16_multi_kernel(CvtSegs sg) {
+  const long long total = sg.start[sg.n];
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    int g = 0;
+#pragma unroll
+    for (int j = 1; j < CVT_MAX; ++j) g += (j < sg.n && i >= sg.start[j]) ? 1 : 0;
+    const long long e = i - sg.start[g];
+    const long long r = e / sg.ldy[g], c = e - r * sg.ldy[g];
+    unsigned short o = 0;
+    if (c < sg.cols[g]) {
+      const unsigned u = __float_as_uint(sg.x[g][r * sg.ldx[g] + c]);
+      o = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    }
+    sg.y[g][e] = o;
+  }
+}
+
+// out[n] += sum_m A[m*lda + n] for bf16 A (bias gradients from bf16 dPre); VEC: 8 columns per
+// lane with 16-B loads (lda % 8 == 0, aligned base), a 64-lane row segment covers 512 columns
+template <bool VEC>
+__global__ __launch_bounds__(256) void colsum_bf16_v_kernel(const unsigned short* __restrict__ A, long long lda, int M,
+                                                            int N, int rows_per_block, float* __restrict__ out) {
+  constexpr int CPL = VEC ? 8 : 1;
+  __shared__ float s[4][64 * CPL];
+  const int c0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * CPL;
   const int rl = threadIdx.x >> 6;
   const int m0 = blockIdx.y * rows_per_block;
   const int m1 = min(M, m0 + rows_per_block);
-  float acc = 0.f;
-  if (c < N)
-    for (int m = m0 + rl; m < m1; m += 4) acc += __uint_as_float((unsigned)A[(long long)m * lda + c] << 16);
-  s[rl][threadIdx.x & 63] = acc;
+  float acc[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) acc[j] = 0.f;
+  if (c0 < N) {
+    if constexpr (VEC) {
+      for (int m = m0 + rl; m < m1; m += 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(A + (long long)m * lda + c0);
+        const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[2 * j] += __uint_as_float(w[j] << 16);
+          acc[2 * j + 1] += __uint_as_float(w[j] & 0xFFFF0000u);
+        }
+      }
+    } else {
+      for (int m = m0 + rl; m < m1; m += 4) acc[0] += __uint_as_float((unsigned)A[(long long)m * lda + c0] << 16);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) s[rl][(threadIdx.x & 63) * CPL + j] = acc[j];
   __syncthreads();
-  if (rl == 0 && c < N) atomicAdd(out + c, s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
+  if (rl == 0)
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int l = (threadIdx.x & 63) * CPL + j;
+      if (c0 + j < N) atomicAdd(out + c0 + j, (s[0][l] + s[1][l]) + (s[2][l] + s[3][l]));
+    }
 }
 
 }  // namespace
@@ -450,8 +502,36 @@ DL4SS_API int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, floa
   DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
   if (M == 0 || N == 0) return 0;
   const int rpb = 256;
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(cdiv(N, 64), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<const unsigned short*>(A), lda, M, N, rpb, out);
+  const auto* a = reinterpret_cast<const unsigned short*>(A);
+  if (lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && lda >= ((N + 7) & ~7))  // 16-B rows, padding readable
+    hipLaunchKernelGGL(colsum_bf16_v_kernel<true>, dim3(cdiv(N, 512), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
+                       a, lda, M, N, rpb, out);
+  else
+    hipLaunchKernelGGL(colsum_bf16_v_kernel<false>, dim3(cdiv(N, 64), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
+                       a, lda, M, N, rpb, out);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+DL4SS_API int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ldx, const int* rows,
+                                         const int* cols, void* const* y, const long long* ldy, void* stream) {
+  DL4SS_REQUIRE(n >= 1 && n <= CVT_MAX && x && ldx && rows && cols && y && ldy);
+  CvtSegs sg{};
+  sg.n = n;
+  sg.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    DL4SS_REQUIRE(x[i] && y[i] && rows[i] >= 0 && cols[i] >= 0 && ldx[i] >= cols[i] && ldy[i] >= cols[i] && ldy[i] > 0);
+    sg.x[i] = x[i];
+    sg.y[i] = reinterpret_cast<unsigned short*>(y[i]);
+    sg.ldx[i] = ldx[i];
+    sg.ldy[i] = ldy[i];
+    sg.cols[i] = cols[i];
+    sg.start[i + 1] = sg.start[i] + (long long)rows[i] * ldy[i];
+  }
+  for (int i = n + 1; i <= CVT_MAX; ++i) sg.start[i] = sg.start[n];
+  if (sg.start[n] == 0) return 0;
+  const unsigned grid = (unsigned)min(16384LL, cdiv(sg.start[n], 256));
+  hipLaunchKernelGGL(f32_to_bf16_multi_kernel, dim3(grid), dim3(256), 0, as_stream(stream), sg);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

@@ -13,53 +13,90 @@
 
 namespace {
 
-// one workgroup per source: fp64 mean and max|x - mean| over its first len samples (a
-// shorter wav of a list file is normalised over its own length, then zero-padded:
-// predata_fromList_cRM_123.py:186-198)
+// Statistics of a source over its first len samples (a shorter wav of a list file is
+// normalised over its own length, then zero-padded: predata_fromList_cRM_123.py:186-198):
+// NSPLIT workgroups per source each reduce one chunk in ONE pass to {fp64 sum, min, max};
+// the mixing kernel combines the NSPLIT partials in fixed order.  max|x - m| is taken as
+// max(max x - m, m - min x): fp32 subtraction is monotonic, so this equals the per-element
+// max of |fl(x - m)| exactly (the previous form re-read the source in a second pass).
+constexpr int NSPLIT = 8;
+struct SrcPart {
+  double sum;
+  float mn, mx;
+};
+static_assert(sizeof(SrcPart) == 16, "16-B partials");
+
 __global__ __launch_bounds__(256) void source_stats_kernel(const float* __restrict__ raw, int NS,
-                                                           const int* __restrict__ lens, float2* __restrict__ stats) {
-  const float* x = raw + (long long)blockIdx.x * NS;
-  const int N = lens ? min(max(lens[blockIdx.x], 0), NS) : NS;
-  __shared__ double sd[4];
-  __shared__ float sm[4];
+                                                           const int* __restrict__ lens, SrcPart* __restrict__ part) {
+  const int src = blockIdx.x, p = blockIdx.y;
+  const float* x = raw + (long long)src * NS;
+  const int N = lens ? min(max(lens[src], 0), NS) : NS;
+  const int chunk = ((N + NSPLIT - 1) / NSPLIT + 3) & ~3;
+  const int i0 = min(N, p * chunk), i1 = min(N, i0 + chunk);
   double s = 0.0;
-  for (int i = threadIdx.x * 4; i < N; i += 1024) {
-    if (i + 3 < N && (NS & 3) == 0) {
+  float mn = INFINITY, mx = -INFINITY;
+  const bool vec = (NS & 3) == 0;
+  for (int i = i0 + threadIdx.x * 4; i < i1; i += 1024) {
+    if (vec && i + 3 < i1) {
       const float4 v = *reinterpret_cast<const float4*>(x + i);
-      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+      s += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+      mn = fminf(fminf(mn, fminf(v.x, v.y)), fminf(v.z, v.w));
+      mx = fmaxf(fmaxf(mx, fmaxf(v.x, v.y)), fmaxf(v.z, v.w));
     } else {
-      for (int k = i; k < N && k < i + 4; ++k) s += x[k];
+      for (int k = i; k < i1 && k < i + 4; ++k) {
+        s += x[k];
+        mn = fminf(mn, x[k]);
+        mx = fmaxf(mx, x[k]);
+      }
     }
   }
   s = wave_sum_d(s);
+  mx = wave_max(mx);
+  mn = -wave_max(-mn);
+  __shared__ double sd[4];
+  __shared__ float smn[4], smx[4];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  if (l == 0) sd[w] = s;
-  __syncthreads();
-  const double mean = N > 0 ? (sd[0] + sd[1] + sd[2] + sd[3]) / N : 0.0;
-  const float meanf = (float)mean;
-  float m = 0.f;
-  for (int i = threadIdx.x; i < N; i += 256) m = fmaxf(m, fabsf(x[i] - meanf));
-  m = wave_max(m);
-  if (l == 0) sm[w] = m;
+  if (l == 0) { sd[w] = s; smn[w] = mn; smx[w] = mx; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float mx = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
-    stats[blockIdx.x] = make_float2(meanf, mx > 0.f ? 1.0f / mx : 0.f);
+    SrcPart r;
+    r.sum = (sd[0] + sd[1]) + (sd[2] + sd[3]);
+    r.mn = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+    r.mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+    part[src * NSPLIT + p] = r;
   }
 }
 
 // grid (ceil(N/1024), B): normalise, gain, write sources and their sum
-__global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw, const float2* __restrict__ stats,
+__global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw, const SrcPart* __restrict__ part,
                                                   const float* __restrict__ gains, const int* __restrict__ lens,
                                                   int K, int N, float* __restrict__ out_src,
                                                   float* __restrict__ out_mix) {
   const int b = blockIdx.y;
+  // per-source (mean, 1 / max|x - mean|) from the NSPLIT partials, fixed order
+  __shared__ float2 sstat[16];
+  if (threadIdx.x < K) {
+    const long long src = (long long)b * K + threadIdx.x;
+    const int len = lens ? min(max(lens[src], 0), N) : N;
+    double s = 0.0;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int p = 0; p < NSPLIT; ++p) {
+      const SrcPart r = part[src * NSPLIT + p];
+      s += r.sum;
+      mn = fminf(mn, r.mn);
+      mx = fmaxf(mx, r.mx);
+    }
+    const float meanf = len > 0 ? (float)(s / len) : 0.f;
+    const float pk = len > 0 ? fmaxf(mx - meanf, meanf - mn) : 0.f;
+    sstat[threadIdx.x] = make_float2(meanf, pk > 0.f ? 1.0f / pk : 0.f);
+  }
+  __syncthreads();
   const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= N) return;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int k = 0; k < K; ++k) {
     const long long src = (long long)b * K + k;
-    const float2 st = stats[src];
+    const float2 st = sstat[k];
     const float g = gains[src] * st.y;
     const float* x = raw + src * N;
     float* o = out_src + ((long long)b * K + k) * N;
@@ -91,13 +128,14 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
 
 DL4SS_API int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gains, int B, int K, int N,
                                    float* stats_ws, float* out_src, float* out_mix, void* stream) {
-  DL4SS_REQUIRE(raw && gains && out_src && out_mix && stats_ws && B >= 0 && K >= 1 && N > 0);
+  DL4SS_REQUIRE(raw && gains && out_src && out_mix && stats_ws && B >= 0 && K >= 1 && K <= 16 && N > 0);
+  DL4SS_REQUIRE(((uintptr_t)stats_ws & 15) == 0);
   if (B == 0) return 0;
-  hipLaunchKernelGGL(source_stats_kernel, dim3(B * K), dim3(256), 0, as_stream(stream), raw, N, lengths,
-                     reinterpret_cast<float2*>(stats_ws));
+  SrcPart* part = reinterpret_cast<SrcPart*>(stats_ws);
+  hipLaunchKernelGGL(source_stats_kernel, dim3(B * K, NSPLIT), dim3(256), 0, as_stream(stream), raw, N, lengths, part);
   DL4SS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(mix_kernel, dim3(cdiv(N, 1024), B), dim3(256), 0, as_stream(stream), raw,
-                     reinterpret_cast<const float2*>(stats_ws), gains, lengths, K, N, out_src, out_mix);
+  hipLaunchKernelGGL(mix_kernel, dim3(cdiv(N, 1024), B), dim3(256), 0, as_stream(stream), raw, part, gains, lengths, K,
+                     N, out_src, out_mix);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

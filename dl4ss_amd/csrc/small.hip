@@ -38,86 +38,137 @@ __global__ __launch_bounds__(256) void time_mean_kernel(const float* __restrict_
   }
 }
 
-// one workgroup per utterance: K*W outputs, each a (D + W)-long dot product
-__global__ __launch_bounds__(256) void query_fwd_kernel(const float* __restrict__ mean, int D,
-                                                        const int* __restrict__ idx, const float* __restrict__ emb,
-                                                        const float* __restrict__ wadj, int K, int W,
-                                                        float* __restrict__ q) {
-  extern __shared__ float sm[];
-  float* smean = sm;       // [D]
-  float* se = sm + D;      // [K][W]
-  const int b = blockIdx.x;
-  if (wadj)
-    for (int c = threadIdx.x; c < D; c += blockDim.x) smean[c] = mean[(long long)b * D + c];
-  for (int i = threadIdx.x; i < K * W; i += blockDim.x) {
-    const int k = i / W, o = i % W;
-    const int id = idx[b * K + k];
-    se[i] = id >= 0 ? emb[(long long)id * W + o] : 0.0f;  // id -1: no speaker (zero query)
+// q[b,k,o] = Emb[idx[b,k]][o] (+ sum_c W_adj[o][c] cat[b,k][c]), cat = [mean_t h[b] ; Emb[idx[b,k]]]:
+// one 64-lane wave per (o, b) (grid W x B): lanes stride c with coalesced loads of the W_adj
+// row and the mean, all K outputs accumulated together, then a wave reduction.  (A thread
+// per output walking its 650-long row issued one dependent L2 load per iteration: 26 us.)
+__global__ __launch_bounds__(64) void query_fwd_kernel(const float* __restrict__ mean, int D,
+                                                       const int* __restrict__ idx, const float* __restrict__ emb,
+                                                       const float* __restrict__ wadj, int K, int W,
+                                                       float* __restrict__ q) {
+  constexpr int KMAX = 4;  // queries per wave; grid.z covers K in groups of 4
+  const int o = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  const int k0 = blockIdx.z * KMAX;
+  idx += k0;
+  q += (long long)k0 * W;
+  const int Kg = min(KMAX, K - k0);
+  int id[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) id[k] = k < Kg ? idx[b * K + k] : -1;
+  float acc[KMAX] = {0.f, 0.f, 0.f, 0.f};
+  if (wadj) {
+    const float* wr = wadj + (long long)o * (D + W);
+    const float* mb = mean + (long long)b * D;
+#pragma unroll 4
+    for (int c = lane; c < D; c += 64) {
+      const float wv = wr[c] * mb[c];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) acc[k] += wv;  // the mean part is shared by every k
+    }
+    for (int c = lane; c < W; c += 64) {
+      const float wv = wr[D + c];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < Kg && id[k] >= 0) acc[k] = fmaf(wv, emb[(long long)id[k] * W + c], acc[k]);
+    }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < K * W; i += blockDim.x) {
-    const int k = i / W, o = i % W;
-    float v = se[i];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (k >= Kg) break;
+    const float r = wave_sum(acc[k]);
+    if (lane == 0) q[((long long)b * K + k) * W + o] = (id[k] >= 0 ? emb[(long long)id[k] * W + o] : 0.0f) + r;
+  }
+}
+
+// Backward of the queries (thread per output, every sum over <= 64 terms, loads unrolled):
+//   dh_bcast[b][c] = sum_o W[o][c] u[b][o] / T,   u[b][o] = sum_k dq[b,k,o]   (c < D)
+//   dEmb[idx[b,k]][c] += dq[b,k,c] + sum_o W[o][D + c] dq[b,k,o]              (atomics)
+//   dW_adj[o][c] += sum_b u[b][o] mean[b][c]  (c < D);  sum_{b,k} dq[b,k,o] Emb[idx[b,k]][c-D]
+// Every dh / dW_adj element has one owner thread and a fixed summation order; only the
+// embedding rows (speaker ids shared across the batch) use atomics.
+__global__ __launch_bounds__(64) void query_bwd_dh_kernel(const float* __restrict__ dq,
+                                                          const float* __restrict__ wadj, int T, int D, int K,
+                                                          int W, float* __restrict__ dh_bcast) {
+  const int b = blockIdx.y, c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= D) return;
+  const float* dqb = dq + (long long)b * K * W;
+  float g0 = 0.f, g1 = 0.f;
+#pragma unroll 5
+  for (int o = 0; o < W; ++o) {
+    float u = 0.f;
+    for (int k = 0; k < K; ++k) u += dqb[k * W + o];
+    const float t = wadj[(long long)o * (D + W) + c] * u;
+    if (o & 1) g1 += t; else g0 += t;
+  }
+  dh_bcast[(long long)b * D + c] = (g0 + g1) / (float)T;
+}
+
+__global__ __launch_bounds__(64) void query_bwd_emb_kernel(const float* __restrict__ dq, const int* __restrict__ idx,
+                                                           const float* __restrict__ wadj, int D, int W,
+                                                           float* __restrict__ demb) {
+  const int bk = blockIdx.x;
+  const float* dqr = dq + (long long)bk * W;
+  const int id = idx[bk];
+  for (int c = threadIdx.x; c < W; c += 64) {
+    float g = dqr[c];
     if (wadj) {
-      const float* wr = wadj + (long long)o * (D + W);
-      float a0 = 0.f, a1 = 0.f;
-      int c = 0;
-      for (; c + 1 < D; c += 2) {
-        a0 = fmaf(wr[c], smean[c], a0);
-        a1 = fmaf(wr[c + 1], smean[c + 1], a1);
-      }
-      for (; c < D; ++c) a0 = fmaf(wr[c], smean[c], a0);
-      for (c = 0; c < W; ++c) a1 = fmaf(wr[D + c], se[k * W + c], a1);
-      v += a0 + a1;
+      float g1 = 0.f;
+#pragma unroll 5
+      for (int o = 0; o < W; ++o) g1 = fmaf(wadj[(long long)o * (D + W) + D + c], dqr[o], g1);
+      g += g1;
     }
-    q[((long long)b * K + k) * W + o] = v;
+    if (id >= 0) atomicAdd(demb + (long long)id * W + c, g);
   }
 }
 
-// dEmb[idx] += dq + W_e^T dq ; dmean[b] = sum_k W_m^T dq[b,k] / T (broadcast grad into h)
-__global__ __launch_bounds__(256) void query_bwd_rows_kernel(const float* __restrict__ dq, const int* __restrict__ idx,
-                                                             const float* __restrict__ wadj, int T, int D, int K,
-                                                             int W, float* __restrict__ demb,
-                                                             float* __restrict__ dh_bcast) {
-  const int b = blockIdx.x;
-  extern __shared__ float sdq[];  // [K][W]
-  for (int i = threadIdx.x; i < K * W; i += blockDim.x) sdq[i] = dq[(long long)b * K * W + i];
+__global__ __launch_bounds__(64) void query_bwd_w_kernel(const float* __restrict__ dq, const int* __restrict__ idx,
+                                                         const float* __restrict__ emb,
+                                                         const float* __restrict__ mean, int B, int D, int K, int W,
+                                                         float* __restrict__ dwadj) {
+  // block (column chunk, o): the o-th dq column (and its per-utterance sums u) and the
+  // speaker ids staged in LDS, then 8 independent loads in flight per thread
+  extern __shared__ float sm[];
+  float* sdq = sm;            // [B*K]  dq[bk][o]
+  float* su = sdq + B * K;    // [B]    u[b][o]
+  int* sid = reinterpret_cast<int*>(su + B);  // [B*K]
+  const int o = blockIdx.y, c = blockIdx.x * 64 + threadIdx.x;
+  for (int i = threadIdx.x; i < B * K; i += 64) {
+    sdq[i] = dq[(long long)i * W + o];
+    sid[i] = idx[i];
+  }
   __syncthreads();
-  if (demb) {
-    for (int i = threadIdx.x; i < K * W; i += blockDim.x) {
-      const int k = i / W, c = i % W;
-      float g = sdq[i];
-      if (wadj)
-        for (int o = 0; o < W; ++o) g = fmaf(wadj[(long long)o * (D + W) + D + c], sdq[k * W + o], g);
-      atomicAdd(demb + (long long)idx[b * K + k] * W + c, g);
-    }
+  for (int b = threadIdx.x; b < B; b += 64) {
+    float u = 0.f;
+    for (int k = 0; k < K; ++k) u += sdq[b * K + k];
+    su[b] = u;
   }
-  if (wadj && dh_bcast) {
-    for (int c = threadIdx.x; c < D; c += blockDim.x) {
-      float g = 0.f;
-      for (int k = 0; k < K; ++k)
-        for (int o = 0; o < W; ++o) g = fmaf(wadj[(long long)o * (D + W) + c], sdq[k * W + o], g);
-      dh_bcast[(long long)b * D + c] = g / (float)T;
+  __syncthreads();
+  if (c >= D + W) return;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < D) {
+    for (int b0 = 0; b0 < B; b0 += 8) {
+      float m[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = b0 + j < B ? mean[(long long)(b0 + j) * D + c] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (b0 + j < B) acc[j] = fmaf(su[b0 + j], m[j], acc[j]);
     }
-  }
-}
-
-// dW_adj[o][i] += sum_{b,k} dq[b,k,o] cat[b,k,i], cat = [mean_b ; Emb[idx[b,k]]]  (fixed order)
-__global__ __launch_bounds__(256) void query_bwd_w_kernel(const float* __restrict__ dq, const int* __restrict__ idx,
-                                                          const float* __restrict__ emb,
-                                                          const float* __restrict__ mean, int B, int D, int K, int W,
-                                                          float* __restrict__ dwadj) {
-  const long long n = (long long)W * (D + W);
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int o = (int)(e / (D + W)), i = (int)(e % (D + W));
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b)
-      for (int k = 0; k < K; ++k) {
-        const float c = i < D ? mean[(long long)b * D + i] : emb[(long long)idx[b * K + k] * W + (i - D)];
-        acc = fmaf(dq[((long long)b * K + k) * W + o], c, acc);
+  } else {
+    const int ce = c - D;
+    for (int b0 = 0; b0 < B * K; b0 += 8) {
+      float e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int id = b0 + j < B * K ? sid[b0 + j] : -1;
+        e[j] = id >= 0 ? emb[(long long)id * W + ce] : 0.f;
       }
-    dwadj[e] += acc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (b0 + j < B * K) acc[j] = fmaf(sdq[b0 + j], e[j], acc[j]);
+    }
   }
+  dwadj[(long long)o * (D + W) + c] += ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 }
 
 // out[n] (+)= sum_m A[m*lda + n]   (bias gradients); block = 64 columns x 4 row lanes
@@ -179,8 +230,8 @@ DL4SS_API int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* id
     hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(256), 0, st, h, T, D, mean_out);
     DL4SS_CHECK_LAUNCH();
   }
-  const size_t smem = sizeof(float) * (D + K * W);
-  hipLaunchKernelGGL(query_fwd_kernel, dim3(B), dim3(256), smem, st, mean_out, D, idx, emb, w_adj, K, W, q);
+  hipLaunchKernelGGL(query_fwd_kernel, dim3(W, B, cdiv(K, 4)), dim3(64), 0, st, mean_out, D, idx, emb, w_adj, K, W,
+                     q);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
@@ -198,14 +249,19 @@ DL4SS_API int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* i
                               float* dh_bcast, void* stream) {
   DL4SS_REQUIRE(dq && idx && B > 0 && K > 0 && W > 0);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(query_bwd_rows_kernel, dim3(B), dim3(256), sizeof(float) * K * W, st, dq, idx, w_adj, T, D, K,
-                     W, d_emb, dh_bcast);
-  DL4SS_CHECK_LAUNCH();
+  if (d_emb) {
+    hipLaunchKernelGGL(query_bwd_emb_kernel, dim3(B * K), dim3(64), 0, st, dq, idx, w_adj, D, W, d_emb);
+    DL4SS_CHECK_LAUNCH();
+  }
+  if (w_adj && dh_bcast) {
+    hipLaunchKernelGGL(query_bwd_dh_kernel, dim3(cdiv(D, 64), B), dim3(64), 0, st, dq, w_adj, T, D, K, W, dh_bcast);
+    DL4SS_CHECK_LAUNCH();
+  }
   if (w_adj && d_wadj) {
     DL4SS_REQUIRE(mean && emb);
-    const long long n = (long long)W * (D + W);
-    hipLaunchKernelGGL(query_bwd_w_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, dq, idx, emb, mean, B, D, K, W,
-                       d_wadj);
+    const size_t smem = sizeof(float) * (2 * (size_t)B * K + B);
+    hipLaunchKernelGGL(query_bwd_w_kernel, dim3(cdiv(D + W, 64), W), dim3(64), smem, st, dq, idx, emb, mean, B, D, K,
+                       W, d_wadj);
     DL4SS_CHECK_LAUNCH();
   }
   return 0;

@@ -15,6 +15,7 @@ flat fp32 buffer (views carry the reference ``state_dict`` key names, so a
 reference / oracle state dict loads directly) and all gradients in a second
 flat buffer: one all-reduce and one Adam launch per step.
 """
+import ctypes
 import math
 import os
 
@@ -23,6 +24,7 @@ import torch
 from . import _lib, ops
 
 CELLS = {"lstm": 0, "gru": 1}
+WS_ZEROED = 0x100  # DL4SS_RNN_WS_ZEROED (include/dl4ss_hip.h)
 
 
 def _ngate(cell):
@@ -127,7 +129,7 @@ class SepTrainer:
         f32 = dict(device=dev, dtype=torch.float32)
         self.src = torch.empty(B, K, N, **f32)
         self.mix = torch.empty(B, N, **f32)
-        self.stats = torch.empty(2 * B * K, **f32)
+        self.stats = torch.empty(32 * B * K, **f32)  # mixing partials (dl4ss_mix_sources)
         self.mag_mix = torch.empty(B, T, F, **f32)
         if mode == "crm":
             self.Xc_mix = torch.empty(B, T, F, 2, **f32)
@@ -158,6 +160,11 @@ class SepTrainer:
             raise RuntimeError("unsupported BiRNN configuration")
         self.ws_bytes = ws
         self.rnn_ws = torch.empty((ws + 7) // 8, device=dev, dtype=torch.int64)
+        # bf16 fast path: one workspace per (layer, pass), zeroed by one fill per pass
+        # (DL4SS_RNN_WS_ZEROED) instead of a memset in front of every recurrence launch
+        w8 = (ws + 255) // 256 * 32
+        self.rnn_ws_all = torch.empty(2, net.L * w8, device=dev, dtype=torch.int64)  # [fwd | bwd][layer]
+        self._ws_slot = lambda l, bwd: self.rnn_ws_all[int(bwd), l * w8:(l + 1) * w8]
         self.status = torch.zeros(1, device=dev, dtype=torch.int32)
         self.m = torch.zeros_like(net.flat)
         self.v = torch.zeros_like(net.flat)
@@ -208,24 +215,41 @@ class SepTrainer:
         _lib.call("dl4ss_f32_to_bf16_2d", _lib.ptr(x, True), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(out),
                   out.stride(0), _lib.stream_ptr())
 
+    def _weights_to_bf16(self):
+        """The bf16 copies of every layer's W_ih and the Linear weight, one launch
+        (dl4ss_f32_to_bf16_2d_multi)."""
+        net = self.net
+        pairs = [(net.cat_view("weight_ih", l), self.wb_ih[l]) for l in range(net.L)]
+        pairs.append((net.view("mix.Linear.weight"), self.wb_lin))
+        if not hasattr(self, "_cvt_args"):
+            n = len(pairs)
+            P = ctypes.c_void_p
+            self._cvt_args = (n, (P * n)(*[x.data_ptr() for x, _ in pairs]),
+                              (ctypes.c_longlong * n)(*[x.stride(0) for x, _ in pairs]),
+                              (ctypes.c_int * n)(*[x.shape[0] for x, _ in pairs]),
+                              (ctypes.c_int * n)(*[x.shape[1] for x, _ in pairs]),
+                              (P * n)(*[y.data_ptr() for _, y in pairs]),
+                              (ctypes.c_longlong * n)(*[y.stride(0) for _, y in pairs]))
+        _lib.call("dl4ss_f32_to_bf16_2d_multi", *self._cvt_args, _lib.stream_ptr())
+
     def _forward_fast(self, x):
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         st = _lib.stream_ptr()
         cell = CELLS[net.cell]
-        for l in range(net.L):
-            self._to_bf16_rows(net.cat_view("weight_ih", l), self.wb_ih[l])
-        self._to_bf16_rows(net.view("mix.Linear.weight"), self.wb_lin)
+        self.rnn_ws_all[0].zero_()  # every layer's forward hand-off workspace, one fill
+        self._weights_to_bf16()
         self._to_bf16_rows(x, self.xb0)
         xb = self.xb0[:, :x.shape[1]]
         for l in range(net.L):
             D = xb.shape[1]
             ops.gemm_bf16(xb, self.wb_ih[l][:, :D], transB=True, bias=net.cat_view("bias_ih", l), out=self.G)
             hp = self.hprev[l]
-            _lib.call("dl4ss_birnn_fwd_ex", cell, 1, B, T, H, _lib.ptr(self.G), _lib.ptr(net.cat_view("weight_hh", l)),
-                      _lib.ptr(net.cat_view("bias_hh", l)), _lib.ptr(self.out[l]), _lib.ptr(hp), _lib.ptr(self.act[l]),
+            _lib.call("dl4ss_birnn_fwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(self.G),
+                      _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
+                      _lib.ptr(self.out[l]), _lib.ptr(hp), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.outb[l]), _lib.ptr(self.hprevb[l]),
-                      _lib.ptr(self.rnn_ws), self.ws_bytes, _lib.ptr(self.status), st)
+                      _lib.ptr(self._ws_slot(l, False)), self.ws_bytes, _lib.ptr(self.status), st)
             xb = self.outb[l][:, :2 * H]
         ops.gemm_bf16(xb, self.wb_lin[:, :2 * H], transB=True, bias=net.view("mix.Linear.bias"),
                       epilogue=ops.EPI_TANH, out=self.V)
@@ -302,6 +326,7 @@ class SepTrainer:
         dPreb = self.dPreb[:, :FE]
         hLb = self.outb[-1][:, :2 * H]
         lt = self.use_lt  # plain (epilogue-free) GEMMs through hipBLASLt, else the hand-written kernel
+        self.rnn_ws_all[1].zero_()  # every layer's BPTT hand-off workspace, one fill
         if lt:
             ops.gemm_bf16_lt(dPreb, hLb, net.view("mix.Linear.weight", g), transA=True, beta=1.0)
         else:
@@ -315,12 +340,12 @@ class SepTrainer:
             ops.gemm_bf16(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk="auto")
         hp8 = self.p8(H)
         for l in range(net.L - 1, -1, -1):
-            _lib.call("dl4ss_birnn_bwd_ex", cell, 1, B, T, H, _lib.ptr(dH),
+            _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(dH),
                       _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), None, None,
                       _lib.ptr(self.dGb), _lib.ptr(self.dGhb), _lib.ptr(net.cat_view("bias_ih", l, g)),
-                      _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self.rnn_ws), self.ws_bytes,
+                      _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self._ws_slot(l, True)), self.ws_bytes,
                       _lib.ptr(self.status), st)
             xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
             dGhb = self.dGhb if self.dGhb is not None else self.dGb

@@ -75,7 +75,7 @@ def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=N
     if out_mix is None:
         out_mix = torch.empty(B, N, device=raw.device, dtype=torch.float32)
     if stats_ws is None:
-        stats_ws = torch.empty(B * K * 2, device=raw.device, dtype=torch.float32)
+        stats_ws = torch.empty(B * K * 32, device=raw.device, dtype=torch.float32)
     if lengths is not None and (lengths.dtype != torch.int32 or tuple(lengths.shape) != (B, K)):
         raise RuntimeError("mix_sources: lengths must be (B, K) int32")
     _lib.call("dl4ss_mix_sources_ex", _lib.ptr(raw), _lib.ptr(lengths), _lib.ptr(gains), B, K, N, _lib.ptr(stats_ws),

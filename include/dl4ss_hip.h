@@ -54,7 +54,7 @@ int dl4ss_istft_apply(const float* X_mix_c64, const float* aux, long long n_sig,
 
 /* ---- R1 preprocessing / mixing ----------------------------------------- */
 /* raw (B, K, N) -> out_src (B, K, N): each source x -> (x - mean) / max|x - mean| * gain;
- * out_mix (B, N): their sum.  stats_ws: 2*B*K floats of workspace.
+ * out_mix (B, N): their sum.  stats_ws: 32*B*K floats of workspace (16-B aligned; K <= 16).
  * Replaces Torch_multi/predata_multiAims_dB.py:156-197 (and the _3dB /
  * fromList_cRM_123 gain variants: gains are computed by the caller). */
 int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws, float* out_src,
@@ -105,10 +105,18 @@ int dl4ss_gemm_bf16_set_tile(int tile);
 int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, void* stream);
 /* out[n] += sum_m A[m*lda + n] for a bf16 matrix A (bias gradient from bf16 dPre). */
 int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, void* stream);
+/* n (<= 8) dl4ss_f32_to_bf16_2d conversions in one launch (host arrays of per-segment
+ * arguments): the step's bf16 weight copies (W_ih of every layer, the Linear). */
+int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ldx, const int* rows, const int* cols,
+                               void* const* y, const long long* ldy, void* stream);
 
 /* ---- persistent bidirectional LSTM / GRU recurrence ---------------------- */
 enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
-/* Granule workspace (bytes) needed by dl4ss_birnn_fwd / _bwd for (cell, B, H); -1 if unsupported. */
+/* Granule workspace (bytes) needed by dl4ss_birnn_fwd / _bwd for (cell, B, H); -1 if unsupported.
+ * The launchers zero the workspace themselves (hipMemsetAsync) unless `precision` carries
+ * DL4SS_RNN_WS_ZEROED: the caller then guarantees it is zero (e.g. one fill per training
+ * step over separate workspaces for every layer and pass). */
+#define DL4SS_RNN_WS_ZEROED 0x100
 long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
 /* One layer, both directions: G (B,T,2,NG*H) = X W_ih^T + b_ih (NG = 4 LSTM / 3 GRU),
  * W_hh (2, NG*H, H), b_hh (2, NG*H) -> out (B,T,2H) [fwd | reverse], hprev (B,T,2H)
