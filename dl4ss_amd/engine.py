@@ -180,6 +180,12 @@ class SepTrainer:
         self.fast = precision == "bf16" and self.rnn_precision == "bf16"
         # bf16 mode: the plain backward GEMMs through hipBLASLt (DL4SS_GEMM_LT=0: the hand-written kernel)
         self.use_lt = self.fast and os.environ.get("DL4SS_GEMM_LT", "1") != "0"
+        # DL4SS_OVERLAP=1: weight-gradient GEMMs of layer l on a side stream, concurrent with the
+        # BPTT of layer l-1.  Off by default: measured 6.89 vs 6.41 ms per step -- the GEMM
+        # workgroups share CUs with the persistent recurrence and slow every hand-off more
+        # than the hidden GEMM time saves.
+        self.overlap = self.use_lt and os.environ.get("DL4SS_OVERLAP", "0") == "1"
+        self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
             p8 = lambda n: (n + 7) // 8 * 8
@@ -188,8 +194,12 @@ class SepTrainer:
             self.xb0 = torch.empty(BT, p8(D0), **bf)
             self.outb = [torch.empty(BT, p8(2 * H), **bf) for _ in range(net.L)]
             self.hprevb = [torch.empty(BT, 2 * p8(H), **bf) for _ in range(net.L)]
-            self.dGb = torch.empty(BT, 2 * NGH, **bf)
-            self.dGhb = torch.empty(BT, 2 * NGH, **bf) if net.cell == "gru" else None
+            # two of each: with the weight-gradient GEMMs of layer l on the side stream, BPTT of
+            # layer l-1 writes the other buffer
+            self.dGb2 = [torch.empty(BT, 2 * NGH, **bf) for _ in range(2)]
+            self.dGhb2 = [torch.empty(BT, 2 * NGH, **bf) for _ in range(2)] if net.cell == "gru" else None
+            self.dGb = self.dGb2[0]
+            self.dGhb = self.dGhb2[0] if self.dGhb2 else None
             self.dPreb = torch.empty(BT, p8(F * net.E), **bf)
             self.wb_ih = [torch.empty(2 * NGH, p8(F if l == 0 else 2 * H), **bf) for l in range(net.L)]
             self.wb_lin = torch.empty(F * net.E, p8(2 * H), **bf)
@@ -321,52 +331,80 @@ class SepTrainer:
         NGH = _ngate(net.cell) * H
         FE = self.F * net.E
         g = net.grad
-        st = _lib.stream_ptr()
         cell = CELLS[net.cell]
         dPreb = self.dPreb[:, :FE]
         hLb = self.outb[-1][:, :2 * H]
         lt = self.use_lt  # plain (epilogue-free) GEMMs through hipBLASLt, else the hand-written kernel
+        main = torch.cuda.current_stream()
+        ov = self.overlap
+        st = _lib.stream_ptr(main)
         self.rnn_ws_all[1].zero_()  # every layer's BPTT hand-off workspace, one fill
-        if lt:
-            ops.gemm_bf16_lt(dPreb, hLb, net.view("mix.Linear.weight", g), transA=True, beta=1.0)
-        else:
-            ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
-        _lib.call("dl4ss_colsum_bf16", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
-                  _lib.ptr(net.view("mix.Linear.bias", g)), st)
+
+        def on_side(fn):
+            """run fn on the side stream once everything queued on the main stream so far is done"""
+            if not ov:
+                fn()
+                return
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                fn()
+
         dH = self.dH[0]
         if lt:
-            ops.gemm_bf16_lt(dPreb, self.wb_lin[:, :2 * H], dH)
+            ops.gemm_bf16_lt(dPreb, self.wb_lin[:, :2 * H], dH)  # the input gradient first: BPTT waits on it
         else:
             ops.gemm_bf16(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk="auto")
+
+        def linear_grads():
+            if lt:
+                ops.gemm_bf16_lt(dPreb, hLb, net.view("mix.Linear.weight", g), transA=True, beta=1.0)
+            else:
+                ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
+            _lib.call("dl4ss_colsum_bf16", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+                      _lib.ptr(net.view("mix.Linear.bias", g)), _lib.stream_ptr())
+
+        on_side(linear_grads)
         hp8 = self.p8(H)
+        done = {}  # layer -> event after its weight-gradient GEMMs on the side stream
         for l in range(net.L - 1, -1, -1):
+            dGb = self.dGb2[l % 2]
+            dGhb = self.dGhb2[l % 2] if self.dGhb2 else dGb
+            if l + 2 in done:  # dGb2[l % 2] was layer l+2's: its weight gradients must have read it
+                main.wait_event(done[l + 2])
             _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(dH),
                       _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), None, None,
-                      _lib.ptr(self.dGb), _lib.ptr(self.dGhb), _lib.ptr(net.cat_view("bias_ih", l, g)),
+                      _lib.ptr(dGb), _lib.ptr(dGhb) if self.dGhb2 else None, _lib.ptr(net.cat_view("bias_ih", l, g)),
                       _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self._ws_slot(l, True)), self.ws_bytes,
                       _lib.ptr(self.status), st)
-            xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
-            dGhb = self.dGhb if self.dGhb is not None else self.dGb
-            whh_g = net.cat_view("weight_hh", l, g)
             if l > 0:  # the input gradient first: it is all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
                 if lt:
-                    ops.gemm_bf16_lt(self.dGb, self.wb_ih[l][:, :2 * H], dH_next)
+                    ops.gemm_bf16_lt(dGb, self.wb_ih[l][:, :2 * H], dH_next)
                 else:
-                    ops.gemm_bf16(self.dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")
-            # both directions' dW_hh in one launch: member d = columns d*NGH of dGh, d*pad8(H) of h_{t-1}
-            if lt:
-                ops.gemm_bf16_lt(self.dGb, xb, net.cat_view("weight_ih", l, g), transA=True, beta=1.0)
-                ops.gemm_bf16_lt(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], transA=True, beta=1.0, batch=2,
-                                 strideA=NGH, strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT)
-            else:
-                ops.gemm_bf16(self.dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0)
-                ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
-                                      NGH, H, BT, transA=True, beta=1.0, splitk="auto")
+                    ops.gemm_bf16(dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")
+            xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
+
+            def weight_grads(l=l, dGb=dGb, dGhb=dGhb, xb=xb):
+                whh_g = net.cat_view("weight_hh", l, g)
+                # both directions' dW_hh in one launch: member d = columns d*NGH of dGh, d*pad8(H) of h_{t-1}
+                if lt:
+                    ops.gemm_bf16_lt(dGb, xb, net.cat_view("weight_ih", l, g), transA=True, beta=1.0)
+                    ops.gemm_bf16_lt(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], transA=True, beta=1.0,
+                                     batch=2, strideA=NGH, strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT)
+                else:
+                    ops.gemm_bf16(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0)
+                    ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
+                                          NGH, H, BT, transA=True, beta=1.0, splitk="auto")
+
+            on_side(weight_grads)
+            if ov:
+                done[l] = self.side.record_event()
             if l > 0:
                 dH = dH_next
+        if ov:
+            main.wait_stream(self.side)  # every gradient is in place before the all-reduce / Adam
 
     def backward(self):
         net, B, T, H = self.net, self.B, self.T, self.net.H

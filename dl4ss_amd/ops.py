@@ -203,10 +203,10 @@ def gemm_bf16_lt(A, B, out, transA=False, transB=False, beta=0.0, batch=1, strid
     if M is None:
         M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
         N = B.shape[0] if transB else B.shape[1]
-    dev = A.device
-    ws = _lt_ws.get(dev)
+    key = (A.device, torch.cuda.current_stream().cuda_stream)  # one workspace per stream (concurrent GEMMs)
+    ws = _lt_ws.get(key)
     if ws is None:
-        ws = _lt_ws[dev] = torch.empty(LT_WS_BYTES, dtype=torch.uint8, device=dev)
+        ws = _lt_ws[key] = torch.empty(LT_WS_BYTES, dtype=torch.uint8, device=A.device)
     _lib.call("dl4ss_gemm_bf16_lt", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
               _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), float(beta), int(batch),
               int(strideA), int(strideB), int(strideC), _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
