@@ -57,6 +57,7 @@ SIGNATURES = {
     "dl4ss_mix_sources_ex": [P, P, P, I, I, I, P, P, P, P],
     "dl4ss_gemm_bf16_set_tile": [I],
     "dl4ss_f32_to_bf16_2d_multi": [I, P, P, P, P, P, P, P],
+    "dl4ss_mask_attn_loss_bf16v": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
     "dl4ss_gemm_bf16_lt": [I, I, I, I, I, P, LL, P, LL, P, LL, F, I, LL, LL, LL, P, LL, P],
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
 }

@@ -43,6 +43,7 @@ struct Perms<3> {
 struct AttnArgs {
   int B, T, F, rows_per_b, nblk;  // rows_per_b = T*F ; nblk = blocks per utterance
   const float* V;                 // (B, T*F, E)
+  const unsigned short* Vb;       // the same as bf16 (the fast path's Linear writes V in bf16); V unused then
   const float* q;                 // (B, K, QW)
   const float* X;                 // mag: (b*xs + row) ; cRM: (b*xs + row)*2
   long long xs;
@@ -59,7 +60,7 @@ struct AttnArgs {
   float* pred_out;                // optional (B, K, T*F) [cRM: x2]
 };
 
-template <int E, int K, bool CRM, bool GRAD>
+template <int E, int K, bool CRM, bool GRAD, bool VB>
 __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
   constexpr int QW = CRM ? 2 * E : E;
   constexpr int NC = CRM ? 2 : 1;  // components per bin
@@ -91,8 +92,16 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
   for (int r0 = rbeg; r0 < rend; r0 += TILE) {
     const int nr = min(TILE, rend - r0);
     __syncthreads();  // previous tile fully consumed (and sq visible on first pass)
-    // coalesced stage of nr rows (nr*E floats, 16-B aligned when r0*E*4 % 16 == 0)
-    {
+    // coalesced stage of nr rows (nr*E floats, 16-B aligned when r0*E*4 % 16 == 0); bf16 V:
+    // 4-B pairs (E even), widened to fp32 in LDS
+    if constexpr (VB) {
+      const unsigned* src = reinterpret_cast<const unsigned*>(a.Vb + ((long long)b * a.rows_per_b + r0) * E);
+      const int n2 = nr * E / 2;
+      for (int i = tid; i < n2; i += NT) {
+        const unsigned w = src[i];
+        reinterpret_cast<float2*>(sv)[i] = make_float2(__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u));
+      }
+    } else {
       const float* src = Vb + (long long)r0 * E;
       const int n = nr * E;
       if ((((long long)r0 * E) & 3) == 0) {
@@ -378,30 +387,36 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
   }
 }
 
-template <int E, int K, bool CRM>
+template <int E, int K, bool CRM, bool VB>
 int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
   dim3 grid(a.nblk, a.B);
   if (grad)
-    hipLaunchKernelGGL((attn_kernel<E, K, CRM, true>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((attn_kernel<E, K, CRM, true, VB>), grid, dim3(NT), 0, st, a);
   else
-    hipLaunchKernelGGL((attn_kernel<E, K, CRM, false>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((attn_kernel<E, K, CRM, false, VB>), grid, dim3(NT), 0, st, a);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
 
-int dispatch(int E, int K, int crm, bool grad, const AttnArgs& a, hipStream_t st) {
+template <bool VB>
+int dispatch_v(int E, int K, int crm, bool grad, const AttnArgs& a, hipStream_t st) {
   if (E != 50) return (int)hipErrorInvalidValue;
   if (!crm) {
-    if (K == 1) return launch_attn<50, 1, false>(grad, a, st);
-    if (K == 2) return launch_attn<50, 2, false>(grad, a, st);
-    if (K == 3) return launch_attn<50, 3, false>(grad, a, st);
+    if (K == 1) return launch_attn<50, 1, false, VB>(grad, a, st);
+    if (K == 2) return launch_attn<50, 2, false, VB>(grad, a, st);
+    if (K == 3) return launch_attn<50, 3, false, VB>(grad, a, st);
   } else {
-    if (K == 1) return launch_attn<50, 1, true>(grad, a, st);
-    if (K == 2) return launch_attn<50, 2, true>(grad, a, st);
-    if (K == 3) return launch_attn<50, 3, true>(grad, a, st);
+    if (K == 1) return launch_attn<50, 1, true, VB>(grad, a, st);
+    if (K == 2) return launch_attn<50, 2, true, VB>(grad, a, st);
+    if (K == 3) return launch_attn<50, 3, true, VB>(grad, a, st);
   }
   return (int)hipErrorInvalidValue;
 }
+
+int attn_common(int pass, int crm, int B, int K, int T, int F, int E, const float* V, const void* Vb, const float* q,
+                const float* X, long long x_bstride, const float* Y, long long y_bstride, long long y_kstride,
+                const int* perm, float s1, float s2, float* dPre, void* dPre_bf16, long long dpre_bf16_ld,
+                float* part_loss, float* part_dq, float* mask_out, float* pred_out, void* stream);
 
 }  // namespace
 
@@ -434,18 +449,42 @@ DL4SS_API int dl4ss_mask_attn_loss_ex(int pass, int crm, int B, int K, int T, in
                                       long long y_bstride, long long y_kstride, const int* perm, float s1, float s2,
                                       float* dPre, void* dPre_bf16, long long dpre_bf16_ld, float* part_loss,
                                       float* part_dq, float* mask_out, float* pred_out, void* stream) {
-  DL4SS_REQUIRE(B > 0 && K >= 1 && K <= 3 && T > 0 && F > 0 && V && q && X && Y && part_loss);
+  DL4SS_REQUIRE(V);
+  return attn_common(pass, crm, B, K, T, F, E, V, nullptr, q, X, x_bstride, Y, y_bstride, y_kstride, perm, s1, s2,
+                     dPre, dPre_bf16, dpre_bf16_ld, part_loss, part_dq, mask_out, pred_out, stream);
+}
+
+DL4SS_API int dl4ss_mask_attn_loss_bf16v(int pass, int crm, int B, int K, int T, int F, int E, const void* V_bf16,
+                                         const float* q, const float* X, long long x_bstride, const float* Y,
+                                         long long y_bstride, long long y_kstride, const int* perm, float s1,
+                                         float s2, float* dPre, void* dPre_bf16, long long dpre_bf16_ld,
+                                         float* part_loss, float* part_dq, float* mask_out, float* pred_out,
+                                         void* stream) {
+  DL4SS_REQUIRE(V_bf16 && ((uintptr_t)V_bf16 & 3) == 0 && E % 2 == 0);
+  return attn_common(pass, crm, B, K, T, F, E, nullptr, V_bf16, q, X, x_bstride, Y, y_bstride, y_kstride, perm, s1,
+                     s2, dPre, dPre_bf16, dpre_bf16_ld, part_loss, part_dq, mask_out, pred_out, stream);
+}
+
+namespace {
+int attn_common(int pass, int crm, int B, int K, int T, int F, int E, const float* V, const void* Vb, const float* q,
+                const float* X, long long x_bstride, const float* Y, long long y_bstride, long long y_kstride,
+                const int* perm, float s1, float s2, float* dPre, void* dPre_bf16, long long dpre_bf16_ld,
+                float* part_loss, float* part_dq, float* mask_out, float* pred_out, void* stream) {
+  DL4SS_REQUIRE(B > 0 && K >= 1 && K <= 3 && T > 0 && F > 0 && q && X && Y && part_loss);
   DL4SS_REQUIRE(pass == 0 || ((dPre || dPre_bf16) && part_dq));
   DL4SS_REQUIRE(!dPre_bf16 || (E % 2 == 0 && dpre_bf16_ld % 2 == 0 && dpre_bf16_ld >= (long long)F * E &&
                                ((uintptr_t)dPre_bf16 & 3) == 0));
   AttnArgs a{};
   a.B = B; a.T = T; a.F = F; a.rows_per_b = T * F; a.nblk = dl4ss_attn_nblk(T, F);
-  a.V = V; a.q = q; a.X = X; a.xs = x_bstride; a.Y = Y; a.ys = y_bstride; a.yks = y_kstride;
+  a.V = V; a.Vb = reinterpret_cast<const unsigned short*>(Vb);
+  a.q = q; a.X = X; a.xs = x_bstride; a.Y = Y; a.ys = y_bstride; a.yks = y_kstride;
   a.perm = perm; a.s1 = s1; a.s2 = s2; a.dPre = dPre; a.part_loss = part_loss; a.part_dq = part_dq;
   a.dPreB = reinterpret_cast<unsigned*>(dPre_bf16); a.ldpb = dpre_bf16_ld;
   a.mask_out = mask_out; a.pred_out = pred_out;
-  return dispatch(E, K, crm, pass == 1, a, as_stream(stream));
+  return Vb ? dispatch_v<true>(E, K, crm, pass == 1, a, as_stream(stream))
+            : dispatch_v<false>(E, K, crm, pass == 1, a, as_stream(stream));
 }
+}  // namespace
 
 DL4SS_API int dl4ss_pit_select(const float* part_loss, int B, int K, int nblk, int* perm, void* stream) {
   DL4SS_REQUIRE(part_loss && perm && B > 0 && K >= 1 && K <= 3);

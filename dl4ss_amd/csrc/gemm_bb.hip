@@ -27,7 +27,7 @@ namespace {
 constexpr int BK = 64, LDK = BK + 8;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
-enum { EPI_NONE = 0, EPI_TANH = 1 };
+enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2 };  // 2: tanh, C written as bf16 (raw 16-bit words)
 
 // tanh for the Linear epilogue: 1 - 2 / (1 + e^{2x}) with v_exp + v_rcp (~1e-6 relative;
 // saturates cleanly: e^{2x} -> inf gives 1, -> 0 gives -1)
@@ -301,6 +301,23 @@ __global__ __launch_bounds__(TC::NT, TC::NT == 256 ? 2 : 1) void gemm_bb_kernel(
         if (row >= M) continue;
         float4 x = *reinterpret_cast<const float4*>(stage + rl * SLD + c4);
         x.x += bv.x; x.y += bv.y; x.z += bv.z; x.w += bv.w;
+        if constexpr (EPI == EPI_TANH_BF16) {  // V of the Linear, written directly as bf16 pairs (ldc even)
+          unsigned short* cb = reinterpret_cast<unsigned short*>(C) + (long long)row * ldc + col;
+          const float xs[4] = {ftanh_fast(x.x), ftanh_fast(x.y), ftanh_fast(x.z), ftanh_fast(x.w)};
+          unsigned short hb[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const unsigned u = __float_as_uint(xs[c]);
+            hb[c] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+          }
+          if (col + 4 <= N) {
+            *reinterpret_cast<unsigned*>(cb) = hb[0] | ((unsigned)hb[1] << 16);
+            *reinterpret_cast<unsigned*>(cb + 2) = hb[2] | ((unsigned)hb[3] << 16);
+          } else {
+            for (int c = 0; c < 4 && col + c < N; ++c) cb[c] = hb[c];
+          }
+          continue;
+        }
         float* cp = C + (long long)row * ldc + col;
         if (vec_c) {
           if (beta != 0.0f) {
@@ -344,7 +361,9 @@ void launch_tile(bool vec, int splitk, int epi, dim3 grid, int M, int N, int K, 
   if (vec) {
     if (splitk > 1) GBB_LAUNCH(EPI_NONE, true, true);
     else if (epi == EPI_TANH) GBB_LAUNCH(EPI_TANH, false, true);
-    else GBB_LAUNCH(EPI_NONE, false, true);
+    else if (epi == EPI_TANH_BF16) {
+      if constexpr (TC::NT == 256) GBB_LAUNCH(EPI_TANH_BF16, false, true);
+    } else GBB_LAUNCH(EPI_NONE, false, true);
   } else if constexpr (TC::NT == 256) {  // unaligned operands: the 128 x 128 tile only
     if (splitk > 1) GBB_LAUNCH(EPI_NONE, true, false);
     else if (epi == EPI_TANH) GBB_LAUNCH(EPI_TANH, false, false);
@@ -363,6 +382,10 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
                    (batch == 1 || (sa % 8 == 0 && sb % 8 == 0));
   int tc = g_tile_override ? g_tile_override : gemm_tile_for(M, N, K, splitk, batch);
   if (!vec) tc = TILE_128x128;
+  if (epi == EPI_TANH_BF16) {  // bf16 output: 128 x 128 tile, aligned operands, even ldc, no accumulation
+    if (!vec || beta != 0.0f || (ldc & 1) || ((uintptr_t)C & 3)) return (int)hipErrorInvalidValue;
+    tc = TILE_128x128;
+  }
   const int BMt = tc == TILE_128x128 ? 128 : 256, BNt = tc == TILE_256x256 ? 256 : 128;
   const int gm = (M + BMt - 1) / BMt, gn = (N + BNt - 1) / BNt;
   int kps = (K + splitk - 1) / splitk;

@@ -201,6 +201,7 @@ class SepTrainer:
             self.dGb = self.dGb2[0]
             self.dGhb = self.dGhb2[0] if self.dGhb2 else None
             self.dPreb = torch.empty(BT, p8(F * net.E), **bf)
+            self.Vb = torch.empty(BT, F * net.E, **bf)  # V = tanh(Linear) in bf16 (even row length)
             self.wb_ih = [torch.empty(2 * NGH, p8(F if l == 0 else 2 * H), **bf) for l in range(net.L)]
             self.wb_lin = torch.empty(F * net.E, p8(2 * H), **bf)
             if net.cell == "lstm":  # the LSTM BPTT never reads the fp32 h_{t-1}
@@ -262,7 +263,7 @@ class SepTrainer:
                       _lib.ptr(self._ws_slot(l, False)), self.ws_bytes, _lib.ptr(self.status), st)
             xb = self.outb[l][:, :2 * H]
         ops.gemm_bf16(xb, self.wb_lin[:, :2 * H], transB=True, bias=net.view("mix.Linear.bias"),
-                      epilogue=ops.EPI_TANH, out=self.V)
+                      epilogue=ops.EPI_TANH_BF16, out=self.Vb)
 
     def forward(self, feats=None):
         net, B, T, H = self.net, self.B, self.T, self.net.H
@@ -305,8 +306,10 @@ class SepTrainer:
         grad = pass_ == 1
         dpre = _lib.ptr(self.V) if grad and not self.fast else None
         dpreb = _lib.ptr(self.dPreb) if grad and self.fast else None
-        _lib.call("dl4ss_mask_attn_loss_ex", pass_, int(self.mode == "crm"), self.B, self.K, self.T, self.F,
-                  self.net.E, _lib.ptr(self.V), _lib.ptr(self.q), _lib.ptr(X), xs, _lib.ptr(Y), ys, yks,
+        # bf16 path: V itself is bf16 (the Linear's EPI_TANH_BF16 epilogue)
+        fn, v = ("dl4ss_mask_attn_loss_bf16v", self.Vb) if self.fast else ("dl4ss_mask_attn_loss_ex", self.V)
+        _lib.call(fn, pass_, int(self.mode == "crm"), self.B, self.K, self.T, self.F,
+                  self.net.E, _lib.ptr(v), _lib.ptr(self.q), _lib.ptr(X), xs, _lib.ptr(Y), ys, yks,
                   _lib.ptr(perm), self.s1, self.s2, dpre, dpreb, self.dPreb.stride(0) if self.fast else 0,
                   _lib.ptr(self.part_loss), _lib.ptr(self.part_dq) if grad else None, _lib.ptr(mask_out),
                   _lib.ptr(pred_out), _lib.stream_ptr())

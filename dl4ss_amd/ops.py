@@ -87,7 +87,7 @@ def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=N
 # dense contractions
 # ---------------------------------------------------------------------------
 PREC = {"fp32": 0, "bf16": 1}
-EPI_NONE, EPI_TANH = 0, 1
+EPI_NONE, EPI_TANH, EPI_TANH_BF16 = 0, 1, 2  # 2: tanh written as bf16 (gemm_bf16 only)
 
 
 def _mat(t, name):
@@ -167,8 +167,14 @@ def gemm_bf16(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, be
     if out is None:
         if beta != 0.0 or splitk not in (1, "auto"):
             raise RuntimeError("gemm_bf16: accumulation needs an output tensor")
-        out = torch.empty(M, N, device=A.device, dtype=torch.float32)
-    _mat(out, "gemm_bf16(out)")
+        out = torch.empty(M, N, device=A.device,
+                          dtype=torch.bfloat16 if epilogue == EPI_TANH_BF16 else torch.float32)
+    if epilogue == EPI_TANH_BF16:
+        _mat_bf16(out, "gemm_bf16(out, bf16 epilogue)")
+        if beta != 0.0:
+            raise RuntimeError("gemm_bf16: the bf16-output epilogue does not accumulate")
+    else:
+        _mat(out, "gemm_bf16(out)")
     if tuple(out.shape) != (M, N):
         raise RuntimeError(f"gemm_bf16: out shape {tuple(out.shape)} != {(M, N)}")
     if bias is not None and (bias.numel() != N or not bias.is_contiguous()):

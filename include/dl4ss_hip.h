@@ -66,7 +66,7 @@ int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gain
                          float* stats_ws, float* out_src, float* out_mix, void* stream);
 
 /* ---- dense contractions (MFMA) ------------------------------------------ */
-enum { DL4SS_EPI_NONE = 0, DL4SS_EPI_TANH = 1 };
+enum { DL4SS_EPI_NONE = 0, DL4SS_EPI_TANH = 1, DL4SS_EPI_TANH_BF16 = 2 /* tanh, C written as bf16 */ };
 enum { DL4SS_PREC_F32 = 0, DL4SS_PREC_BF16 = 1 };
 /* C = op(A) op(B) (+ bias[N]) (tanh) (+ beta C); row-major, leading dims in elements.
  * transA: A stored K x M (else M x K); transB: B stored N x K (else K x N).
@@ -178,6 +178,14 @@ int dl4ss_mask_attn_loss_ex(int pass, int crm, int B, int K, int T, int F, int E
                             long long y_kstride, const int* perm, float s1, float s2, float* dPre, void* dPre_bf16,
                             long long dpre_bf16_ld, float* part_loss, float* part_dq, float* mask_out,
                             float* pred_out, void* stream);
+/* dl4ss_mask_attn_loss_ex with V in bf16 (V_bf16: (B, T*F, E) raw 16-bit words, 4-B aligned):
+ * the bf16 path's Linear writes V = tanh(h W^T + b) directly in bf16 (gemm EPI_TANH_BF16),
+ * halving the bytes of the Linear's output and of both attention passes' V reads. */
+int dl4ss_mask_attn_loss_bf16v(int pass, int crm, int B, int K, int T, int F, int E, const void* V_bf16, const float* q,
+                               const float* X, long long x_bstride, const float* Y, long long y_bstride,
+                               long long y_kstride, const int* perm, float s1, float s2, float* dPre, void* dPre_bf16,
+                               long long dpre_bf16_ld, float* part_loss, float* part_dq, float* mask_out,
+                               float* pred_out, void* stream);
 /* PIT: per utterance the lowest-index permutation minimising the summed costs. */
 int dl4ss_pit_select(const float* part_loss, int B, int K, int nblk, int* perm, void* stream);
 /* loss_out[3] = {total, MSE term, weighted sum-to-one term}; dq = sum of partials. */

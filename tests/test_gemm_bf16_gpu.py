@@ -128,3 +128,41 @@ def test_gemm_bf16_lt_batched(dev):
     for d in range(2):
         ref = ops.gemm_bf16(D[:, d * NGH:(d + 1) * NGH], Hb[:, d * hp8:d * hp8 + H], transA=True)
         assert ((out[d * NGH:(d + 1) * NGH] - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+def test_gemm_bf16_tanh_bf16_output(dev):
+    """EPI_TANH_BF16 (the Linear's V written as bf16): equals bf16(RNE) of the fp32 tanh epilogue."""
+    g = torch.Generator(device="cpu").manual_seed(21)
+    A = ops.to_bf16(torch.randn(700, 600, generator=g).to(dev) * 0.1)
+    Bw = ops.to_bf16(torch.randn(450, 600, generator=g).to(dev) * 0.1)
+    bias = torch.randn(450, generator=g).to(dev)
+    ref = ops.gemm_bf16(A, Bw, transB=True, bias=bias, epilogue=ops.EPI_TANH)
+    out = torch.empty(700, 450, device=dev, dtype=torch.bfloat16)
+    ops.gemm_bf16(A, Bw, transB=True, bias=bias, epilogue=ops.EPI_TANH_BF16, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref.to(torch.bfloat16))
+
+
+def test_attention_bf16v_matches_fp32_of_bf16(dev):
+    """dl4ss_mask_attn_loss_bf16v on bf16 V == dl4ss_mask_attn_loss_ex on the same values in fp32."""
+    from dl4ss_amd import _lib
+    g = torch.Generator(device="cpu").manual_seed(22)
+    B, K, T, F, E = 2, 2, 9, 129, 50
+    Vb = (torch.randn(B, T * F, E, generator=g) * 0.3).to(torch.bfloat16).to(dev)
+    V = Vb.float()
+    q = torch.randn(B, K, E, generator=g).to(dev)
+    X = torch.rand(B, T * F, generator=g).to(dev)
+    Y = torch.rand(B, K, T * F, generator=g).to(dev)
+    nblk = _lib.query("dl4ss_attn_nblk", T, F)
+    outs = []
+    for fn, v in (("dl4ss_mask_attn_loss_ex", V), ("dl4ss_mask_attn_loss_bf16v", Vb)):
+        part = torch.zeros(B, nblk, K * K + 1, device=dev)
+        pdq = torch.zeros(B, nblk, K, E, device=dev)
+        dpre = torch.zeros(B * T, F * E + 6, device=dev, dtype=torch.bfloat16)
+        _lib.call(fn, 1, 0, B, K, T, F, E, _lib.ptr(v), _lib.ptr(q), _lib.ptr(X), T * F, _lib.ptr(Y), K * T * F,
+                  T * F, None, 1e-3, 5e-4, None, _lib.ptr(dpre), dpre.stride(0), _lib.ptr(part), _lib.ptr(pdq), None,
+                  None, _lib.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append((part, pdq, dpre))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

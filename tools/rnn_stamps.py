@@ -57,7 +57,7 @@ def main():
         fw = stamps.view(240, 16).double().cpu() / T
         stamps.zero_()
         tr.dq.normal_()
-        tr.V.normal_()
+        (tr.Vb if getattr(tr, 'fast', False) else tr.V).normal_()
         tr.backward()
         torch.cuda.synchronize()
         bw = stamps.view(240, 16).double().cpu() / T
