@@ -439,24 +439,35 @@ constexpr int CVT_MAX = 8;
 struct CvtSegs {
   const float* x[CVT_MAX];
   unsigned short* y[CVT_MAX];
-  long long ldx[CVT_MAX], ldy[CVT_MAX], start[CVT_MAX + 1];  // element prefix over rows * ldy
+  long long ldx[CVT_MAX], ldy[CVT_MAX];
+  int row0[CVT_MAX + 1];  // row prefix over the segments
   int cols[CVT_MAX];
   int n;
 };
+// one workgroup per row (rows of every segment in sequence); each thread converts pairs of
+// columns and stores them as one 4-B word (ldy even)
 __global__ __launch_bounds__(256) void f32_to_bf16_multi_kernel(CvtSegs sg) {
-  const long long total = sg.start[sg.n];
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    int g = 0;
+  const int row = blockIdx.x;
+  int g = 0;
 #pragma unroll
-    for (int j = 1; j < CVT_MAX; ++j) g += (j < sg.n && i >= sg.start[j]) ? 1 : 0;
-    const long long e = i - sg.start[g];
-    const long long r = e / sg.ldy[g], c = e - r * sg.ldy[g];
-    unsigned short o = 0;
-    if (c < sg.cols[g]) {
-      const unsigned u = __float_as_uint(sg.x[g][r * sg.ldx[g] + c]);
-      o = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  for (int j = 1; j < CVT_MAX; ++j) g += (j < sg.n && row >= sg.row0[j]) ? 1 : 0;
+  const long long r = row - sg.row0[g];
+  const float* xr = sg.x[g] + r * sg.ldx[g];
+  unsigned* yr = reinterpret_cast<unsigned*>(sg.y[g] + r * sg.ldy[g]);
+  const int cols = sg.cols[g];
+  const int np = (int)(sg.ldy[g] >> 1);
+  for (int p = threadIdx.x; p < np; p += 256) {
+    const int c = 2 * p;
+    unsigned lo = 0, hi = 0;
+    if (c < cols) {
+      const unsigned u = __float_as_uint(xr[c]);
+      lo = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
     }
-    sg.y[g][e] = o;
+    if (c + 1 < cols) {
+      const unsigned u = __float_as_uint(xr[c + 1]);
+      hi = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    }
+    yr[p] = lo | (hi << 16);
   }
 }
 
@@ -541,20 +552,20 @@ DL4SS_API int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const lon
   DL4SS_REQUIRE(n >= 1 && n <= CVT_MAX && x && ldx && rows && cols && y && ldy);
   CvtSegs sg{};
   sg.n = n;
-  sg.start[0] = 0;
+  sg.row0[0] = 0;
   for (int i = 0; i < n; ++i) {
     DL4SS_REQUIRE(x[i] && y[i] && rows[i] >= 0 && cols[i] >= 0 && ldx[i] >= cols[i] && ldy[i] >= cols[i] && ldy[i] > 0);
+    DL4SS_REQUIRE(ldy[i] % 2 == 0 && ((uintptr_t)y[i] & 3) == 0);  // 4-B pair stores
     sg.x[i] = x[i];
     sg.y[i] = reinterpret_cast<unsigned short*>(y[i]);
     sg.ldx[i] = ldx[i];
     sg.ldy[i] = ldy[i];
     sg.cols[i] = cols[i];
-    sg.start[i + 1] = sg.start[i] + (long long)rows[i] * ldy[i];
+    sg.row0[i + 1] = sg.row0[i] + rows[i];
   }
-  for (int i = n + 1; i <= CVT_MAX; ++i) sg.start[i] = sg.start[n];
-  if (sg.start[n] == 0) return 0;
-  const unsigned grid = (unsigned)min(16384LL, cdiv(sg.start[n], 256));
-  hipLaunchKernelGGL(f32_to_bf16_multi_kernel, dim3(grid), dim3(256), 0, as_stream(stream), sg);
+  for (int i = n + 1; i <= CVT_MAX; ++i) sg.row0[i] = sg.row0[n];
+  if (sg.row0[n] == 0) return 0;
+  hipLaunchKernelGGL(f32_to_bf16_multi_kernel, dim3(sg.row0[n]), dim3(256), 0, as_stream(stream), sg);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
