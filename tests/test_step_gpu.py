@@ -166,3 +166,15 @@ def test_pit_finds_swapped_targets(dev):
     _lib.call("dl4ss_pit_select", _lib.ptr(tr.part_loss), tr.B, tr.K, tr.nblk, _lib.ptr(tr.perm), _lib.stream_ptr())
     p2 = tr.perm.cpu()
     assert torch.equal(p2, 1 - p1)  # swapped targets -> swapped assignment, bit-exact
+
+
+def test_step_c2_full_size_bf16_pit(dev):
+    """The benchmark's own configuration (BiLSTM-4L, B = 32, N = 32000 -> T = 251,
+    2-spk PIT, bf16 operands) against the fp32 oracle: loss 1e-2 rel, grads 5e-2 of max."""
+    _compare_step(dev, "lstm", 4, 32, 2, 32000, "pit", precision="bf16", tol_loss=1e-2, tol_grad=5e-2)
+
+
+def test_step_c2_full_size_fp32_masked_magnitude(dev):
+    """C2 at full size in the fp32 parity mode, label order: the north-star bar -- masked
+    magnitude spectrogram within 1e-3 relative L2 of the CPU path -- plus loss / gradients."""
+    _compare_step(dev, "lstm", 4, 32, 2, 32000, "label")
