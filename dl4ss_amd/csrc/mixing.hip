@@ -128,9 +128,10 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
 
 DL4SS_API int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gains, int B, int K, int N,
                                    float* stats_ws, float* out_src, float* out_mix, void* stream) {
-  DL4SS_REQUIRE(raw && gains && out_src && out_mix && stats_ws && B >= 0 && K >= 1 && K <= 16 && N > 0);
+  DL4SS_REQUIRE(B >= 0 && K >= 1 && K <= 16 && N > 0);
+  if (B == 0) return 0;  // empty batch: no-op (an empty tensor's pointer may be null)
+  DL4SS_REQUIRE(raw && gains && out_src && out_mix && stats_ws);
   DL4SS_REQUIRE(((uintptr_t)stats_ws & 15) == 0);
-  if (B == 0) return 0;
   SrcPart* part = reinterpret_cast<SrcPart*>(stats_ws);
   hipLaunchKernelGGL(source_stats_kernel, dim3(B * K, NSPLIT), dim3(256), 0, as_stream(stream), raw, N, lengths, part);
   DL4SS_CHECK_LAUNCH();

@@ -344,9 +344,10 @@ __global__ __launch_bounds__(256) void istft_kernel(const float2* __restrict__ S
 DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int n_fft, int hop, int flags,
                              float* X_c64, float* mag, void* stream) {
   DL4SS_REQUIRE(n_fft == NFFT && hop == HOPL && n_samples > NFFT / 2 && n_sig >= 0);
+  if (n_sig == 0) return 0;  // empty batch: no-op (an empty tensor's pointer may be null)
+  DL4SS_REQUIRE(x);
   DL4SS_REQUIRE(!((flags & F_COMPLEX) && !X_c64));
   DL4SS_REQUIRE(!((flags & (F_MAG | F_LOGMAG)) && !mag));
-  if (n_sig == 0) return 0;
   const int T = 1 + n_samples / HOPL;
   const int tiles = (T + FPT - 1) / FPT;
   // one workgroup per tile: measured on MI355X (2048 x 4 s signals, complex + magnitude)
@@ -363,8 +364,9 @@ DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int
 
 DL4SS_API int dl4ss_istft(const float* S_c64, long long n_sig, int T, int n_fft, int hop, int flags, float* y,
                           void* stream) {
-  DL4SS_REQUIRE(n_fft == NFFT && hop == HOPL && T >= 2 && n_sig >= 0 && S_c64 && y);
+  DL4SS_REQUIRE(n_fft == NFFT && hop == HOPL && T >= 2 && n_sig >= 0);
   if (n_sig == 0) return 0;
+  DL4SS_REQUIRE(S_c64 && y);
   const int out_len = HOPL * (T - 1);
   const int tiles = (T - 1 + FPW - 1) / FPW;
   hipLaunchKernelGGL(istft_kernel, dim3((unsigned)(n_sig * tiles)), dim3(256), 0, as_stream(stream),
@@ -379,8 +381,9 @@ DL4SS_API int dl4ss_istft(const float* S_c64, long long n_sig, int T, int n_fft,
 // mask (n_sig, T, 129, 2) multiplied with the mixture spectrum.
 DL4SS_API int dl4ss_istft_apply(const float* X_mix_c64, const float* aux, long long n_sig, int k_per_mix, int T,
                                 int mode, int conj, float* y, void* stream) {
-  DL4SS_REQUIRE(X_mix_c64 && aux && y && T >= 2 && n_sig >= 0 && k_per_mix >= 1 && (mode == 0 || mode == 1));
+  DL4SS_REQUIRE(T >= 2 && n_sig >= 0 && k_per_mix >= 1 && (mode == 0 || mode == 1));
   if (n_sig == 0) return 0;
+  DL4SS_REQUIRE(X_mix_c64 && aux && y);
   const int out_len = HOPL * (T - 1);
   const int tiles = (T - 1 + FPW - 1) / FPW;
   const int flags = (mode == 0 ? F_APPLY_MAG : F_APPLY_CRM) | (conj ? F_CONJ : 0);
