@@ -13,6 +13,9 @@
 
 #include <hipblaslt/hipblaslt.h>
 
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -52,6 +55,56 @@ hipblasLtMatrixLayout_t layout(hipDataType t, uint64_t rows, uint64_t cols, int6
   return l;
 }
 
+constexpr int LT_CANDIDATES = 16;
+
+bool tune_enabled() {
+  const char* e = std::getenv("DL4SS_LT_TUNE");
+  return !(e && std::strcmp(e, "0") == 0);
+}
+
+// time each candidate (2 warm runs, then 5 timed) and return the index of the fastest;
+// C (extent c_elems floats) is restored afterwards
+int pick_fastest(hipblasLtHandle_t h, const LtPlan& p, const hipblasLtMatmulHeuristicResult_t* res, int nres,
+                 const void* A, const void* B, float* C, size_t c_elems, float beta, void* ws, long long ws_bytes,
+                 hipStream_t st) {
+  float* save = nullptr;
+  if (hipMalloc(&save, c_elems * sizeof(float)) != hipSuccess) return 0;
+  hipMemcpyAsync(save, C, c_elems * sizeof(float), hipMemcpyDeviceToDevice, st);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const float alpha = 1.0f;
+  int best = 0;
+  float best_ms = 1e30f;
+  for (int i = 0; i < nres; ++i) {
+    if ((long long)res[i].workspaceSize > ws_bytes) continue;
+    bool ok = true;
+    for (int r = 0; r < 2 && ok; ++r)
+      ok = hipblasLtMatmul(h, p.desc, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo, ws,
+                           res[i].workspaceSize, st) == HIPBLAS_STATUS_SUCCESS;
+    if (!ok) continue;
+    hipEventRecord(e0, st);
+    for (int r = 0; r < 5; ++r)
+      hipblasLtMatmul(h, p.desc, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo, ws,
+                      res[i].workspaceSize, st);
+    hipEventRecord(e1, st);
+    float ms = 0.0f;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+    if (std::getenv("DL4SS_LT_VERBOSE"))
+      fprintf(stderr, "[lt] cand %d ws %zu: %.2f us\n", i, (size_t)res[i].workspaceSize, ms * 1000.0f / 5);
+    if (ms < best_ms) {
+      best_ms = ms;
+      best = i;
+    }
+  }
+  hipMemcpyAsync(C, save, c_elems * sizeof(float), hipMemcpyDeviceToDevice, st);
+  hipStreamSynchronize(st);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(save);
+  return best;
+}
+
 }  // namespace
 
 DL4SS_API int dl4ss_gemm_bf16_lt(int transA, int transB, int M, int N, int K, const void* A, long long lda,
@@ -88,14 +141,24 @@ DL4SS_API int dl4ss_gemm_bf16_lt(int transA, int transB, int M, int N, int K, co
       hipblasLtMatmulPreferenceCreate(&pref);
       uint64_t wsmax = (uint64_t)ws_bytes;
       hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsmax, sizeof(wsmax));
-      hipblasLtMatmulHeuristicResult_t res[1];
+      hipblasLtMatmulHeuristicResult_t res[LT_CANDIDATES];
       int nres = 0;
+      const int want = tune_enabled() ? LT_CANDIDATES : 1;
       const hipblasStatus_t hs = hipblasLtMatmulAlgoGetHeuristic(g_handle[dev], plan.desc, plan.la, plan.lb, plan.lc,
-                                                                 plan.lc, pref, 1, res, &nres);
+                                                                 plan.lc, pref, want, res, &nres);
       hipblasLtMatmulPreferenceDestroy(pref);
       if (hs != HIPBLAS_STATUS_SUCCESS || nres < 1) return (int)hipErrorNotSupported;
-      plan.algo = res[0].algo;
-      plan.ws = res[0].workspaceSize;
+      int pick = 0;
+      if (nres > 1) {
+        const size_t c_elems = (size_t)(batch - 1) * (size_t)strideC + (size_t)(M - 1) * (size_t)ldc + (size_t)N;
+        pick = pick_fastest(g_handle[dev], plan, res, nres, A, B, C, c_elems, beta, workspace, ws_bytes,
+                            as_stream(stream));
+        if (std::getenv("DL4SS_LT_VERBOSE"))
+          fprintf(stderr, "[lt] ta %d tb %d M %d N %d K %d batch %d beta %g: %d candidates, pick %d\n", transA,
+                  transB, M, N, K, batch, beta, nres, pick);
+      }
+      plan.algo = res[pick].algo;
+      plan.ws = res[pick].workspaceSize;
       g_plans[{dev, key}] = plan;
     }
   }

@@ -134,8 +134,11 @@ __device__ __forceinline__ void load_span(const float* __restrict__ x, int n_sam
   }
 }
 
+// the output flags are template parameters: the emit loop carries no per-bin branches and
+// computes the log only where it is written
+template <bool WC, bool WM, bool LOG, bool CONJ>
 __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restrict__ x, int n_samples, int T,
-                                                          int tiles_per_sig, int n_tiles, int flags,
+                                                          int tiles_per_sig, int n_tiles,
                                                           float2* __restrict__ Xc, float* __restrict__ mag) {
   __shared__ float sw[NFFT];
   __shared__ float2 stw[NFFT];
@@ -156,8 +159,6 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
   if (tile < n_tiles) load_span(x, n_samples, tiles_per_sig, tile, tid, pf);
   const int pr = tid >> 4;  // frame pair within the tile
   const int j = tid & 15;
-  const bool conj = flags & F_CONJ;
-  const bool want_c = flags & F_COMPLEX, want_m = flags & (F_MAG | F_LOGMAG), logm = flags & F_LOGMAG;
   float2* sz = &sy[0][0];  // Z of pair p at sz[p * 256 + k]
 
   for (; tile < n_tiles; tile += gridDim.x) {
@@ -213,28 +214,41 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
     const int km = (NFFT - k) & (NFFT - 1);
     float2* xc = Xc + row0 + par * NBIN + k;
     float* xm = mag + row0 + par * NBIN + k;
-    for (int it = 0; 2 * it + par < nfr; ++it) {
-      const float2 zk = sz[it * NFFT + k];
-      const float2 zm = sz[it * NFFT + km];
+    auto emit = [&](int it, float2 zk, float2 zm) {
       float2 X = par == 0 ? make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y))
                           : make_float2(0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x));
-      if (conj) X.y = -X.y;
-      if (want_c) xc[2 * it * NBIN] = X;
-      if (want_m) {
+      if (CONJ) X.y = -X.y;
+      if (WC) xc[2 * it * NBIN] = X;
+      if (WM) {
         float m = __builtin_amdgcn_sqrtf(X.x * X.x + X.y * X.y);
-        if (logm) m = __logf(m + 2.220446049250313e-16f);
+        if (LOG) m = __logf(m + 2.220446049250313e-16f);
         xm[2 * it * NBIN] = m;
       }
+    };
+    if (nfr == FPT) {  // full tile: the LDS reads of four frames issued together
+#pragma unroll
+      for (int i0 = 0; i0 < FPT / 2; i0 += 4) {
+        float2 zk[4], zm[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          zk[u] = sz[(i0 + u) * NFFT + k];
+          zm[u] = sz[(i0 + u) * NFFT + km];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) emit(i0 + u, zk[u], zm[u]);
+      }
+    } else {
+      for (int it = 0; 2 * it + par < nfr; ++it) emit(it, sz[it * NFFT + k], sz[it * NFFT + km]);
     }
     if (tid < nfr) {  // Nyquist bin: Z[128] pairs with itself
       const int f = tid;
       const float2 z = sz[(f >> 1) * NFFT + 128];
       float2 X = (f & 1) == 0 ? make_float2(z.x, 0.0f) : make_float2(z.y, 0.0f);
-      if (conj) X.y = -X.y;
-      if (want_c) Xc[row0 + f * NBIN + 128] = X;
-      if (want_m) {
+      if (CONJ) X.y = -X.y;
+      if (WC) Xc[row0 + f * NBIN + 128] = X;
+      if (WM) {
         float m = fabsf(X.x);
-        if (logm) m = __logf(m + 2.220446049250313e-16f);
+        if (LOG) m = __logf(m + 2.220446049250313e-16f);
         mag[row0 + f * NBIN + 128] = m;
       }
     }
@@ -356,8 +370,16 @@ DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int
   const long long n_tiles = n_sig * tiles;
   DL4SS_REQUIRE(n_tiles < (1LL << 31));
   const long long grid = n_tiles;
-  hipLaunchKernelGGL(stft_fwd_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), x, n_samples, T, tiles,
-                     (int)n_tiles, flags, reinterpret_cast<float2*>(X_c64), mag);
+  using K = void (*)(const float*, int, int, int, int, float2*, float*);
+  static const K kern[16] = {
+      stft_fwd_kernel<0, 0, 0, 0>, stft_fwd_kernel<1, 0, 0, 0>, stft_fwd_kernel<0, 1, 0, 0>, stft_fwd_kernel<1, 1, 0, 0>,
+      stft_fwd_kernel<0, 0, 1, 0>, stft_fwd_kernel<1, 0, 1, 0>, stft_fwd_kernel<0, 1, 1, 0>, stft_fwd_kernel<1, 1, 1, 0>,
+      stft_fwd_kernel<0, 0, 0, 1>, stft_fwd_kernel<1, 0, 0, 1>, stft_fwd_kernel<0, 1, 0, 1>, stft_fwd_kernel<1, 1, 0, 1>,
+      stft_fwd_kernel<0, 0, 1, 1>, stft_fwd_kernel<1, 0, 1, 1>, stft_fwd_kernel<0, 1, 1, 1>, stft_fwd_kernel<1, 1, 1, 1>};
+  const int sel = ((flags & F_COMPLEX) ? 1 : 0) | ((flags & (F_MAG | F_LOGMAG)) ? 2 : 0) |
+                  ((flags & F_LOGMAG) ? 4 : 0) | ((flags & F_CONJ) ? 8 : 0);
+  hipLaunchKernelGGL(kern[sel], dim3((unsigned)grid), dim3(256), 0, as_stream(stream), x, n_samples, T, tiles,
+                     (int)n_tiles, reinterpret_cast<float2*>(X_c64), mag);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

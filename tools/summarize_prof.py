@@ -1,6 +1,6 @@
 """Summarise one tools/prof_round.sh session into profiles/ (tracked).
 
-  python tools/summarize_prof.py gpurun_out/<TAG> <round-tag>
+  python tools/summarize_prof.py gpurun_out/<TAG> <round-tag> [warmup steps]   (bench's --warmup / --steps)
 
 Writes
   profiles/<round>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
@@ -22,7 +22,32 @@ def short(name):
     return name.split("(")[0] if not name.startswith("void ") else name[5:].split("(")[0]
 
 
-def main(src, tag, out="profiles"):
+def per_step(tr, warmup, steps):
+    """Device time per timed step and kernel: the dispatches from the start of step
+    warmup+1 (its source_stats_kernel) to the end of step warmup+steps (its adam_kernel),
+    so one-off work (warmup, first-call GEMM algorithm timing, the bench's probes) is out."""
+    rows = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+            for r in csv.DictReader(open(tr))]
+    rows.sort(key=lambda r: r[1])
+    starts = [r[1] for r in rows if r[0] == "source_stats_kernel"]
+    ends = [r[2] for r in rows if r[0] == "adam_kernel"]
+    if len(starts) < warmup + steps or len(ends) < warmup + steps:
+        return []
+    t0, t1 = starts[warmup], ends[warmup + steps - 1]
+    acc = collections.defaultdict(float)
+    for nm, a, b in rows:
+        if a >= t0 and b <= t1:
+            acc[nm] += (b - a) / 1e3 / steps
+    busy = sum(acc.values())
+    out = ["", f"## Per timed step (steps {warmup + 1}..{warmup + steps}: device us per step)", "",
+           f"wall {(t1 - t0) / 1e3 / steps:.1f} us per step, kernels busy {busy:.1f} us", "",
+           "| kernel | us / step | share % |", "|---|---|---|"]
+    for nm, v in sorted(acc.items(), key=lambda kv: -kv[1]):
+        out.append(f"| `{nm[:90]}` | {v:.1f} | {100 * v / busy:.1f} |")
+    return out
+
+
+def main(src, tag, out="profiles", warmup=1, steps=3):
     os.makedirs(out, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(out, f"{tag}_kernel_stats.csv"))
@@ -48,6 +73,7 @@ def main(src, tag, out="profiles"):
                   "|---|---|---|---|"]
         for (nm, g), v in sorted(by.items()):
             lines.append(f"| `{nm}` | {g} | {len(v)} | {sum(v) / len(v):.2f} |")
+        lines += per_step(tr, warmup, steps)
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
     for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
         f = os.path.join(src, sub, "run_counter_collection.csv")
@@ -80,4 +106,4 @@ def main(src, tag, out="profiles"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *([] if len(sys.argv) < 5 else ["profiles", int(sys.argv[3]), int(sys.argv[4])]))
