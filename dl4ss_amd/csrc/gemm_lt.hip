@@ -69,10 +69,10 @@ int pick_fastest(hipblasLtHandle_t h, const LtPlan& p, const hipblasLtMatmulHeur
                  hipStream_t st) {
   float* save = nullptr;
   if (hipMalloc(&save, c_elems * sizeof(float)) != hipSuccess) return 0;
-  hipMemcpyAsync(save, C, c_elems * sizeof(float), hipMemcpyDeviceToDevice, st);
+  (void)hipMemcpyAsync(save, C, c_elems * sizeof(float), hipMemcpyDeviceToDevice, st);
   hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
   const float alpha = 1.0f;
   int best = 0;
   float best_ms = 1e30f;
@@ -83,11 +83,11 @@ int pick_fastest(hipblasLtHandle_t h, const LtPlan& p, const hipblasLtMatmulHeur
       ok = hipblasLtMatmul(h, p.desc, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo, ws,
                            res[i].workspaceSize, st) == HIPBLAS_STATUS_SUCCESS;
     if (!ok) continue;
-    hipEventRecord(e0, st);
+    (void)hipEventRecord(e0, st);
     for (int r = 0; r < 5; ++r)
       hipblasLtMatmul(h, p.desc, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo, ws,
                       res[i].workspaceSize, st);
-    hipEventRecord(e1, st);
+    (void)hipEventRecord(e1, st);
     float ms = 0.0f;
     if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
     if (std::getenv("DL4SS_LT_VERBOSE"))
@@ -97,11 +97,11 @@ int pick_fastest(hipblasLtHandle_t h, const LtPlan& p, const hipblasLtMatmulHeur
       best = i;
     }
   }
-  hipMemcpyAsync(C, save, c_elems * sizeof(float), hipMemcpyDeviceToDevice, st);
-  hipStreamSynchronize(st);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipFree(save);
+  (void)hipMemcpyAsync(C, save, c_elems * sizeof(float), hipMemcpyDeviceToDevice, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(save);
   return best;
 }
 
