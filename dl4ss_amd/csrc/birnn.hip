@@ -99,9 +99,14 @@ __device__ __forceinline__ float sum_partials(const float* p, int stride, int NG
     for (int i = 0; i < NG; ++i) a += p[i * stride];
     return a;
   }
+  // branch-free: 16 loads from valid addresses (index clamped to NG - 1), then a select --
+  // a guarded load per element compiled to a branch and a saved exec mask each
   float v[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) v[i] = i < NG ? p[i * stride] : 0.0f;
+  for (int i = 0; i < 16; ++i) {
+    const float x = p[(i < NG ? i : NG - 1) * stride];
+    v[i] = i < NG ? x : 0.0f;
+  }
 #pragma unroll
   for (int w = 8; w > 0; w >>= 1)
 #pragma unroll
@@ -705,10 +710,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       float hn = 0.0f, st[4] = {0.f, 0.f, 0.f, 0.f};
       if (cval) {
         float hg[NGATE], gx[NGATE];
+        const float4 g4 = *reinterpret_cast<const float4*>(sin + (s & 1) * BC * 32 * 4 + tid * 4);  // one 16-B read
+        const float gxa[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
           hg[q] = bh[q] + sgate[cb * MT * 16 + q * J + cu];
-          gx[q] = sin[(s & 1) * BC * 32 * 4 + tid * 4 + q];
+          gx[q] = gxa[q];
         }
         if constexpr (CELL == CELL_LSTM) {
           const float ig = fsig(gx[0] + hg[0]);
@@ -1354,10 +1361,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       if (cval) {
         float dh_rec = 0.0f;
         if (s > 0) dh_rec = sum_partials(sdh + cb * J + cu, BC * J, NG);
-        const float* op = sop + (s & 1) * BC * 32 * 8 + tid * 8;
-        const float dout = op[0] + doutb;
-        const float act[4] = {op[1], op[2], op[3], op[4]};
-        const float c = op[5], cprev = op[6], hprev = op[5];
+        // two 16-B reads per lane: the 8-float operand record read as scalars is an 8-way
+        // bank conflict (lanes 32 B apart)
+        const float4 o0 = *reinterpret_cast<const float4*>(sop + (s & 1) * BC * 32 * 8 + tid * 8);
+        const float4 o1 = *reinterpret_cast<const float4*>(sop + (s & 1) * BC * 32 * 8 + tid * 8 + 4);
+        const float dout = o0.x + doutb;
+        const float act[4] = {o0.y, o0.z, o0.w, o1.x};
+        const float c = o1.y, cprev = o1.z, hprev = o1.y;
         const float dh = dout + dh_rec + dh_dir;
         if constexpr (CELL == CELL_LSTM) {
           const float ig = act[0], fg = act[1], gg = act[2], og = act[3];
