@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--mode", default="pit", choices=["label", "pit"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel of the step eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-stft-standalone", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=24)
     ap.add_argument("--cpu-batch", type=int, default=8)
@@ -158,6 +160,8 @@ def main():
 
     def timed_step(i, record):
         raw, gains, spk = pool[i % len(pool)]
+        if use_graph:
+            return tr.step_graph(raw, gains, spk)
         if not record:
             return tr.step(raw, gains, spk)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -175,7 +179,13 @@ def main():
         tr.optimizer_step()
         return loss
 
-    for i in range(args.warmup):
+    # HIP graph (default): the step's launches from STFT to the end of backward replay as
+    # one graph after an eager warm-up step (GEMM plans, workspaces); mixing, the all-reduce
+    # and Adam stay eager (engine.SepTrainer.capture)
+    use_graph = False
+    timed_step(0, False)
+    use_graph = not args.eager
+    for i in range(1, max(args.warmup, 1)):
         timed_step(i, False)
     tr.check()
 
@@ -203,6 +213,15 @@ def main():
     loss_v = float(loss[0].item())
     if not np.isfinite(loss_v):
         raise RuntimeError("non-finite loss")
+
+    if use_graph:  # the in-step STFT launches, timed eagerly on the step's buffers
+        for _ in range(args.steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.stft(tr.mix, complex_out=False, mag_out=True, out_mag=tr.mag_mix)
+            ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
+            e1.record()
+            ev["stft"].append((e0, e1))
 
     # ---- roofline of the two north-star kernels (STFT in-step events; input GEMM isolated), same stream
     T, F = tr.T, tr.F
@@ -277,7 +296,8 @@ def main():
             "config": {"workload": f"C2: 2-spk {args.mode} BiLSTM-4L magnitude mask, B=32/GPU, N=32000 (T=251,F=129),"
                                    " full step: mix+STFT+fwd+loss+bwd+allreduce+Adam",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
-                       "precision": args.precision, "loss": args.mode},
+                       "precision": args.precision, "loss": args.mode,
+                       "launch": "hip-graph" if use_graph else "eager"},
             "loss": loss_v,
             "roofline": sa,
             "roofline_instep": {"bound": "hbm", "kernel": "stft_fwd in-step (2 launches/step: 32 mixtures + 64 "

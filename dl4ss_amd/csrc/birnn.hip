@@ -31,6 +31,7 @@
 // saved activations); waves 4-7 only poll granules into LDS.  All 8 waves run
 // the register-resident matvec (two waves per SIMD keep the VALU issuing).
 // Co-residency: grid <= 240 workgroups.
+#include <cstdlib>
 #include "common.h"
 
 namespace {
@@ -1546,7 +1547,10 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true) {
     const int NG = (H + J - 1) / J;
     if (J > 20) continue;  // gather/publish offset arrays are sized for J <= 20, H <= HMAX(_L)
     int BC = 0;
+    // DL4SS_RNN_MIN_BC (experiments): a wider batch chunk per group, fewer workgroups
+    static const int min_bc = std::getenv("DL4SS_RNN_MIN_BC") ? std::atoi(std::getenv("DL4SS_RNN_MIN_BC")) : 1;
     for (int bc : {1, 2, 4, 8}) {
+      if (bc < min_bc) continue;
       const int nchunk = (B + bc - 1) / bc;
       if (2 * nchunk * NG <= 240 && bc * J <= NROLE) {
         BC = bc;

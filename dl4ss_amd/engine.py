@@ -481,6 +481,52 @@ class SepTrainer:
         self.optimizer_step()
         return loss
 
+    # ------------------------------------------------------------------ HIP graph
+    def _graph_body(self):
+        """The launch sequence recorded into the step graph: STFT features of the mixed
+        batch, forward, loss + its gradient, backward (everything between the mixing
+        kernel and the all-reduce; no host synchronisation inside)."""
+        B, K, N = self.B, self.K, self.N
+        if self.mode == "crm":
+            ops.stft(self.mix, complex_out=True, mag_out=True, out_c=self.Xc_mix, out_mag=self.mag_mix)
+            ops.stft(self.src.view(B * K, N), complex_out=True, mag_out=False,
+                     out_c=self.Xc_src.view(B * K, self.T, self.F, 2))
+        else:
+            ops.stft(self.mix, complex_out=False, mag_out=True, out_mag=self.mag_mix)
+            ops.stft(self.src.view(B * K, N), complex_out=False, mag_out=True,
+                     out_mag=self.mag_src.view(B * K, self.T, self.F))
+        self.forward()
+        return self.loss_and_grad()
+
+    def capture(self):
+        """Record STFT -> forward -> loss -> backward (~70 launches: persistent BiRNN
+        kernels, MFMA / hipBLASLt GEMMs, attention, small kernels) as one HIP graph,
+        replayed by step_graph().  The mixing kernel (its input pointer changes per batch),
+        the RCCL all-reduce and Adam (its bias correction is a per-step host scalar) stay
+        eager launches around the replay.  Call after at least one eager step(), so every
+        GEMM plan (hipBLASLt heuristic timing) and workspace exists before the capture."""
+        if self.overlap:
+            raise RuntimeError("capture(): the DL4SS_OVERLAP side stream is not captured")
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_loss = self._graph_body()
+            self.backward()
+        torch.cuda.synchronize()
+        self.graph = g
+        return g
+
+    def step_graph(self, raw, gains, spk_idx):
+        """step() with the captured graph: mixing, graph replay, all-reduce, Adam."""
+        if getattr(self, "graph", None) is None:
+            self.capture()
+        self.spk.copy_(spk_idx)
+        ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
+        self.graph.replay()
+        self.allreduce()
+        self.optimizer_step()
+        return self._graph_loss
+
     def check(self):
         torch.cuda.synchronize()
         s = int(self.status.item())
