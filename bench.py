@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_FILE = "profiles/r01_prof_h_pmc.json"
+PMC_FILE = "profiles/r01_prof_i_pmc.json"
 
 
 def stft_grid_threads(n_sig, T):
@@ -222,6 +222,7 @@ def main():
             ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
             e1.record()
             ev["stft"].append((e0, e1))
+        torch.cuda.synchronize()
 
     # ---- roofline of the two north-star kernels (STFT in-step events; input GEMM isolated), same stream
     T, F = tr.T, tr.F
