@@ -136,13 +136,16 @@ __device__ __forceinline__ void store_block(const uint4 (&v)[8], unsigned short*
 // MFMA that every workgroup pulls through L2 -- the 128 x 128 tile needs ~2x the per-CU
 // L2 bandwidth at full MFMA rate.  Staging: threads [0, BM) stage A blocks, [BM, BM+BN)
 // B blocks, the rest (256x128: 128 threads) only run MFMAs; all share the barriers.
+#ifndef GBB_NS
+#define GBB_NS 3  // k-tiles in flight per staging thread, 256-thread tiles
+#endif
 template <int BM_, int BN_, int WM_, int WN_>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr int TI = WM / 32, TJ = WN / 32;
   static constexpr int WAVES_N = BN / WN;
   static constexpr int NT = (BM / WM) * (BN / WN) * 64;
-  static constexpr int NS = TI * TJ > 4 ? 2 : 3;  // register ring depth (VGPR budget at 512 threads)
+  static constexpr int NS = TI * TJ > 4 ? 2 : GBB_NS;  // register ring depth (VGPR budget at 512 threads)
   static_assert(WN == 64, "the epilogue maps 16 lanes x 4 columns onto a 64-wide wave tile");
 };
 typedef Tile<128, 128, 64, 64> T128x128;

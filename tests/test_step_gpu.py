@@ -183,9 +183,13 @@ def test_step_c2_full_size_fp32_masked_magnitude(dev):
 @pytest.mark.parametrize("precision,mode", [("bf16", "pit"), ("fp32", "label")])
 def test_graph_step_matches_eager(dev, precision, mode):
     """SepTrainer.step_graph (STFT -> forward -> loss -> backward replayed as one HIP graph,
-    mixing / Adam eager) against step() from identical weights over three steps on
-    changing batches: losses and Adam-updated parameters agree (the BiRNN bias gradients
-    are float atomics, so last-bit differences are allowed: gradients 1e-5 of max)."""
+    mixing / Adam eager) against step() from the same state on three changing batches: for
+    each batch the trainer state (parameters, Adam moments, step count) is saved, one eager
+    step is taken, the state is restored and the graph step is taken on the same batch;
+    losses, gradients and updated parameters must agree.  The BiRNN bias gradients are
+    float atomics (order varies between runs), so last-bit differences are allowed: loss
+    1e-6 relative, gradients 1e-5 of max, parameters 1e-6 absolute (one Adam step; up
+    to lr on at most 1e-4 of the elements)."""
     B, K, N = 4, 2, 8000
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=5)
     batches = []
@@ -194,19 +198,19 @@ def test_graph_step_matches_eager(dev, precision, mode):
         batches.append((torch.from_numpy(src.astype(np.float32)).to(dev),
                         torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
                         torch.from_numpy(spk.astype(np.int32)).to(dev)))
-    res = []
-    for use_graph in (False, True):
-        net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=7)
-        tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision)
-        tr.step(*batches[0])  # eager warm-up step (GEMM plans, workspaces), then the compared steps
-        losses = []
-        for b in batches:
-            loss = tr.step_graph(*b) if use_graph else tr.step(*b)
-            losses.append(float(loss[0].item()))
+    net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=7)
+    tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision)
+    tr.step(*batches[0])  # eager warm-up step (GEMM plans, workspaces) before the capture
+    for b in batches:
+        state = (net.flat.detach().clone(), tr.m.clone(), tr.v.clone(), tr.step_count)
+        le = float(tr.step(*b)[0].item())
+        ge, pe = net.grad.detach().clone(), net.flat.detach().clone()
+        net.flat.copy_(state[0]); tr.m.copy_(state[1]); tr.v.copy_(state[2]); tr.step_count = state[3]
+        lg = float(tr.step_graph(*b)[0].item())
         tr.check()
-        res.append((losses, net.grad.detach().clone(), net.flat.detach().clone()))
-    (l0, g0, p0), (l1, g1, p1) = res
-    assert np.allclose(l0, l1, rtol=1e-5, atol=0), (l0, l1)
-    assert float((g0 - g1).abs().max()) <= 1e-5 * float(g0.abs().max())
-    # Adam turns a last-bit sign difference of a near-zero gradient into up to lr per step
-    assert float((p0 - p1).abs().max()) <= 4 * 2e-4 + 1e-6
+        assert abs(lg - le) <= 1e-6 * abs(le), (lg, le)
+        assert float((net.grad - ge).abs().max()) <= 1e-5 * float(ge.abs().max())
+        # a near-zero gradient whose last bits differ can move its Adam step by up to lr:
+        # allow that on a handful of elements, everything else within 1e-6
+        dp = (net.flat - pe).abs()
+        assert float(dp.max()) <= 2 * 2e-4 and int((dp > 1e-6).sum()) <= max(1, dp.numel() // 10000)
