@@ -154,6 +154,8 @@ struct RnnArgs {
   unsigned short* dGhb;    // bwd GRU: bf16(dGh)            -- dW_hh GEMM operand
   float* dbi;              // bwd: += sum_{b,t} dG   (bias_ih gradient, (2, NGATE*H))
   float* dbh;              // bwd: += sum_{b,t} dGh  (bias_hh gradient)
+  float* dbpart;           // bwd: per-row bias sums [b][d][ih | hh][NGATE*H] (fixed-order reduce), or
+                           //      null: float atomics straight into dbi / dbh
 };
 
 __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& group, int& w) {
@@ -1487,8 +1489,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     store_dg();  // this step's dG / dGh, after the publish (off the critical path)
     STAMP(6)
   }
-  // fused bias gradients: one atomic per (cell, gate) for the whole sequence
-  if (cval) {
+  // fused bias gradients: this cell's sums over t, one plain store per (row, gate) into the
+  // per-row partials (bias_reduce_kernel sums the rows in fixed order: deterministic)
+  if (cval && a.dbpart) {
+    float* pp = a.dbpart + (long long)(bg * 2 + d) * 2 * GH;
+#pragma unroll
+    for (int q = 0; q < NGATE; ++q) {
+      pp[q * H + cj] = sbi[q];
+      pp[GH + q * H + cj] = sbh[q];
+    }
+  } else if (cval) {
 #pragma unroll
     for (int q = 0; q < NGATE; ++q) {
       if (a.dbi) atomicAdd(a.dbi + d * GH + q * H + cj, sbi[q]);
@@ -1646,7 +1656,34 @@ void fill_args(RnnArgs& a, const Plan& p, int B, int T, int H) {
 DL4SS_API void dl4ss_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
 #endif
 
-static long long workspace_bytes(const Plan& p, int H) {
+// dbi[i] += sum_b part[b][d][0][g], dbh[i] += sum_b part[b][d][1][g] for i = d * GH + g, rows
+// in order b = 0 .. B-1 (the BPTT kernel's per-row bias sums)
+__global__ __launch_bounds__(256) void bias_reduce_kernel(const float* __restrict__ part, int B, int GH,
+                                                          float* __restrict__ dbi, float* __restrict__ dbh) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * GH) return;
+  const int d = i / GH, g = i - d * GH;
+  float si = 0.0f, sh = 0.0f;
+  for (int b = 0; b < B; ++b) {
+    const float* pp = part + (long long)(b * 2 + d) * 2 * GH + g;
+    si += pp[0];
+    sh += pp[GH];
+  }
+  if (dbi) dbi[i] += si;
+  if (dbh) dbh[i] += sh;
+}
+
+// hand-off area of the BPTT / forward workspace, 256-B aligned
+static long long handoff_bytes(const Plan& p, int H);
+
+// per-row bias partials behind the hand-off area (BPTT with fused bias gradients)
+static long long bias_part_bytes(const Plan& p, int H) {
+  return p.big ? 0 : (long long)p.nchunk * p.BC * 2 * 2 * 4 * H * 4;
+}
+
+static long long workspace_bytes(const Plan& p, int H) { return handoff_bytes(p, H) + bias_part_bytes(p, H); }
+
+static long long handoff_bytes(const Plan& p, int H) {
   const long long groups = 2LL * p.nchunk;
   long long fwd = groups * 2 * p.BC * H * 8;
   const long long fwd_pk = groups * 4 * p.BC * p.NG * 8 * 8;
@@ -1655,7 +1692,8 @@ static long long workspace_bytes(const Plan& p, int H) {
   long long bwd = groups * 2 * p.NG * p.BC * H * 8;
   const long long bwd_pk = groups * 4LL * p.NG * p.BC * (((H + 1) / 2 + 1) & ~1) * 8;
   if (bwd_pk > bwd) bwd = bwd_pk;
-  return fwd > bwd ? fwd : bwd;
+  const long long n = fwd > bwd ? fwd : bwd;
+  return (n + 255) / 256 * 256;
 }
 
 // the larger of the fp32 and bf16 plans' needs (either precision may use the buffer);
@@ -1768,9 +1806,15 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   a.dGb = reinterpret_cast<unsigned short*>(dG_bf16); a.dGhb = reinterpret_cast<unsigned short*>(dGh_bf16);
   a.dbi = db_ih; a.dbh = db_hh;
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
+  const bool bias = pk && (db_ih || db_hh);
+  a.dbpart = bias ? reinterpret_cast<float*>(static_cast<char*>(workspace) + handoff_bytes(p, H)) : nullptr;
   a.status = status;
   const int grid = (int)(groups * p.NG);
   const size_t smem = pk ? p.smem_bwd_pk : mf ? p.smem_bwd_mf : p.smem_bwd;
-  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, pk, p.BC, a, grid, smem, st)
-                           : dispatch<CELL_GRU>(false, mf, pk, p.BC, a, grid, smem, st);
+  const int e = cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, pk, p.BC, a, grid, smem, st)
+                                  : dispatch<CELL_GRU>(false, mf, pk, p.BC, a, grid, smem, st);
+  if (e || !bias) return e;
+  const int GH = (cell == CELL_LSTM ? 4 : 3) * H;
+  hipLaunchKernelGGL(bias_reduce_kernel, dim3((2 * GH + 255) / 256), dim3(256), 0, st, a.dbpart, B, GH, db_ih, db_hh);
+  return (int)hipGetLastError();
 }

@@ -112,7 +112,9 @@ int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ld
 
 /* ---- persistent bidirectional LSTM / GRU recurrence ---------------------- */
 enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
-/* Granule workspace (bytes) needed by dl4ss_birnn_fwd / _bwd for (cell, B, H); -1 if unsupported.
+/* Workspace (bytes) needed by dl4ss_birnn_fwd / _bwd for (cell, B, H); -1 if unsupported: the
+ * hand-off granules, then (bf16 BPTT with fused bias gradients) the per-row bias partials that
+ * a fixed-order reduce adds into db_ih / db_hh, so the gradients are bitwise reproducible.
  * The launchers zero the workspace themselves (hipMemsetAsync) unless `precision` carries
  * DL4SS_RNN_WS_ZEROED: the caller then guarantees it is zero (e.g. one fill per training
  * step over separate workspaces for every layer and pass). */
