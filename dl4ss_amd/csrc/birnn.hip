@@ -481,7 +481,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 // --------------------------------------------------------------------------
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int PKU = 24;     // staged h slots per (row, producer): 8 granules x 3
-constexpr int WPOLL = 4;    // the polling wave
+constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
+#ifndef BWD_NPW
+#define BWD_NPW 2  // BPTT polling waves
+#endif
 constexpr unsigned FAST_SPINS = 256;  // sweeps of the fast copy before the safe copy is polled
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
@@ -1192,17 +1195,18 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   u64* xg = a.xbuf + (long long)group * 4 * copy_g;
   const __amdgpu_buffer_rsrc_t xr = granule_rsrc(xg, (unsigned)(4 * copy_g * 8));
 
-  // ---- prefetch waves 5-7: per-step operands of every own (b, unit): 8 slots per cell
+  // ---- prefetch waves WPF..7: per-step operands of every own (b, unit): 8 slots per cell
   //   0 dOut, 1..4 act, 5 c (LSTM) / h_prev (GRU), 6 c_prev (LSTM), 7 unused
-  constexpr int NPF = NT - (WPOLL + 1) * 64;
+  constexpr int WPF = WPOLL + BWD_NPW;  // waves WPOLL .. WPF-1 poll
+  constexpr int NPF = NT - WPF * 64;
   constexpr int NQ = (BC * 20 * 8 + NPF - 1) / NPF;
   StepLoader<NQ> ld;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int i = tid - (WPOLL + 1) * 64 + q * NPF;  // item = slot * (BC*J) + cell
+    const int i = tid - WPF * 64 + q * NPF;  // item = slot * (BC*J) + cell
     const int slot = i / (BC * J), cell = i % (BC * J);
     const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
-    const bool on = wv > WPOLL && slot < 8;
+    const bool on = wv >= WPF && slot < 8;
     const bool valid = on && ib < a.B && ij < H;
     const float* p = nullptr;
     int stride = 2 * H, shift = 0;
@@ -1224,20 +1228,22 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.shift[q] = shift;
     ld.dst[q] = on ? ((cell / J) * 32 + iu) * 8 + slot : -1;
   }
-  if (wv > WPOLL) ld.issue(d == 0 ? T - 1 : 0, T);
+  if (wv >= WPF) ld.issue(d == 0 ? T - 1 : 0, T);
   __syncthreads();
   STAMP_DECL
 
-  if (wv == WPOLL) {
-    // ---- polling wave: 16-B unit idx = (producer * BC + b) * (J/4) + quad
-    constexpr int GLK = (80 * BC + 63) / 64;  // NG <= 16, J <= 20
+  if (wv >= WPOLL && wv < WPF) {
+    // ---- polling waves: 16-B unit idx = (producer * BC + b) * (J/4) + quad, wave pw
+    //      takes the 64-unit blocks pw, pw + BWD_NPW, ...
+    constexpr int GLK = (80 * BC + 64 * BWD_NPW - 1) / (64 * BWD_NPW);  // NG <= 16, J <= 20
+    const int pw = wv - WPOLL;
     const int JQ = J / 4;
     const int n16 = NG * BC * JQ;
     int loff[GLK], doff[GLK];
     bool on[GLK];
 #pragma unroll
     for (int g = 0; g < GLK; ++g) {
-      const int idx = lane + 64 * g;
+      const int idx = lane + 64 * (g * BWD_NPW + pw);
       on[g] = idx < n16;
       const int pb = idx / JQ, qd = idx % JQ;  // pb = producer * BC + b
       loff[g] = on[g] ? pb * HG + (j0 >> 1) + 2 * qd : 0;  // granule offset within a copy
@@ -1313,7 +1319,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     STAMP_FLUSH
     return;
   }
-  if (wv > WPOLL) {
+  if (wv >= WPF) {
     for (int s = 0; s < T; ++s) {
       ld.commit(sop + (s & 1) * BC * 32 * 8);
       if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
