@@ -485,6 +485,9 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
 #endif
+#ifndef FWD_NPW
+#define FWD_NPW 2  // forward polling waves: 4, and 7 when 2 (its MFMA tile index 6 must be >= MT)
+#endif
 constexpr unsigned FAST_SPINS = 256;  // sweeps of the fast copy before the safe copy is polled
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
@@ -551,8 +554,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   u64* xg = a.xbuf + (long long)group * 4 * slot_g;
   const __amdgpu_buffer_rsrc_t xr = granule_rsrc(xg, (unsigned)(4 * slot_g * 8));
 
-  // ---- prefetch waves 5-7: input projection G[b][t][d][q*H + j] of every own (b, unit, gate)
-  constexpr int NPF = NT - (WPOLL + 1) * 64;  // 192 prefetch lanes
+  // ---- prefetch waves 5-7 (5-6 with FWD_NPW = 2: wave 7 polls too): input projection
+  //      G[b][t][d][q*H + j] of every own (b, unit, gate)
+  constexpr int NPF = NT - (WPOLL + FWD_NPW) * 64;  // 192 / 128 prefetch lanes
+  const bool pollw = wv == WPOLL || (FWD_NPW == 2 && wv == 7);
+  const bool pfw = wv > WPOLL && !pollw;
   constexpr int NQ = (BC * 20 * 4 + NPF - 1) / NPF;
   StepLoader<NQ> ld;
 #pragma unroll
@@ -560,13 +566,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     const int i = tid - (WPOLL + 1) * 64 + q * NPF;  // item = gate * (BC*J) + cell
     const int gate = i / (BC * J), cell = i % (BC * J);
     const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
-    const bool on = wv > WPOLL && gate < NGATE;
+    const bool on = pfw && gate < NGATE;
     ld.p[q] = (on && ib < a.B && ij < H) ? a.G + ((long long)ib * T * 2 + d) * GH + gate * H + ij : nullptr;
     ld.stride[q] = 2 * GH;
     ld.shift[q] = 0;
     ld.dst[q] = on ? ((cell / J) * 32 + iu) * 4 + gate : -1;
   }
-  if (wv > WPOLL) ld.issue(d == 0 ? 0 : T - 1, T);
+  if (pfw) ld.issue(d == 0 ? 0 : T - 1, T);
   __syncthreads();
   STAMP_DECL
 
@@ -589,16 +595,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     }
   };
 
-  if (wv == WPOLL) {
-    // ---- polling wave: 16-B unit idx = (b * NG + producer) * 4 + pair; lane holds
-    //      units lane + 64 g (idle lanes re-read unit 0: every load is unconditional,
-    //      so the compiler can keep a sweep in flight behind a counted vmcnt)
-    constexpr int GLK = BC;  // BC * NG * 4 <= 64 * BC  (NG <= 16, checked by the plan)
+  if (pollw) {
+    // ---- polling wave(s): 16-B unit idx = (b * NG + producer) * 4 + pair; lane holds
+    //      units lane + 64 (g FWD_NPW + pwv) (idle lanes re-read unit 0: every load is
+    //      unconditional, so the compiler can keep a sweep in flight behind a counted vmcnt)
+    constexpr int GLK = (BC + FWD_NPW - 1) / FWD_NPW;  // BC * NG * 4 <= 64 * BC  (NG <= 16, checked by the plan)
+    const int pwv = wv == WPOLL ? 0 : 1;
     const int n16 = BC * NG * 4;
     int loff[GLK], doff[GLK], dlim[GLK];
 #pragma unroll
     for (int g = 0; g < GLK; ++g) {
-      const int idx = lane + 64 * g;
+      const int idx = lane + 64 * (g * FWD_NPW + pwv);
       const bool on = idx < n16;
       const int b = idx / (NG * 4), pw = (idx / 4) % NG, pp = idx % 4;
       const int k0 = pw * J + 6 * pp;
@@ -693,7 +700,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     STAMP_FLUSH
     return;
   }
-  if (wv > WPOLL) {
+  if (pfw) {
     for (int s = 0; s < T; ++s) {
       ld.commit(sin + (s & 1) * BC * 32 * 4);
       if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
@@ -1584,7 +1591,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true) {
     const int SHB = (p.big ? HMAX_L : HMAX) + 8, MT = (R + 15) / 16, SDG = (4 * 20 + 31) / 32 * 32 + 8;
     p.smem_fwd_mf = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * J * 4);
     p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
-    p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= 7;
+    p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= (FWD_NPW == 2 ? 6 : 7);
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
     p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((NG * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16) + 2 * BC * 32 * 8);
     p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
