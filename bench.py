@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_FILE = "profiles/r01_prof_j_pmc.json"
+PMC_FILE = "profiles/r01_prof_k_pmc.json"
 
 
 def stft_grid_threads(n_sig, T):
