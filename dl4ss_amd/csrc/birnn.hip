@@ -486,7 +486,7 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #define BWD_NPW 2  // BPTT polling waves
 #endif
 #ifndef FWD_NPW
-#define FWD_NPW 2  // forward polling waves: 4, and 7 when 2 (its MFMA tile index 6 must be >= MT)
+#define FWD_NPW 2  // forward polling waves: 4, and 7 when >= 2, and 6 when 3 (their MFMA tile indices must be >= MT)
 #endif
 constexpr unsigned FAST_SPINS = 256;  // sweeps of the fast copy before the safe copy is polled
 
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   // ---- prefetch waves 5-7 (5-6 with FWD_NPW = 2: wave 7 polls too): input projection
   //      G[b][t][d][q*H + j] of every own (b, unit, gate)
   constexpr int NPF = NT - (WPOLL + FWD_NPW) * 64;  // 192 / 128 prefetch lanes
-  const bool pollw = wv == WPOLL || (FWD_NPW == 2 && wv == 7);
+  const bool pollw = wv == WPOLL || (FWD_NPW >= 2 && wv == 7) || (FWD_NPW == 3 && wv == 6);
   const bool pfw = wv > WPOLL && !pollw;
   constexpr int NQ = (BC * 20 * 4 + NPF - 1) / NPF;
   StepLoader<NQ> ld;
@@ -600,7 +600,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     //      units lane + 64 (g FWD_NPW + pwv) (idle lanes re-read unit 0: every load is
     //      unconditional, so the compiler can keep a sweep in flight behind a counted vmcnt)
     constexpr int GLK = (BC + FWD_NPW - 1) / FWD_NPW;  // BC * NG * 4 <= 64 * BC  (NG <= 16, checked by the plan)
-    const int pwv = wv == WPOLL ? 0 : 1;
+    const int pwv = wv == WPOLL ? 0 : wv == 7 ? 1 : 2;
     const int n16 = BC * NG * 4;
     int loff[GLK], doff[GLK], dlim[GLK];
 #pragma unroll
@@ -1591,7 +1591,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true) {
     const int SHB = (p.big ? HMAX_L : HMAX) + 8, MT = (R + 15) / 16, SDG = (4 * 20 + 31) / 32 * 32 + 8;
     p.smem_fwd_mf = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * J * 4);
     p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
-    p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= (FWD_NPW == 2 ? 6 : 7);
+    p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= (FWD_NPW == 3 ? 5 : FWD_NPW == 2 ? 6 : 7);
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
     p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((NG * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16) + 2 * BC * 32 * 8);
     p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
