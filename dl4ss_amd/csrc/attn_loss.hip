@@ -98,10 +98,28 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
     if constexpr (VB) {
       const unsigned* src = reinterpret_cast<const unsigned*>(a.Vb + ((long long)b * a.rows_per_b + r0) * E);
       const int n2 = nr * E / 2;
+#ifdef ATTN_STAGE_LOOP
       for (int i = tid; i < n2; i += NT) {
         const unsigned w = src[i];
         reinterpret_cast<float2*>(sv)[i] = make_float2(__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u));
       }
+#else
+      // every load of the tile issued before the first LDS store (a load -> store loop
+      // kept one 4-B load per thread in flight)
+      constexpr int NW = (TILE * E / 2 + NT - 1) / NT;
+      unsigned w[NW];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int i = tid + q * NT;
+        w[q] = i < n2 ? src[i] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int i = tid + q * NT;
+        if (i < n2)
+          reinterpret_cast<float2*>(sv)[i] = make_float2(__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xFFFF0000u));
+      }
+#endif
     } else {
       const float* src = Vb + (long long)r0 * E;
       const int n = nr * E;
