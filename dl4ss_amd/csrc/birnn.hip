@@ -485,6 +485,9 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
 #endif
+#ifndef FWD_MV_CHAINS
+#define FWD_MV_CHAINS 2  // forward bf16 matvec: accumulator chains per MFMA tile (4: 367 vs 363 us per pass)
+#endif
 #ifndef FWD_NPW
 #define FWD_NPW 2  // forward polling waves: 4, and 7 when >= 2, and 6 when 3 (their MFMA tile indices must be >= MT)
 #endif
@@ -578,20 +581,24 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 
   auto matvec = [&]() {  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
     if (!mv) return;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const unsigned short* bp = shb + (lane & 15) * SHB + 8 * (lane >> 4);
     bf16x8 bv[KSMAX];
 #pragma unroll
     for (int ks = 0; ks < KSMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
+    // FWD_MV_CHAINS independent accumulator chains over the k-steps (the chain length is
+    // the matvec's latency), summed in fixed order
+    f32x4 acc[FWD_MV_CHAINS];
 #pragma unroll
-    for (int ks = 0; ks < KSMAX; ks += 2) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[ks], bv[ks], acc0, 0, 0, 0);
-      if (ks + 1 < KSMAX) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[ks + 1], bv[ks + 1], acc1, 0, 0, 0);
-    }
+    for (int c = 0; c < FWD_MV_CHAINS; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks)
+      acc[ks % FWD_MV_CHAINS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[ks], bv[ks], acc[ks % FWD_MV_CHAINS], 0, 0, 0);
+#pragma unroll
+    for (int c = 1; c < FWD_MV_CHAINS; ++c) acc[0] += acc[c];
     const int col = lane & 15;
     if (col < BC) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sgate[col * MT * 16 + tile * 16 + (lane >> 4) * 4 + i] = acc0[i] + acc1[i];
+      for (int i = 0; i < 4; ++i) sgate[col * MT * 16 + tile * 16 + (lane >> 4) * 4 + i] = acc[0][i];
     }
   };
 
