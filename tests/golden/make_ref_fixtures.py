@@ -1,0 +1,554 @@
+"""Golden fixtures produced by the REFERENCE's own code (run in the build container only:
+``python tests/golden/make_ref_fixtures.py``; needs ``/root/reference``).
+
+The reference is Python-2 code.  This script reads its driver files
+as text, translates them in memory with ``lib2to3``, picks out by AST the module pieces
+on the hot path and the training-loop statements by their reference line numbers, and
+executes them on torch-CPU with
+
+* a ``config`` stub holding the values the drivers read (BATCH_SIZE, HIDDEN_UNITS, ...),
+* ``Tensor.cuda`` / ``Module.cuda`` as no-ops (no GPU here; the arithmetic is torch-CPU fp32),
+* the logging lines (``print``, ``lrs.send``) and the Discriminator lines left out.
+
+Nothing of the reference is written into the repository: only the resulting data
+(inputs, weights recipe, masks, predictions, losses, gradients, Adam-updated
+parameters) goes into ``tests/golden/ref_*.npz``.  The reference's librosa STFT is
+absent, so the network inputs (|STFT| of synthetic mixtures) come from
+``oracle/dsp.py`` (pinned to numpy.fft) -- the fixtures pin everything downstream
+of the features: R5-R15 as the reference computes them.
+
+Fixtures
+--------
+ref_c2_evalver.npz   TDAA_beta/main_run_sstune_EvalVer.py:587-641,658-668,673-675
+                     (BiLSTM-4L MIX_SPEECH, embedding, ADDJUST, dot attention, MSE +
+                     0.5 sum-to-one, Adam) + the discarded classifier forward (:592)
+ref_c1_mainrun.npz   Torch_multi/main_run.py:460-522 (BiGRU-2L, dense 101-channel
+                     embedding, multi-hot mask, 101-channel MSE, no ADDJUST)
+ref_c3_crm.npz       TDAA_beta/main_run_sstune_cRM_EvalVer.py:645-752 (cRM branch,
+                     inverse compression :688, complex MSE :720-743)
+ref_c4_3spk.npz      Torch_multi/main_run_multi_selfSS_dB.py:457-532 (3 speakers)
+ref_topk.npz         top_k_mask (EvalVer.py:390-405, GRID.py:227-244), multi_label_vector
+                     (TDAA_beta/test_multi_labels_speech.py:287-300), LR schedules
+                     (EvalVer.py:570-575, selfSS_dB.py:442-444)
+"""
+import ast
+import contextlib
+import io
+import os
+import sys
+import types
+import warnings
+
+import numpy as np
+import torch
+from torch import nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import ref_recipe as rr  # noqa: E402
+from oracle import dsp  # noqa: E402
+from dl4ss_amd import synth  # noqa: E402
+
+REF = os.environ.get("DL4SS_REFERENCE", "/root/reference")
+EVALVER = "TDAA_beta/main_run_sstune_EvalVer.py"
+CRM = "TDAA_beta/main_run_sstune_cRM_EvalVer.py"
+MAINRUN = "Torch_multi/main_run.py"
+SELFSS = "Torch_multi/main_run_multi_selfSS_dB.py"
+GRID = "Torch_multi/main_run_multi_selfSS_recuReal_GRID.py"
+LABELS = "TDAA_beta/test_multi_labels_speech.py"
+
+
+# ----------------------------------------------------------------------------- translation
+_cache = {}
+
+
+def translated(rel):
+    """py2 source -> py3 source (lib2to3, line structure preserved)."""
+    if rel not in _cache:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            from lib2to3 import refactor
+
+            tool = refactor.RefactoringTool(refactor.get_fixers_from_package("lib2to3.fixes"))
+        with open(os.path.join(REF, rel), encoding="utf-8") as f:
+            src = f.read()
+        _cache[rel] = str(tool.refactor_string(src, rel))
+    return _cache[rel]
+
+
+def snippet_defs(rel, first, last, names):
+    """Definitions from reference lines first..last only (for files whose remainder
+    lib2to3 cannot parse), translated on their own."""
+    key = (rel, first, last)
+    if key not in _cache:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            from lib2to3 import refactor
+
+            tool = refactor.RefactoringTool(refactor.get_fixers_from_package("lib2to3.fixes"))
+        with open(os.path.join(REF, rel), encoding="utf-8") as f:
+            lines = f.read().splitlines()[first - 1:last]
+        _cache[key] = str(tool.refactor_string("\n".join(lines) + "\n", rel))
+    tree = ast.parse(_cache[key], rel)
+    keep = [n for n in tree.body if isinstance(n, (ast.ClassDef, ast.FunctionDef)) and n.name in names]
+    assert {n.name for n in keep} == set(names), (rel, first, last, names)
+    return compile(ast.Module(body=keep, type_ignores=[]), os.path.join(REF, rel), "exec")
+
+
+def line(rel, n):
+    return translated(rel).splitlines()[n - 1]
+
+
+def check_line(rel, n, text):
+    """Guard: the statement at reference line n still reads as expected after translation."""
+    got = line(rel, n).replace(" ", "")
+    assert text.replace(" ", "") in got, (rel, n, got)
+
+
+def module_defs(rel, names, consts=()):
+    """The top-level class / function definitions (and constant assignments) named."""
+    tree = ast.parse(translated(rel), rel)
+    keep = []
+    for node in tree.body:
+        if isinstance(node, (ast.ClassDef, ast.FunctionDef)) and node.name in names:
+            keep.append(node)
+        elif isinstance(node, ast.Assign) and any(isinstance(t, ast.Name) and t.id in consts for t in node.targets):
+            keep.append(node)
+    found = {getattr(n, "name", None) for n in keep}
+    missing = set(names) - found
+    assert not missing, (rel, missing)
+    return compile(ast.Module(body=keep, type_ignores=[]), os.path.join(REF, rel), "exec")
+
+
+def _is_logging(stmt):
+    """print(...) / lrs.send(...) expression statements."""
+    if isinstance(stmt, ast.Expr) and isinstance(stmt.value, ast.Call):
+        f = stmt.value.func
+        if isinstance(f, ast.Name) and f.id == "print":
+            return True
+        if isinstance(f, ast.Attribute) and isinstance(f.value, ast.Name) and f.value.id == "lrs":
+            return True
+    return False
+
+
+def loop_body(rel, loop_line, keep_ranges):
+    """Statements of the loop starting at reference line loop_line (inside main()) whose
+    first line falls in one of keep_ranges (inclusive), minus logging statements."""
+    tree = ast.parse(translated(rel), rel)
+    loop = None
+    for node in ast.walk(tree):
+        if isinstance(node, (ast.For, ast.While)) and node.lineno == loop_line:
+            loop = node
+    assert loop is not None, (rel, loop_line)
+    body = [s for s in loop.body if any(a <= s.lineno <= b for a, b in keep_ranges) and not _is_logging(s)]
+    return compile(ast.Module(body=body, type_ignores=[]), os.path.join(REF, rel), "exec")
+
+
+@contextlib.contextmanager
+def cpu_cuda():
+    """Tensor.cuda / Module.cuda as no-ops for the duration (no GPU in this container)."""
+    t_cuda, m_cuda = torch.Tensor.cuda, nn.Module.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    nn.Module.cuda = lambda self, *a, **k: self
+    try:
+        yield
+    finally:
+        torch.Tensor.cuda, nn.Module.cuda = t_cuda, m_cuda
+
+
+def base_namespace(config):
+    import torch.nn.functional as F
+    from torch.autograd import Variable
+
+    return dict(torch=torch, nn=nn, F=F, np=np, Variable=Variable, config=config, __name__="ref_exec")
+
+
+def make_config(**kw):
+    c = types.SimpleNamespace(HIDDEN_UNITS=300, EMBEDDING_SIZE=50, NUM_LAYERS=2, Ground_truth=True,
+                              UNK_SPK_SUPP=3, is_ComlexMask=False, is_SelfTune=True)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+# ----------------------------------------------------------------------------- data
+NUM_LABELS = 101
+SPK_NAMES = [f"spk{i:03d}" for i in range(NUM_LABELS)]
+DICT_SPK2IDX = {s: i for i, s in enumerate(SPK_NAMES)}
+DICT_IDX2SPK = {i: s for i, s in enumerate(SPK_NAMES)}
+
+
+def synthetic_batch(B, K, N, seed, crm=False):
+    """Synthetic sources -> oracle features (the librosa STFT is absent here)."""
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=seed)
+    src, spk, u = gen.batch(B)
+    gains = synth.gains_for(u, K)
+    mix_feas, mix_mag, targets = [], [], []
+    for b in range(B):
+        srcs = [dsp.normalise_source(src[b, k].astype(np.float32), N) for k in range(K)]
+        s, m = dsp.mix_sources(srcs, gains[b])
+        Sm = dsp.stft_tf(m)
+        mix_feas.append(np.abs(Sm).astype(np.float32))
+        if crm:
+            mix_mag.append(dsp.convert2(Sm))
+            targets.append(np.stack([dsp.convert2(dsp.stft_tf(s[k])) for k in range(K)]))
+        else:
+            targets.append(np.stack([np.abs(dsp.stft_tf(s[k])).astype(np.float32) for k in range(K)]))
+    d = dict(src=src.astype(np.float32), gains=gains.astype(np.float32), spk=spk,
+             mix_feas=np.array(mix_feas, np.float32), targets=np.array(targets, np.float32))
+    if crm:
+        d["mix_mag"] = np.array(mix_mag, np.float32)
+    # the batch dict of prepare_data('once', ...); dict insertion
+    # order = ascending speaker index, as the reference's label order sorts it anyway
+    d["multi_spk_fea_list"] = [{SPK_NAMES[spk[b, k]]: d["targets"][b, k] for k in range(K)} for b in range(B)]
+    return d
+
+
+def prefixed_modules(mods):
+    """{prefix: module} -> [(name, shape)] in the build's naming."""
+    specs = []
+    for pre, m in mods.items():
+        for n, p in m.state_dict().items():
+            specs.append((f"{pre}.{n}", tuple(p.shape)))
+    return specs
+
+
+def load_weights(mods, w):
+    for pre, m in mods.items():
+        sd = {n: torch.from_numpy(w[f"{pre}.{n}"]) for n in m.state_dict()}
+        m.load_state_dict(sd)
+
+
+def record_params(out, mods, prefix, grads=False):
+    for pre, m in mods.items():
+        for n, p in m.named_parameters():
+            name = f"{pre}.{n}"
+            if grads:
+                if p.grad is None:
+                    continue
+                rr.pack(prefix, name, p.grad.detach().numpy(), out)
+            else:
+                rr.pack(prefix, name, p.detach().numpy(), out)
+
+
+def meta(out, **kw):
+    for k, v in kw.items():
+        out[f"meta/{k}"] = np.asarray(v)
+
+
+# ----------------------------------------------------------------------------- C2: EvalVer
+def make_c2(B=2, K=2, N=2048, seed=11, wseed=101):
+    rel = EVALVER
+    for n, t in [(587, "mix_speech_hidden,mix_tmp_hidden=mix_hidden_layer_3d("),
+                 (592, "mix_speech_output=mix_speech_classifier("),
+                 (604, "top_k_mask_mixspeech=top_k_mask(mix_speech_output,alpha=0.5,top_k=num_labels)"),
+                 (641, "loss_multi_speech=loss_multi_func(predict_multi_map,y_multi_map)"),
+                 (666, "loss_multi_speech=loss_multi_speech+0.5*loss_multi_sum_speech"),
+                 (675, "optimizer.step()")]:
+        check_line(rel, n, t)
+    d = synthetic_batch(B, K, N, seed)
+    T, F = d["mix_feas"].shape[1:]
+    config = make_config(BATCH_SIZE=B)
+    ns = base_namespace(config)
+    exec(module_defs(rel, ["ATTENTION", "MIX_SPEECH", "MIX_SPEECH_classifier", "SPEECH_EMBEDDING", "ADDJUST",
+                           "top_k_mask"]), ns)
+    exec(snippet_defs(LABELS, 287, 300, ["multi_label_vector"]), ns)
+    with cpu_cuda():
+        mix = ns["MIX_SPEECH"](F, T)
+        cls = ns["MIX_SPEECH_classifier"](F, T, NUM_LABELS)
+        emb = ns["SPEECH_EMBEDDING"](NUM_LABELS, 50, 2 + 3)
+        att = ns["ATTENTION"](50, "dot")
+        adj = ns["ADDJUST"](600, 50)
+    train_mods = {"mix": mix, "emb": emb, "adj": adj}
+    mods = dict(train_mods, cls=cls)
+    w = rr.weights(prefixed_modules(mods), hidden=300, seed=wseed, cls_hidden=600)
+    load_weights(mods, w)
+    # EvalVer.py:538-544 (the Discriminator's group is left out with its loss lines)
+    optimizer = torch.optim.Adam([{"params": mix.parameters()}, {"params": emb.parameters()},
+                                  {"params": cls.parameters()}, {"params": adj.parameters()},
+                                  {"params": att.parameters()}], lr=0.0002)
+    ns.update(mix_hidden_layer_3d=mix, mix_speech_classifier=cls, mix_speech_multiEmbedding=emb,
+              att_speech_layer=att, adjust_layer=adj, optimizer=optimizer, loss_multi_func=nn.MSELoss(),
+              dict_spk2idx=DICT_SPK2IDX, dict_idx2spk=DICT_IDX2SPK, num_labels=NUM_LABELS, mix_speech_len=T,
+              speech_fre=F, test_all_outputchannel=0,
+              train_data={"mix_feas": d["mix_feas"], "multi_spk_fea_list": d["multi_spk_fea_list"]})
+    # the classifier's own output (computed, then replaced by the ground truth at :599)
+    with torch.no_grad():
+        cls_out = cls(torch.from_numpy(d["mix_feas"])).numpy()
+    # forward .. loss (no Discriminator: 643-656, 670-671), then backward + Adam (673-675)
+    body = loop_body(rel, 582, [(587, 641), (658, 668), (673, 675)])
+    # keep the graph's intermediates: run the same statements, then read the namespace
+    with cpu_cuda():
+        exec(body, ns)
+    out = {}
+    meta(out, B=B, K=K, N=N, T=T, F=F, seed=seed, wseed=wseed, cell="lstm", layers=4, cls_hidden=600,
+         adjust=1, crm=0, source=f"{rel}:587-641,658-668,673-675")
+    for k in ("src", "gains", "spk", "mix_feas", "targets"):
+        out[f"in/{k}"] = d[k]
+    out["out/top_k_mask"] = ns["top_k_mask_mixspeech"].numpy()
+    out["out/top_k_idx"] = np.array([list(x) for x in ns["top_k_mask_idx"]], dtype=np.int64)
+    out["out/query"] = ns["mix_speech_multiEmbs"].detach().numpy()
+    out["out/h"] = ns["mix_tmp_hidden"].detach().numpy()
+    rr.pack("out", "V", ns["mix_speech_hidden"].detach().numpy(), out)
+    out["out/mask"] = ns["multi_mask"].detach().numpy()
+    out["out/pred"] = ns["predict_multi_map"].detach().numpy()
+    out["out/y_multi_map"] = ns["y_multi_map"].detach().numpy()
+    out["out/loss_mask"] = np.float64(ns["loss_multi_func"](ns["predict_multi_map"], ns["y_multi_map"]).item())
+    out["out/loss_sum"] = np.float64(ns["loss_multi_sum_speech"].item())
+    out["out/loss"] = np.float64(ns["loss_multi_speech"].item())
+    out["out/classifier"] = cls_out
+    record_params(out, train_mods, "grad", grads=True)
+    record_params(out, train_mods, "param")
+    assert all(p.grad is None for p in cls.parameters())  # the classifier receives no gradient
+    np.savez_compressed(os.path.join(HERE, "ref_c2_evalver.npz"), **out)
+    return out
+
+
+# ----------------------------------------------------------------------------- C1: main_run
+def make_c1(B=1, K=2, N=4000, seed=12, wseed=102):
+    rel = MAINRUN
+    for n, t in [(461, "mix_speech_hidden=mix_hidden_layer_3d("),
+                 (473, "top_k_mask_mixspeech=top_k_mask(mix_speech_output,alpha=0.5,top_k=num_labels)"),
+                 (489, "multi_mask=multi_mask*Variable(top_k_mask_mixspeech_multi).cuda()"),
+                 (506, "loss_multi_speech=loss_multi_func(predict_multi_map,y_multi_map)"),
+                 (522, "optimizer.step()")]:
+        check_line(rel, n, t)
+    d = synthetic_batch(B, K, N, seed)
+    T, F = d["mix_feas"].shape[1:]
+    config = make_config(BATCH_SIZE=B, NUM_LAYERS=2)
+    ns = base_namespace(config)
+    exec(module_defs(rel, ["ATTENTION", "MIX_SPEECH", "SPEECH_EMBEDDING", "top_k_mask"]), ns)
+    exec(snippet_defs("Torch_multi/test_multi_labels_speech.py", 285, 298, ["multi_label_vector"]), ns)
+    with cpu_cuda():
+        mix = ns["MIX_SPEECH"](F, T)
+        emb = ns["SPEECH_EMBEDDING"](NUM_LABELS, 50, 2 + 3)
+    train_mods = {"mix": mix, "emb": emb}
+    w = rr.weights(prefixed_modules(train_mods), hidden=300, seed=wseed)
+    load_weights(train_mods, w)
+    # main_run.py:434-443 (the classifier and the unused 'align' layers get no gradient)
+    optimizer = torch.optim.Adam([{"params": mix.parameters()}, {"params": emb.parameters()}], lr=0.0002)
+    # main_run.py:465 runs the classifier, whose output :470-471 replaces by the ground
+    # truth; :467 passes dict.keys() *lists* to multi_label_vector, which calls .keys()
+    # on them (an AttributeError in py2 too) -- the dicts themselves are passed here,
+    # as every other driver does (e.g. EvalVer.py:595)
+    ns.update(mix_hidden_layer_3d=mix, mix_speech_multiEmbedding=emb, optimizer=optimizer,
+              loss_multi_func=nn.MSELoss(), dict_spk2idx=DICT_SPK2IDX, dict_idx2spk=DICT_IDX2SPK,
+              num_labels=NUM_LABELS, mix_speech_len=T, speech_fre=F, batch_idx=1,
+              y_spk_list=d["multi_spk_fea_list"],
+              train_data={"mix_feas": d["mix_feas"], "multi_spk_fea_list": d["multi_spk_fea_list"]})
+    body = loop_body(rel, 455, [(461, 461), (468, 494), (499, 512), (520, 522)])
+    with cpu_cuda():
+        exec(body, ns)
+    out = {}
+    meta(out, B=B, K=K, N=N, T=T, F=F, seed=seed, wseed=wseed, cell="gru", layers=2, adjust=0, crm=0,
+         loss_channels=NUM_LABELS, source=f"{rel}:461,468-494,499-512,520-522")
+    for k in ("src", "gains", "spk", "mix_feas", "targets"):
+        out[f"in/{k}"] = d[k]
+    mm = ns["multi_mask"].detach().numpy()  # (B, 101, T, F), zero outside the active channels
+    pr = ns["predict_multi_map"].detach().numpy()
+    act = d["spk"]
+    out["out/top_k_mask"] = ns["top_k_mask_mixspeech"].numpy()
+    out["out/mask"] = np.stack([mm[b, act[b]] for b in range(B)])
+    out["out/pred"] = np.stack([pr[b, act[b]] for b in range(B)])
+    inactive = np.ones(NUM_LABELS, bool)
+    inactive[act.reshape(-1)] = False
+    out["out/inactive_max"] = np.float64(np.abs(mm[:, inactive]).max())
+    out["out/loss"] = np.float64(ns["loss_multi_speech"].item())
+    out["out/loss_sum_unused"] = np.float64(ns["loss_multi_sum_speech"].item())
+    record_params(out, train_mods, "grad", grads=True)
+    record_params(out, train_mods, "param")
+    np.savez_compressed(os.path.join(HERE, "ref_c1_mainrun.npz"), **out)
+    return out
+
+
+# ----------------------------------------------------------------------------- C3: cRM
+def make_c3(B=2, K=2, N=2048, seed=13, wseed=103):
+    rel = CRM
+    for n, t in [(645, "mix_speech_hidden,mix_tmp_hidden=mix_hidden_layer_3d("),
+                 (688, "att_multi_speech=-1/cRM_C*torch.log((cRM_k-att_multi_speech)/(cRM_k+att_multi_speech))"),
+                 (743, "loss_multi_speech=loss_multi_speech_fake+loss_multi_speech_real"),
+                 (752, "optimizer.step()")]:
+        check_line(rel, n, t)
+    d = synthetic_batch(B, K, N, seed, crm=True)
+    T, F = d["mix_feas"].shape[1:]
+    config = make_config(BATCH_SIZE=B, NUM_LAYERS=2, is_ComlexMask=True, is_SelfTune=True)
+    ns = base_namespace(config)
+    exec(module_defs(rel, ["ATTENTION", "MIX_SPEECH", "SPEECH_EMBEDDING", "ADDJUST", "top_k_mask"],
+                     consts=("cRM_k", "cRM_C")), ns)
+    exec(snippet_defs(LABELS, 287, 300, ["multi_label_vector"]), ns)
+    with cpu_cuda():
+        mix = ns["MIX_SPEECH"](F, T)
+        emb = ns["SPEECH_EMBEDDING"](NUM_LABELS, 50, 2 + 3)
+        att = ns["ATTENTION"](50, "dot")
+        adj = ns["ADDJUST"](600, 50)
+    train_mods = {"mix": mix, "emb": emb, "adj": adj}
+    w = rr.weights(prefixed_modules(train_mods), hidden=300, seed=wseed)
+    # small query scale: keeps every cRM logit well inside the inverse compression's
+    # finite range (|e| < 9.02) for this fixture
+    w["emb.layer.weight"] *= np.float32(0.1)
+    load_weights(train_mods, w)
+    optimizer = torch.optim.Adam([{"params": mix.parameters()}, {"params": emb.parameters()},
+                                  {"params": adj.parameters()}, {"params": att.parameters()}], lr=0.0002)
+    y_spk_gt = [[DICT_SPK2IDX[s] for s in smp] for smp in d["multi_spk_fea_list"]]
+    y_map = np.zeros((B, NUM_LABELS), np.float32)
+    for b, l in enumerate(y_spk_gt):
+        y_map[b, l] = 1
+    ns.update(mix_hidden_layer_3d=mix, mix_speech_multiEmbedding=emb, att_speech_layer=att, adjust_layer=adj,
+              optimizer=optimizer, loss_multi_func=nn.MSELoss(), dict_spk2idx=DICT_SPK2IDX,
+              dict_idx2spk=DICT_IDX2SPK, num_labels=NUM_LABELS, mix_speech_len=T, speech_fre=F,
+              test_all_outputchannel=0,
+              train_data={"mix_feas": d["mix_feas"], "mix_mag": d["mix_mag"],
+                          "multi_spk_fea_list": d["multi_spk_fea_list"]})
+    # :650 (classifier forward) is left out: its output is replaced by the ground truth (:656-657)
+    body = loop_body(rel, 639, [(645, 645), (653, 681), (684, 752)])
+    with cpu_cuda():
+        exec(body, ns)
+    out = {}
+    meta(out, B=B, K=K, N=N, T=T, F=F, seed=seed, wseed=wseed, cell="gru", layers=2, adjust=1, crm=1,
+         emb_scale=0.1, source=f"{rel}:645,653-681,684-752")
+    for k in ("src", "gains", "spk", "mix_feas", "targets", "mix_mag"):
+        out[f"in/{k}"] = d[k]
+    out["out/query"] = ns["mix_speech_multiEmbs"].detach().numpy().reshape(B, K, -1)
+    out["out/h"] = ns["mix_tmp_hidden"].detach().numpy()
+    out["out/mask"] = ns["multi_mask"].detach().numpy()
+    out["out/pred"] = np.stack([ns["predict_map_real"].detach().numpy(), ns["predict_map_fake"].detach().numpy()], -1)
+    out["out/loss_real"] = np.float64(ns["loss_multi_speech_real"].item())
+    out["out/loss_imag"] = np.float64(ns["loss_multi_speech_fake"].item())
+    out["out/loss"] = np.float64(ns["loss_multi_speech"].item())
+    assert np.isfinite(out["out/loss"])
+    record_params(out, train_mods, "grad", grads=True)
+    record_params(out, train_mods, "param")
+    np.savez_compressed(os.path.join(HERE, "ref_c3_crm.npz"), **out)
+    return out
+
+
+# ----------------------------------------------------------------------------- C4: 3-spk
+def make_c4(B=2, K=3, N=2048, seed=14, wseed=104):
+    rel = SELFSS
+    for n, t in [(457, "mix_speech_hidden=mix_hidden_layer_3d("),
+                 (513, "loss_multi_speech=loss_multi_func(predict_multi_map,y_multi_map)"),
+                 (521, "loss_multi_speech=loss_multi_speech+0.5*loss_multi_sum_speech"),
+                 (532, "optimizer.step()")]:
+        check_line(rel, n, t)
+    d = synthetic_batch(B, K, N, seed)
+    T, F = d["mix_feas"].shape[1:]
+    config = make_config(BATCH_SIZE=B, NUM_LAYERS=2)
+    ns = base_namespace(config)
+    exec(module_defs(rel, ["ATTENTION", "MIX_SPEECH", "SPEECH_EMBEDDING", "top_k_mask"]), ns)
+    exec(snippet_defs("Torch_multi/test_multi_labels_speech.py", 285, 298, ["multi_label_vector"]), ns)
+    with cpu_cuda():
+        mix = ns["MIX_SPEECH"](F, T)
+        emb = ns["SPEECH_EMBEDDING"](NUM_LABELS, 50, 3 + 3)
+    train_mods = {"mix": mix, "emb": emb}
+    w = rr.weights(prefixed_modules(train_mods), hidden=300, seed=wseed)
+    load_weights(train_mods, w)
+    optimizer = torch.optim.Adam([{"params": mix.parameters()}, {"params": emb.parameters()}], lr=0.0002)
+    ns.update(mix_hidden_layer_3d=mix, mix_speech_multiEmbedding=emb, optimizer=optimizer,
+              loss_multi_func=nn.MSELoss(), dict_spk2idx=DICT_SPK2IDX, dict_idx2spk=DICT_IDX2SPK,
+              num_labels=NUM_LABELS, mix_speech_len=T, speech_fre=F, batch_idx=1, test_all_outputchannel=0,
+              train_data={"mix_feas": d["mix_feas"], "multi_spk_fea_list": d["multi_spk_fea_list"]})
+    # :461 classifier forward left out (replaced by the ground truth at :467-468); :525-527
+    # (bss_eval / SDR on wavs) left out
+    body = loop_body(rel, 450, [(457, 457), (464, 499), (504, 521), (530, 532)])
+    with cpu_cuda():
+        exec(body, ns)
+    out = {}
+    meta(out, B=B, K=K, N=N, T=T, F=F, seed=seed, wseed=wseed, cell="gru", layers=2, adjust=0, crm=0,
+         source=f"{rel}:457,464-499,504-521,530-532")
+    for k in ("src", "gains", "spk", "mix_feas", "targets"):
+        out[f"in/{k}"] = d[k]
+    out["out/mask"] = ns["multi_mask"].detach().numpy()
+    out["out/pred"] = ns["predict_multi_map"].detach().numpy()
+    out["out/loss_mask"] = np.float64(ns["loss_multi_func"](ns["predict_multi_map"], ns["y_multi_map"]).item())
+    out["out/loss_sum"] = np.float64(ns["loss_multi_sum_speech"].item())
+    out["out/loss"] = np.float64(ns["loss_multi_speech"].item())
+    record_params(out, train_mods, "grad", grads=True)
+    record_params(out, train_mods, "param")
+    np.savez_compressed(os.path.join(HERE, "ref_c4_3spk.npz"), **out)
+    return out
+
+
+# ----------------------------------------------------------------------------- small pieces
+class _FakeOpt:
+    def __init__(self, lr):
+        self.param_groups = [{"lr": lr}]
+
+
+def make_small(seed=15):
+    out = {}
+    ns = base_namespace(make_config(BATCH_SIZE=8))
+    exec(module_defs(EVALVER, ["top_k_mask"]), ns)
+    tkm = ns["top_k_mask"]
+    ns_g = base_namespace(make_config(BATCH_SIZE=1))
+    exec(module_defs(GRID, ["top_k_mask"]), ns_g)
+    tkm_g = ns_g["top_k_mask"]
+    r = np.random.Generator(np.random.PCG64(seed))
+    cases = []
+    P = r.uniform(size=(8, NUM_LABELS)).astype(np.float32)
+    P[3, 10] = P[3, 20] = P[3, 30] = np.float32(0.9)  # ties at the top
+    P[4] = 0.25  # nothing above 0.5
+    P[5, :] = r.uniform(0, 0.4, size=NUM_LABELS)
+    P[5, [7, 70]] = np.float32(0.8)  # exactly two above 0.5
+    cases += [(P, 0.5, NUM_LABELS), (P, -0.5, 2), (P, -0.3, 3), (P, 0.5, 3), (P, 0.95, NUM_LABELS)]
+    G = np.zeros((4, NUM_LABELS), np.float32)  # multi-hot ground truth rows (training use)
+    for i, ids in enumerate([[1, 2], [0, 100], [50, 51], [3, 99]]):
+        G[i, ids] = 1
+    cases.append((G, 0.5, NUM_LABELS))
+    for i, (p, a, k) in enumerate(cases):
+        out[f"topk/{i}/in"] = p
+        out[f"topk/{i}/alpha"] = np.float64(a)
+        out[f"topk/{i}/top_k"] = np.int64(k)
+        out[f"topk/{i}/out"] = tkm(torch.from_numpy(p), a, k).numpy()
+    # the GRID variant also returns the sorted top-k indices (recursive extraction, B=1)
+    for i, (p, a, k) in enumerate([(P[:1], -0.3, 3), (P[4:5], 0.5, 3), (P[3:4], 0.5, 3)]):
+        fin, idx = tkm_g(torch.from_numpy(p), a, k)
+        out[f"topk_grid/{i}/in"] = p
+        out[f"topk_grid/{i}/alpha"] = np.float64(a)
+        out[f"topk_grid/{i}/top_k"] = np.int64(k)
+        out[f"topk_grid/{i}/out"] = fin.numpy()
+        out[f"topk_grid/{i}/idx"] = np.array(idx, dtype=np.int64).reshape(len(idx), -1)
+    # multi_label_vector
+    ns_l = base_namespace(None)
+    exec(snippet_defs(LABELS, 287, 300, ["multi_label_vector"]), ns_l)
+    samples = [{SPK_NAMES[3]: 0, SPK_NAMES[1]: 0}, {SPK_NAMES[100]: 0, SPK_NAMES[0]: 0, SPK_NAMES[7]: 0}]
+    y_spk, y_map = ns_l["multi_label_vector"](samples, DICT_SPK2IDX)
+    out["mlv/names"] = np.array([",".join(s) for s in samples])
+    out["mlv/y_spk"] = np.array([",".join(str(i) for i in l) for l in y_spk])
+    out["mlv/y_map"] = y_map
+    # LR schedules: EvalVer.py:571-575 (halve every 10 epochs while lr >= 1e-7) and
+    # selfSS_dB.py:442-444 (halve every 50 epochs, no floor)
+    for tag, rel, ln, ep in (("evalver", EVALVER, 570, 400), ("selfss_db", SELFSS, 441, 400)):
+        tree = ast.parse(translated(rel), rel)
+        loop = [n for n in ast.walk(tree) if isinstance(n, ast.For) and n.lineno == ln][0]
+        stmt = loop.body[0]
+        assert isinstance(stmt, ast.If), (rel, ln)
+        code = compile(ast.Module(body=[stmt], type_ignores=[]), rel, "exec")
+        opt = _FakeOpt(0.0002)
+        lrs = []
+        ns_s = dict(optimizer=opt, lrs=types.SimpleNamespace(send=lambda *a, **k: None))
+        for e in range(ep):
+            ns_s["epoch_idx"] = e
+            exec(code, ns_s)
+            lrs.append(opt.param_groups[0]["lr"])
+        out[f"lr/{tag}"] = np.array(lrs, np.float64)
+    np.savez_compressed(os.path.join(HERE, "ref_small.npz"), **out)
+    return out
+
+
+def main():
+    torch.manual_seed(1)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    which = sys.argv[1:] or ["small", "c2", "c1", "c3", "c4"]
+    fns = dict(small=make_small, c2=make_c2, c1=make_c1, c3=make_c3, c4=make_c4)
+    for w in which:
+        sink = io.StringIO()
+        with contextlib.redirect_stdout(sink):
+            o = fns[w]()
+        print(w, "ok", {k: (v.shape if hasattr(v, "shape") else v) for k, v in o.items() if k.startswith("out/loss")})
+
+
+if __name__ == "__main__":
+    main()

@@ -245,3 +245,56 @@ def test_step_bitwise_reproducible(dev, precision, mode):
     assert torch.equal(l0, l1)
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_step_c2_full_size_pit_indices(dev, precision):
+    """The benchmark's configuration (C2: BiLSTM-4L, B = 32, N = 32000, 2-spk PIT) in both the
+    fp32 parity mode and the benched bf16 mode: the permutation indices the HIP step selects
+    (dl4ss_pit_select) equal the oracle's om.pit_assign bit-exactly for every utterance whose
+    two assignment costs are not tied within the mode's arithmetic error (relative cost margin
+    > 1e-4 fp32 / 5e-4 bf16: every utterance of this batch, whose smallest margin is 9.1e-4;
+    13 of the 32 choose the swapped assignment), and the masked magnitude spectrogram is within
+    the north-star bar, 1e-3 rel-L2, in BOTH modes (measured: fp32 1.5e-7, bf16 3.2e-4).
+    Achieved values are written to $DL4SS_PARITY_OUT (json) when set."""
+    import itertools
+    import json
+    import os
+
+    B, K, N = 32, 2, 32000
+    net, tr, src, spk, gains, ref = _setup(dev, "lstm", 4, B, K, N, "pit", precision=precision)
+    feats, X, Y = _oracle_features(src, gains, False)
+    with torch.no_grad():
+        mask, V, h, q = ref(feats, torch.from_numpy(spk))
+    perm_ref, _ = om.pit_assign(mask, X, Y)
+    pred_ref = (mask * X[:, None]).double()
+    C = ((pred_ref[:, :, None] - Y.double()[:, None, :]) ** 2).sum(dim=(-1, -2))  # (B, k, j)
+    perms = list(itertools.permutations(range(K)))
+    costs = torch.stack([sum(C[:, k, p[k]] for k in range(K)) for p in perms], dim=1)
+    srt = torch.sort(costs, dim=1).values
+    margin = ((srt[:, 1] - srt[:, 0]) / srt[:, 0]).numpy()
+    tr.spk.copy_(torch.from_numpy(spk.astype(np.int32)).to(dev))
+    tr.features(torch.from_numpy(src.astype(np.float32)).to(dev), torch.from_numpy(gains.astype(np.float32)).to(dev))
+    tr.forward()
+    pred = torch.empty(B, K, tr.T * tr.F, device=dev)
+    tr.attn(0, pred_out=pred)
+    tr.loss_and_grad()
+    tr.check()
+    perm = tr.perm.cpu().long()
+    pred = pred.cpu().view(B, K, tr.T, tr.F)
+    # masked magnitude under the chosen assignment: channel k of utterance b vs the oracle's
+    rel = float((pred - pred_ref.float()).norm() / pred_ref.float().norm())
+    tie = 1e-4 if precision == "fp32" else 5e-4
+    decided = margin > tie
+    agree = (perm == perm_ref).all(dim=1).numpy()
+    rec = {"precision": precision, "masked_magnitude_rel_l2": rel, "perm_agree": int(agree.sum()), "B": B,
+           "decided": int(decided.sum()), "agree_on_decided": int(agree[decided].sum()),
+           "min_margin": float(margin.min()), "median_margin": float(np.median(margin)),
+           "n_swapped_ref": int((perm_ref[:, 0] == 1).sum())}
+    out = os.environ.get("DL4SS_PARITY_OUT")
+    if out:
+        with open(out.replace(".json", f"_{precision}.json"), "w") as f:
+            json.dump(rec, f)
+    print(json.dumps(rec))
+    assert decided.all() and agree.all(), rec
+    assert rel < 1e-3, rec
