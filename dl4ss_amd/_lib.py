@@ -60,10 +60,13 @@ SIGNATURES = {
     "dl4ss_mask_attn_loss_bf16v": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
     "dl4ss_gemm_bf16_lt": [I, I, I, I, I, P, LL, P, LL, P, LL, F, I, LL, LL, LL, P, LL, P],
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
+    "dl4ss_adam_guarded": [P, P, P, P, LL, F, F, F, F, I, P, P, P],
+    "dl4ss_birnn_plan_info": [I, I, I, I, I, P],
+    "dl4ss_debug_set_spin_limit": [ctypes.c_uint],
 }
 # entry points that return a value rather than a hipError_t
 RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
-            "dl4ss_attn_dot_nblk": ctypes.c_int}
+            "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None}
 
 _lib = None
 

@@ -10,8 +10,11 @@ the module's own: ``layer.weight_ih_l0[_reverse]`` / ``Linear.weight`` (MIX_SPEE
 ``layer.weight`` (embedding, ADDJUST), ``Linear_{1,2,3}.weight`` (attention).
 
 Files are read with ``torch.load(..., weights_only=True)`` only (no arbitrary unpickling):
-torch-0.3 era files in the legacy (non-zip) format load through the same safe path; a file
-the safe loader refuses raises.  The flat parameter buffers of ``SepNet`` /
+torch-0.3 / Python-2 files in the legacy (non-zip) format -- protocol-2 pickles of an
+``OrderedDict`` of ``torch._utils._rebuild_tensor`` tensors over ``torch.cuda.FloatStorage``
+persistent ids saved on ``cuda:N`` (fixture: ``tests/golden/legacy_py2_torch03``, built
+opcode by opcode by ``tests/golden/make_legacy_ckpt.py``) -- load through the same safe
+path; a file the safe loader refuses raises.  The flat parameter buffers of ``SepNet`` /
 ``ClassifierNet`` carry the same names under a module prefix (``mix.``, ``emb.``, ``adj.``),
 so loading is a rename and a copy; ``save_reference_params`` writes the reference layout
 back (one file per module, legacy-compatible keys).
@@ -32,11 +35,19 @@ def load_state(path):
 
 def load_reference_params(net, hidden3d=None, emblayer=None, adjlayer=None, strict=True):
     """Load the reference's per-module files into a SepNet (in place).  Missing module files
-    are skipped; with ``strict`` every key of a given file must map onto the net."""
+    are skipped; with ``strict`` every key of a given file must map onto the net AND every
+    parameter of the net under that file's module prefix must be in the file (torch's
+    ``load_state_dict(strict=True)`` in both directions: a 2-layer hidden3d file does not
+    silently leave layers 2-3 of a 4-layer net at their random init)."""
     for kind, path in (("hidden3d", hidden3d), ("emblayer", emblayer), ("adjlayer", adjlayer)):
         if path is None:
             continue
         sd = load_state(path)
+        if strict:
+            want = {name[len(PREFIX[kind]):] for name, _ in net.specs if name.startswith(PREFIX[kind])}
+            missing = sorted(want - set(sd))
+            if missing:
+                raise KeyError(f"{path}: missing {missing} for this net")
         for k, v in sd.items():
             name = PREFIX[kind] + k
             if name not in net.offsets:
@@ -53,12 +64,19 @@ def load_reference_params(net, hidden3d=None, emblayer=None, adjlayer=None, stri
 def load_reference_classifier(cnet, path, strict=True):
     """MIX_SPEECH_classifier file into a ClassifierNet (the ``cnn`` keys dropped, EvalVer.py:547-549)."""
     sd = {k: v for k, v in load_state(path).items() if "cnn" not in k}
+    if strict:
+        missing = sorted({name for name, _ in cnet.specs} - set(sd))
+        if missing:
+            raise KeyError(f"{path}: missing {missing} for this classifier")
     for k, v in sd.items():
         if k not in cnet.offsets:
             if strict:
                 raise KeyError(f"{path}: key {k!r} has no counterpart in the classifier")
             continue
-        cnet.view(k).copy_(v.to(torch.float32))
+        dst = cnet.view(k)
+        if tuple(dst.shape) != tuple(v.shape):
+            raise ValueError(f"{path}: {k} has shape {tuple(v.shape)}, the classifier expects {tuple(dst.shape)}")
+        dst.copy_(v.to(torch.float32))
     return cnet
 
 

@@ -30,8 +30,14 @@
 // stores (granules first, then prefetch loads for the next step, then the
 // saved activations); waves 4-7 only poll granules into LDS.  All 8 waves run
 // the register-resident matvec (two waves per SIMD keep the VALU issuing).
-// Co-residency: grid <= 240 workgroups.
+// The packed bf16 kernels (rnn_fwd_pk_kernel / rnn_bwd_pk_kernel, below) split the roles
+// differently: waves 0-3 cell + stores, FWD_NPW / BWD_NPW polling waves from wave 4 (the
+// forward's second one is wave 7), the rest MFMA tiles + prefetch (see their comments).
+// Co-residency: every workgroup of a launch must be resident at once; the plan keeps the
+// grid within the device's CUs minus 1/16 (240 on a full MI355X, wg_limit) and every launch
+// re-checks it against CUs x occupancy (launch_resident).
 #include <cstdlib>
+#include <mutex>
 #include "common.h"
 
 namespace {
@@ -146,6 +152,7 @@ struct RnnArgs {
   float* dGh;            // bwd GRU: grad wrt W_hh h + b_hh (LSTM: == dG, may be null)
   u64* xbuf;             // granules
   int* status;
+  unsigned spin_limit;   // polls before a hand-off times out (SPIN_LIMIT; dl4ss_debug_set_spin_limit)
   u64* stamps;           // diagnostic build only
   // bf16 mode extras (packed kernels only; any may be null)
   unsigned short* outb;    // fwd (B,T,2H) bf16(h)          -- next layer's / Linear's GEMM operand
@@ -197,7 +204,8 @@ struct StepLoader {
 // returns false on timeout.  Offsets are computed once per launch by the caller;
 // all loads of the thread are in flight at once and only stale ones are re-issued.
 template <int GM>
-__device__ __forceinline__ bool gather(const u64* src, const int (&off)[GM], unsigned tag, u64 (&v)[GM]) {
+__device__ __forceinline__ bool gather(const u64* src, const int (&off)[GM], unsigned tag, u64 (&v)[GM],
+                                       unsigned limit) {
   const u64 done = (u64)tag << 32;
 #pragma unroll
   for (int g = 0; g < GM; ++g) v[g] = off[g] >= 0 ? get_granule(src + off[g]) : done;
@@ -207,7 +215,7 @@ __device__ __forceinline__ bool gather(const u64* src, const int (&off)[GM], uns
 #pragma unroll
     for (int g = 0; g < GM; ++g) ok &= (unsigned)(v[g] >> 32) == tag;
     if (ok) return true;
-    if (++spins > SPIN_LIMIT) return false;
+    if (++spins > limit) return false;
     __builtin_amdgcn_s_sleep(1);
 #pragma unroll
     for (int g = 0; g < GM; ++g)
@@ -365,7 +373,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
       // ---- gather h_{s-1} (granules, tag s) and commit this step's inputs
       if (s > 0) {
         u64 v[GM];
-        if (!gather<GM>(xg + (long long)((s - 1) & 1) * BC * H, goff, (unsigned)s, v)) {
+        if (!gather<GM>(xg + (long long)((s - 1) & 1) * BC * H, goff, (unsigned)s, v, a.spin_limit)) {
           atomicOr(a.status, 1);
           return;
         }
@@ -475,9 +483,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 //    MI355X_MICROARCH.md, Valid forms R2), and a consumer that has not completed a
 //    poll of the fast copy after FAST_SPINS sweeps switches to the safe copy for the
 //    rest of the launch.  Every value is validated by its own tag either way.
-// Waves: 0-3 MFMA tiles 0-3 + cell update + publish + saved-state stores;
-//        4 poll;  5-7 MFMA tiles 4-6 + per-step input prefetch.
-// Each MFMA tile runs two independent accumulator chains (even / odd k-steps).
+// Waves (FWD_NPW polling waves, default 2): 0-3 MFMA tiles 0-3 + cell update + publish +
+//        saved-state stores; 4 polls, and 7 (FWD_NPW >= 2) and 6 (FWD_NPW == 3) poll too
+//        (those waves hold no MFMA tile); the remaining waves of 5-7 run MFMA tiles 4..MT-1
+//        and the per-step input prefetch.
+// Each MFMA tile runs FWD_MV_CHAINS independent accumulator chains over its k-steps.
 // --------------------------------------------------------------------------
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int PKU = 24;     // staged h slots per (row, producer): 8 granules x 3
@@ -491,6 +501,9 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef FWD_NPW
 #define FWD_NPW 2  // forward polling waves: 4, and 7 when >= 2, and 6 when 3 (their MFMA tile indices must be >= MT)
 #endif
+static_assert(FWD_MV_CHAINS >= 1 && FWD_MV_CHAINS <= 8, "FWD_MV_CHAINS: 1..KSMAX accumulator chains");
+static_assert(FWD_NPW >= 1 && FWD_NPW <= 3, "FWD_NPW: 1..3 polling waves");
+static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
 constexpr unsigned FAST_SPINS = 256;  // sweeps of the fast copy before the safe copy is polled
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
@@ -673,7 +686,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
-          if (++spins > SPIN_LIMIT) {
+          if (++spins > a.spin_limit) {
             atomicOr(a.status, 1);
             return;
           }
@@ -1004,7 +1017,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
       //      step's operands (issued during the previous step)
       if (s > 0) {
         u64 v[GM];
-        if (!gather<GM>(xg + (long long)((s - 1) & 1) * NG * BC * H, goff, (unsigned)s, v)) {
+        if (!gather<GM>(xg + (long long)((s - 1) & 1) * NG * BC * H, goff, (unsigned)s, v, a.spin_limit)) {
           atomicOr(a.status, 2);
           return;
         }
@@ -1303,7 +1316,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
-          if (++spins > SPIN_LIMIT) {
+          if (++spins > a.spin_limit) {
             atomicOr(a.status, 2);
             return;
           }
@@ -1540,6 +1553,43 @@ void bwd_dims(int rpl, int kgl, int& rpln, int& kgln) {
   }
 }
 
+// CUs of the current device (cached per device id); 0 when no device is visible
+int device_cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cache[dev] == 0) {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cache[dev] = cu;
+  }
+  return cache[dev];
+}
+
+// Launch-time guard of the co-residency assumption: the grid must not exceed the CUs times
+// the kernel's occupancy at this LDS size (a persistent launch whose workgroups cannot all
+// be resident would spin to the hand-off timeout on every step).
+template <typename K>
+bool fits_resident(K kernel, int grid, size_t smem) {
+  struct Entry { const void* k; size_t smem; int dev; int occ; };
+  static std::mutex mu;
+  static Entry cache[64];
+  static int n = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const void* kp = reinterpret_cast<const void*>(kernel);
+  std::lock_guard<std::mutex> lk(mu);
+  int occ = -1;
+  for (int i = 0; i < n; ++i)
+    if (cache[i].k == kp && cache[i].smem == smem && cache[i].dev == dev) occ = cache[i].occ;
+  if (occ < 0) {
+    occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, NT, smem) != hipSuccess) occ = 0;
+    if (n < 64) cache[n++] = Entry{kp, smem, dev, occ};
+  }
+  return grid <= occ * device_cu_count();
+}
+
 struct Plan {
   int BC, NG, J, nchunk;
   int KP, KPL, HP, RP, RPL, KG, KGL;
@@ -1554,8 +1604,20 @@ struct Plan {
 
 // mf: plan for the bf16 MFMA matvec (the fp32 VALU forward's per-thread weight limit
 // KPL <= WMAX does not apply).  H > HMAX is the forward-only large-H plan (HM = HMAX_L).
-bool make_plan(int cell, int B, int H, Plan& p, bool mf = true) {
+// Co-residency budget of one persistent launch (both directions, all batch chunks): every
+// workgroup must be resident at once, so the plan keeps 2 * nchunk * NG within the device's
+// CU count minus 1/16 of it (240 of 256 on a full MI355X; 30 on a 32-CU CPX partition),
+// leaving room for concurrent kernels (RCCL).  DL4SS_RNN_MAX_WG overrides it (experiments).
+int wg_limit() {
+  static const int env = std::getenv("DL4SS_RNN_MAX_WG") ? std::atoi(std::getenv("DL4SS_RNN_MAX_WG")) : 0;
+  if (env > 0) return env;
+  const int cu = device_cu_count();
+  return cu > 0 ? cu - cu / 16 : 240;
+}
+
+bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) {
   if (H > HMAX_L) return false;
+  if (max_wg <= 0) max_wg = wg_limit();
   p.big = H > HMAX;
   const int ngate = cell == CELL_LSTM ? 4 : 3;
   for (int J = 20; J >= 4; --J) {
@@ -1582,7 +1644,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true) {
     for (int bc : {1, 2, 4, 8}) {
       if (bc < min_bc) continue;
       const int nchunk = (B + bc - 1) / bc;
-      if (2 * nchunk * NG <= 240 && bc * J <= NROLE) {
+      if (2 * nchunk * NG <= max_wg && bc * J <= NROLE) {
         BC = bc;
         break;
       }
@@ -1607,52 +1669,62 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true) {
   return false;
 }
 
+// every persistent recurrence launch goes through the co-residency guard
+template <typename K>
+int launch_resident(K kernel, int grid, size_t smem, hipStream_t st, const RnnArgs& a) {
+  if (!fits_resident(kernel, grid, smem)) return (int)hipErrorCooperativeLaunchTooLarge;
+  RnnArgs arg = a;
+  void* args[] = {&arg};
+  return (int)hipLaunchKernel(reinterpret_cast<const void*>(kernel), dim3(grid), dim3(NT), args, smem, st);
+}
+
 template <int CELL, int BC>
-void launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
+int launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
   if (a.H > HMAX) {  // forward-only large-H instantiations (the H = 600 classifier)
     if (mf)
-      hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, true, HMAX_L>), dim3(grid), dim3(NT), smem, st, a);
+      return launch_resident(rnn_fwd_kernel<CELL, BC, 0, true, HMAX_L>, grid, smem, st, a);
     else
-      hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, false, HMAX_L>), dim3(grid), dim3(NT), smem, st, a);
-    return;
+      return launch_resident(rnn_fwd_kernel<CELL, BC, 0, false, HMAX_L>, grid, smem, st, a);
   }
   // compile-time k-slice lengths for the shipped H = 300 plans (LSTM J=20: 52, GRU J=20: 40)
   if (mf && pk)
-    hipLaunchKernelGGL((rnn_fwd_pk_kernel<CELL, BC>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_fwd_pk_kernel<CELL, BC>, grid, smem, st, a);
   else if (mf)
-    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, true>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_fwd_kernel<CELL, BC, 0, true>, grid, smem, st, a);
   else if (a.KPL == 52)
-    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 52, false>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_fwd_kernel<CELL, BC, 52, false>, grid, smem, st, a);
   else if (a.KPL == 40)
-    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 40, false>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_fwd_kernel<CELL, BC, 40, false>, grid, smem, st, a);
   else
-    hipLaunchKernelGGL((rnn_fwd_kernel<CELL, BC, 0, false>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_fwd_kernel<CELL, BC, 0, false>, grid, smem, st, a);
 }
 template <int CELL, int BC>
-void launch_bwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
+int launch_bwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
   int rpln, kgln;
   bwd_dims(a.RPL, a.KGL, rpln, kgln);
   if (mf && pk)
-    hipLaunchKernelGGL((rnn_bwd_pk_kernel<CELL, BC>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_bwd_pk_kernel<CELL, BC>, grid, smem, st, a);
   else if (mf)
-    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 0, 0, true>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_bwd_kernel<CELL, BC, 0, 0, true>, grid, smem, st, a);
   else if (rpln == 20 && kgln == 3)
-    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 20, 3, false>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_bwd_kernel<CELL, BC, 20, 3, false>, grid, smem, st, a);
   else if (rpln == 20 && kgln == 2)
-    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 20, 2, false>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_bwd_kernel<CELL, BC, 20, 2, false>, grid, smem, st, a);
   else
-    hipLaunchKernelGGL((rnn_bwd_kernel<CELL, BC, 0, 0, false>), dim3(grid), dim3(NT), smem, st, a);
+    return launch_resident(rnn_bwd_kernel<CELL, BC, 0, 0, false>, grid, smem, st, a);
 }
 
 template <int CELL>
 int dispatch(bool fwd, bool mf, bool pk, int BC, const RnnArgs& a, int grid, size_t smem, hipStream_t st) {
+  int e;
   switch (BC) {
-    case 1: fwd ? launch_fwd<CELL, 1>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 1>(a, mf, pk, grid, smem, st); break;
-    case 2: fwd ? launch_fwd<CELL, 2>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 2>(a, mf, pk, grid, smem, st); break;
-    case 4: fwd ? launch_fwd<CELL, 4>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 4>(a, mf, pk, grid, smem, st); break;
-    case 8: fwd ? launch_fwd<CELL, 8>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 8>(a, mf, pk, grid, smem, st); break;
+    case 1: e = fwd ? launch_fwd<CELL, 1>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 1>(a, mf, pk, grid, smem, st); break;
+    case 2: e = fwd ? launch_fwd<CELL, 2>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 2>(a, mf, pk, grid, smem, st); break;
+    case 4: e = fwd ? launch_fwd<CELL, 4>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 4>(a, mf, pk, grid, smem, st); break;
+    case 8: e = fwd ? launch_fwd<CELL, 8>(a, mf, pk, grid, smem, st) : launch_bwd<CELL, 8>(a, mf, pk, grid, smem, st); break;
     default: return (int)hipErrorInvalidValue;
   }
+  if (e) return e;
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
@@ -1661,7 +1733,10 @@ int dispatch(bool fwd, bool mf, bool pk, int BC, const RnnArgs& a, int grid, siz
 u64* g_stamps = nullptr;
 #endif
 
+unsigned g_spin_limit = SPIN_LIMIT;  // dl4ss_debug_set_spin_limit (tests force a hand-off timeout)
+
 void fill_args(RnnArgs& a, const Plan& p, int B, int T, int H) {
+  a.spin_limit = g_spin_limit;
 #if defined(RNN_STAMPS) || defined(RNN_TRACE)
   a.stamps = g_stamps;
 #endif
@@ -1714,6 +1789,22 @@ static long long handoff_bytes(const Plan& p, int H) {
   if (bwd_pk > bwd) bwd = bwd_pk;
   const long long n = fwd > bwd ? fwd : bwd;
   return (n + 255) / 256 * 256;
+}
+
+// Polls a hand-off may spin before it times out (sets *status and the polling wave exits;
+// the launch still completes).  0 restores the default (SPIN_LIMIT, ~1 s).  Test hook: a
+// tiny limit forces the timeout path that the Adam guard (dl4ss_adam_guarded) must catch.
+DL4SS_API void dl4ss_debug_set_spin_limit(unsigned limit) { g_spin_limit = limit ? limit : SPIN_LIMIT; }
+
+// The recurrence plan for (cell, B, H) under a co-residency budget of max_wg workgroups
+// (<= 0: the current device's, see wg_limit): info = {BC, NG, J, nchunk, grid}.  Host-only
+// (no device call when max_wg > 0).  Returns 0, or hipErrorInvalidValue when no plan fits.
+DL4SS_API int dl4ss_birnn_plan_info(int cell, int B, int H, int precision, int max_wg, int* info) {
+  DL4SS_REQUIRE(info && (cell == CELL_LSTM || cell == CELL_GRU) && B > 0 && H > 0);
+  Plan p;
+  if (!make_plan(cell, B, H, p, precision == 1, max_wg)) return (int)hipErrorInvalidValue;
+  info[0] = p.BC; info[1] = p.NG; info[2] = p.J; info[3] = p.nchunk; info[4] = 2 * p.nchunk * p.NG;
+  return 0;
 }
 
 // the larger of the fp32 and bf16 plans' needs (either precision may use the buffer);

@@ -191,7 +191,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ A
 // (EvalVer.py:538-544,673-675: Adam(lr=2e-4), betas (0.9, 0.999), eps 1e-8)
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
-                                                   float lr, float b1, float b2, float eps, float bc1, float bc2s) {
+                                                   float lr, float b1, float b2, float eps, float bc1, float bc2s,
+                                                   const int* __restrict__ status, float* __restrict__ loss) {
+  if (status && *status) {  // a recurrence hand-off of this step timed out: refuse the update
+    if (loss && blockIdx.x == 0 && threadIdx.x == 0) loss[0] = __builtin_nanf("");
+    return;
+  }
   const float step = lr / bc1;
   for (long long i = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * 4; i < n;
        i += (long long)gridDim.x * blockDim.x * 4) {
@@ -277,8 +282,16 @@ DL4SS_API int dl4ss_colsum(const float* A, long long lda, int M, int N, float* o
   return 0;
 }
 
+DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                                 float beta2, float eps, int step, const int* status, float* loss, void* stream);
+
 DL4SS_API int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                          float beta2, float eps, int step, void* stream) {
+  return dl4ss_adam_guarded(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, nullptr, stream);
+}
+
+DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                                 float beta2, float eps, int step, const int* status, float* loss, void* stream) {
   DL4SS_REQUIRE(p && g && m && v && n >= 0 && step >= 1);
   if (n == 0) return 0;
   // bias corrections in double on the host, as torch computes them in Python floats
@@ -286,7 +299,7 @@ DL4SS_API int dl4ss_adam(float* p, const float* g, float* m, float* v, long long
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   const unsigned grid = (unsigned)min(8192LL, (n / 4 + 255) / 256 + 1);
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr, beta1, beta2, eps,
-                     bc1, bc2s);
+                     bc1, bc2s, status, loss);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

@@ -467,8 +467,11 @@ class SepTrainer:
         dp.allreduce_mean_(self.net.grad, self.pg)
 
     def optimizer_step(self):
+        """Adam on device; refused (parameters untouched, loss[0] = NaN) when a recurrence
+        hand-off of this step timed out -- a timed-out step never reaches the weights."""
         self.step_count += 1
-        ops.adam_(self.net.flat, self.net.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
+        ops.adam_(self.net.flat, self.net.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps,
+                  status=self.status, loss=self.loss)
 
     def step(self, raw, gains, spk_idx):
         """One full training step on device-resident inputs; returns the loss tensor (not synced)."""
@@ -528,7 +531,11 @@ class SepTrainer:
         return self._graph_loss
 
     def check(self):
+        """Raise if a recurrence hand-off timed out since the last check (the status word is
+        reset, so the trainer can continue after the caller has handled it; the guarded Adam
+        already refused every update computed from the timed-out step)."""
         torch.cuda.synchronize()
         s = int(self.status.item())
         if s:
-            raise RuntimeError(f"BiRNN hand-off timed out (status {s})")
+            self.status.zero_()
+            raise RuntimeError(f"BiRNN hand-off timed out (status {s}): the step's update was refused")

@@ -254,8 +254,26 @@ def colsum(A, out):
     return out
 
 
-def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8):
+def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, loss=None):
+    """torch Adam step on flat buffers; with ``status`` (the recurrence hand-off status word)
+    the update is refused on device when a hand-off of this step timed out, and loss[0] is
+    set to NaN (dl4ss_adam_guarded)."""
     for t in (p, g, m, v):
         _f32c(t, "adam")
-    _lib.call("dl4ss_adam", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(), float(lr), float(betas[0]),
-              float(betas[1]), float(eps), int(step), _lib.stream_ptr())
+    _lib.call("dl4ss_adam_guarded", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(), float(lr),
+              float(betas[0]), float(betas[1]), float(eps), int(step), _lib.ptr(status), _lib.ptr(loss),
+              _lib.stream_ptr())
+
+
+def birnn_plan(cell, B, H, precision="bf16", max_wg=0):
+    """The persistent recurrence's plan {BC, NG, J, nchunk, grid} under a co-residency budget
+    of max_wg workgroups (0: the current device's); None when no plan fits (host-only for
+    max_wg > 0)."""
+    import ctypes
+
+    info = (ctypes.c_int * 5)()
+    rc = _lib.lib().dl4ss_birnn_plan_info({"lstm": 0, "gru": 1}[cell], int(B), int(H),
+                                          1 if precision == "bf16" else 0, int(max_wg), info)
+    if rc != 0:
+        return None
+    return dict(zip(("BC", "NG", "J", "nchunk", "grid"), list(info)))

@@ -120,6 +120,17 @@ enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
  * step over separate workspaces for every layer and pass). */
 #define DL4SS_RNN_WS_ZEROED 0x100
 long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
+/* The persistent recurrence's plan under a co-residency budget: every workgroup of a launch
+ * (2 directions x nchunk batch chunks x NG units groups) must be resident at once, so the
+ * batch chunk BC is the smallest in {1, 2, 4, 8} with 2 * nchunk * NG <= max_wg (max_wg <= 0:
+ * the current device's CUs minus 1/16, 240 on a full MI355X; env DL4SS_RNN_MAX_WG overrides).
+ * info[5] = {BC, NG, J, nchunk, grid}.  Host-only when max_wg > 0.  0, or
+ * hipErrorInvalidValue when no plan fits.  Every launch re-checks the grid against the CU
+ * count x the kernel's occupancy and fails with hipErrorCooperativeLaunchTooLarge (720)
+ * instead of spinning to the hand-off timeout. */
+int dl4ss_birnn_plan_info(int cell, int B, int H, int precision, int max_wg, int* info);
+/* Test hook: polls before a recurrence hand-off times out (0 = default, ~1 s of polling). */
+void dl4ss_debug_set_spin_limit(unsigned limit);
 /* One layer, both directions: G (B,T,2,NG*H) = X W_ih^T + b_ih (NG = 4 LSTM / 3 GRU),
  * W_hh (2, NG*H, H), b_hh (2, NG*H) -> out (B,T,2H) [fwd | reverse], hprev (B,T,2H)
  * (h_{t-1} per step), act (B,T,2,4H) gate activations, cs (B,T,2,H) LSTM cells.
@@ -207,6 +218,11 @@ int dl4ss_colsum(const float* A, long long lda, int M, int N, float* out, void* 
 /* torch.optim.Adam step on flat fp32 buffers (EvalVer.py:538-544). */
 int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
                float eps, int step, void* stream);
+/* dl4ss_adam that refuses a step computed from a timed-out recurrence: when *status != 0
+ * (a BiRNN hand-off of this step timed out) no parameter or moment changes and loss[0]
+ * (if not NULL) is set to NaN, so the step's loss read by the caller reports it. */
+int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                       float beta2, float eps, int step, const int* status, float* loss, void* stream);
 
 /* ---- kernels behind the reference-API nn.Modules (dl4ss_amd/compat/myNet.py) ---- */
 /* dpre = dv * (1 - v^2): backward of MIX_SPEECH's tanh(Linear) (EvalVer.py:298-299). */

@@ -11,7 +11,7 @@ HEADER = os.path.join(ROOT, "include", "dl4ss_hip.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|long long) (dl4ss_\w+)\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|long long|void) (dl4ss_\w+)\(", txt, flags=re.M)))
 
 
 def test_header_declares_entry_points():
