@@ -79,24 +79,44 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel of the step eagerly instead of replaying the captured HIP graph")
     ap.add_argument("--no-stft-standalone", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=24)
-    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--dist", action="store_true",
                     help="initialise the RCCL process group even at world size 1 (exercises the DP path)")
     return ap.parse_args()
 
 
-def cpu_baseline(args, N, K):
+def cpu_threads():
+    """Host threads for the CPU baseline: the CPUs this process may run on
+    (len(os.sched_getaffinity(0))), capped by the cgroup CPU quota when
+    one is set (a container whose affinity lists the whole machine but whose quota is a
+    share of it would otherwise oversubscribe its share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(args, N, K, with_classifier=False):
     """Reference CPU path (the oracle restatement, torch-CPU fp32 + numpy FFT) on a
-    bounded sample of the same workload: cpu_batch mixtures of the B=32 batch."""
-    from oracle import dsp, model as om
+    bounded sample of the same workload: cpu_steps steps of the B = 32 batch.  With
+    ``with_classifier`` each step also runs the speaker classifier's forward (BiLSTM-3L,
+    H = 600, EvalVer.py:592 / 305-326), which the reference computes and then discards
+    (its output is replaced by the ground truth, :598-599): the reference-faithful cost."""
+    from oracle import dsp, model as om, recursive as orec
     from dl4ss_amd import synth
 
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    cores = cpu_threads()
     torch.set_num_threads(cores)
     torch.manual_seed(1)
     ref = om.SepModel(cell="lstm", num_layers=4)
     opt = om.make_adam(ref)
+    cls = orec.Classifier(hidden=600, num_layers=3) if with_classifier else None
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1)
     src, spk, u = gen.batch(args.cpu_batch)
     gains = synth.gains_for(u, K)
@@ -110,6 +130,9 @@ def cpu_baseline(args, N, K):
             feats.append(dsp.magnitude(m))
             Y.append(np.stack([dsp.magnitude(s[k]) for k in range(K)]))
         f = torch.from_numpy(np.array(feats))
+        if cls is not None:
+            with torch.no_grad():
+                cls(f)
         om.train_step(ref, opt, f, f, torch.from_numpy(np.array(Y)), torch.from_numpy(spk), mode=args.mode)
 
     one_step()  # warm-up
@@ -117,9 +140,11 @@ def cpu_baseline(args, N, K):
     for _ in range(args.cpu_steps):
         one_step()
     dt = time.perf_counter() - t0
+    what = "+ classifier BiLSTM-3L H=600 fwd (reference-faithful) " if with_classifier else "(mask path) "
     return {"value": args.cpu_batch * args.cpu_steps / dt, "unit": "mixtures/s", "cores": cores, "kind": "port",
-            "sample": f"{args.cpu_steps} step(s) of {args.cpu_batch} mixtures (of the B={args.batch} workload), "
-                      f"oracle torch-CPU fp32 BiLSTM-4L fwd+{args.mode} loss+bwd+Adam incl. numpy STFT features"}
+            "sample": f"{args.cpu_steps} step(s) of the B={args.cpu_batch} batch, oracle torch-CPU fp32 BiLSTM-4L "
+                      f"fwd+{args.mode} loss+bwd+Adam incl. numpy STFT features {what}on {cores} thread(s)",
+            "seconds": dt}
 
 
 def main():
@@ -315,6 +340,7 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args, N, K)
+            out["cpu_baseline_with_classifier"] = cpu_baseline(args, N, K, with_classifier=True)
         print(json.dumps(out), flush=True)
     if pg is not None:
         import torch.distributed as dist

@@ -45,6 +45,8 @@ BGD_NOISE_WAV = None
 BGD_NOISE_FILE = 'Dataset_Multi/BGD_150203_010_STR.CH1.wav'
 Out_Sep_Result = True
 VideoSize = (299, 299)
+VIDEO_RATE = 10
+channel_first = True
 
 # ---- this build (not in the reference) ----
 # mask net of MIX_SPEECH (main_run.py: BiGRU NUM_LAYERS; EvalVer: BiLSTM 4 layers)

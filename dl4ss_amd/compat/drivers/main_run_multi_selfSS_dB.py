@@ -1,0 +1,110 @@
+"""py3 mirror of ``Torch_multi/main_run_multi_selfSS_dB.py`` -- config C4 (BiGRU mask net, no
+ADDJUST, MSE + 0.5 sum-to-one; 3 speakers with ``MIN_MIX = MAX_MIX = 3``; LR halved every 50
+epochs, :442-444).  Imports the reference's names (``config_WSJ0_dB``, ``predata_multiAims_dB``,
+``myNet``, ``test_multi_labels_speech``, ``bss_test``); ``loader='3dB'`` takes the 3-speaker
+gain rule of ``predata_multiAims_3dB`` instead.  Runs :441-532 on the ``myNet`` modules with
+the HIP Adam (the per-batch wav / SDR evaluation, :525-527, is not part of the step)."""
+import random
+
+import numpy as np
+import torch
+
+from dl4ss_amd import compat as _compat
+
+_compat.install()
+
+import config_WSJ0_dB as config  # noqa: E402
+from predata_multiAims_dB import prepare_data, prepare_datasize, prepare_data_fake  # noqa: E402,F401
+import myNet  # noqa: E402
+from test_multi_labels_speech import multi_label_vector  # noqa: E402
+import librosa  # noqa: E402,F401
+import soundfile as sf  # noqa: E402,F401
+import bss_test  # noqa: E402,F401
+
+from dl4ss_amd.compat.optim import Adam  # noqa: E402
+from dl4ss_amd.compat.drivers import _common as C  # noqa: E402
+from dl4ss_amd import schedule  # noqa: E402
+
+
+class MIX_SPEECH(myNet.MIX_SPEECH):
+    """selfSS_dB.py:259-283: nn.GRU(HIDDEN_UNITS, NUM_LAYERS) + Linear + tanh, returns V."""
+
+    def __init__(self, input_fre, mix_speech_len):
+        super().__init__(input_fre, mix_speech_len, cell="gru", num_layers=config.NUM_LAYERS,
+                         precision=getattr(config, "PRECISION", "fp32"))
+
+
+class SPEECH_EMBEDDING(myNet.SPEECH_EMBEDDING):
+    def __init__(self, num_labels, embedding_size, max_num_channel):
+        super().__init__(num_labels, embedding_size, max_num_channel, crm=False)
+
+
+class ATTENTION(myNet.ATTENTION):
+    def __init__(self, hidden_size, mode='dot'):
+        super().__init__(hidden_size, mode, crm=False)
+
+
+top_k_mask = myNet.top_k_mask
+
+
+def build(speech_fre, mix_speech_len, num_labels, spk_num_total):
+    d = C.dev()
+    m = dict(mix_hidden_layer_3d=MIX_SPEECH(speech_fre, mix_speech_len).to(d),
+             mix_speech_multiEmbedding=SPEECH_EMBEDDING(num_labels, config.EMBEDDING_SIZE,
+                                                        spk_num_total + config.UNK_SPK_SUPP).to(d),
+             att_speech_layer=ATTENTION(config.EMBEDDING_SIZE, 'dot').to(d))
+    optimizer = Adam([{'params': m['mix_hidden_layer_3d'].parameters()},
+                      {'params': m['mix_speech_multiEmbedding'].parameters()}], lr=0.0002)
+    return m, optimizer
+
+
+def train_step(m, optimizer, train_data, dict_spk2idx, dict_idx2spk, num_labels):
+    """selfSS_dB.py:457-532 on one batch dict."""
+    x = C.cuda(train_data['mix_feas'])
+    B, T, F = x.shape
+    mix_speech_hidden = m['mix_hidden_layer_3d'](x)
+    top_k_mask_mixspeech, top_k_mask_idx, _ = C.ground_truth_selection(
+        train_data, dict_spk2idx, num_labels, multi_label_vector, top_k_mask)
+    mix_speech_multiEmbs = m['mix_speech_multiEmbedding'](top_k_mask_mixspeech, top_k_mask_idx)
+    top_k_num = len(top_k_mask_idx[0])
+    multi_mask = C.expanded_attention(m['att_speech_layer'], mix_speech_hidden, mix_speech_multiEmbs, B, top_k_num,
+                                      T, F, config.EMBEDDING_SIZE)
+    y_multi_map = C.label_ordered_targets(train_data, top_k_mask_idx, dict_spk2idx, dict_idx2spk,
+                                          (B, top_k_num, T, F))
+    loss, pred, l_mask, l_sum = C.magnitude_loss(multi_mask, x, y_multi_map)
+    optimizer.zero_grad()
+    loss.backward()
+    optimizer.step()
+    return dict(loss=loss.detach(), loss_mask=l_mask.detach(), loss_sum=l_sum.detach(), mask=multi_mask.detach(),
+                pred=pred.detach())
+
+
+def main(max_epoch=None, max_batches=None, log=print, loader="dB"):
+    np.random.seed(1)
+    torch.manual_seed(1)
+    random.seed(1)
+    prep = prepare_data
+    if loader == "3dB":
+        import predata_multiAims_3dB
+
+        prep = predata_multiAims_3dB.prepare_data
+    spk_all_list, dict_spk2idx, dict_idx2spk, mix_speech_len, speech_fre, total_frames, spk_num_total = \
+        next(prep(mode='global', train_or_test='train'))
+    num_labels = len(spk_all_list)
+    m, optimizer = build(speech_fre, mix_speech_len, num_labels, spk_num_total)
+    sched = schedule.selfss_db(optimizer.param_groups[0]['lr'])
+    history = []
+    for epoch_idx in range(config.MAX_EPOCH if max_epoch is None else max_epoch):
+        lr = sched.at_epoch_start(epoch_idx)
+        for ee in optimizer.param_groups:
+            ee['lr'] = lr
+        for batch_idx in range(config.EPOCH_SIZE if max_batches is None else max_batches):
+            train_data = next(prep('once', 'train'))
+            out = train_step(m, optimizer, train_data, dict_spk2idx, dict_idx2spk, num_labels)
+            history.append(float(out['loss']))
+            log(f"epoch {epoch_idx} batch {batch_idx} loss {history[-1]:.6f} lr {lr:g}")
+    return m, history
+
+
+if __name__ == "__main__":
+    main()

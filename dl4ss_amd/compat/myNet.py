@@ -18,8 +18,10 @@ reference ``state_dict`` keys load unchanged) and forward semantics follow:
 Forward and backward of the recurrence, every Linear / GEMM, the attention, the
 gather and top_k_mask run on the HIP kernels (``dl4ss_amd.autograd``); only
 reshapes, time means, concatenations and the classifier's sigmoid are torch glue.  The
-Inception-v3 video branch (``inception_v3`` / ``Inception3``) is off the separation
-path (VIDEO_QUERY is unused by the audio drivers) and raises.
+Inception-v3 video branch (``inception_v3`` / ``Inception3``, ``_inception.py``) is off
+the separation path (VIDEO_QUERY is constructed by main_run.py:407 but never called):
+it constructs, loads the reference's ImageNet file by name when present, and runs on
+plain torch.
 """
 import math
 
@@ -38,14 +40,10 @@ __all__ = ['Inception3', 'inception_v3', 'BiRNN', 'MIX_SPEECH', 'MIX_SPEECH_clas
            'ADDJUST', 'ATTENTION', 'top_k_mask']
 
 
-def inception_v3(pretrained=False, **kwargs):
-    """Torch_multi/myNet.py:17-32 signature.  The video query branch is out of scope."""
-    return Inception3(**kwargs)
-
-
-class Inception3(nn.Module):
-    def __init__(self, num_classes=1000, aux_logits=True, transform_input=False):
-        raise NotImplementedError("Inception-v3 (VIDEO_QUERY) is not on the audio separation path of this build")
+try:  # Torch_multi/myNet.py:17-330: the VIDEO_QUERY image net (off the audio path; plain torch)
+    from ._inception import Inception3, inception_v3  # noqa: F401
+except ImportError:  # imported by its bare name (compat.install())
+    from dl4ss_amd.compat._inception import Inception3, inception_v3  # noqa: F401
 
 
 class BiRNN(nn.Module):

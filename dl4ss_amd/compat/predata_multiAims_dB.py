@@ -15,14 +15,15 @@ import random
 
 import numpy as np
 
-try:
-    from . import config
+try:  # predata_multiAims_dB.py:7 imports config_WSJ0_dB as config
+    from . import config_WSJ0_dB as config
     from ._data import BatchMaker, split_speakers, to_reference_dict
 except ImportError:  # imported by its bare name (compat.install())
-    import config
+    import config_WSJ0_dB as config
     from dl4ss_amd.compat._data import BatchMaker, split_speakers, to_reference_dict
 
 channel_first = True
+GAIN_RULE = "db2"  # predata_multiAims_dB.py:124-130 (compat._data.gains_of)
 
 
 def prepare_datasize(gen):
@@ -47,14 +48,17 @@ def prepare_data_fake(train_or_test, num_labels):
         yield out
 
 
-def prepare_data(mode, train_or_test):
-    if config.MODE != 1 or config.DATASET != 'WSJ0':
-        raise ValueError('No such dataset:{} for Speech.'.format(config.DATASET))
-    all_spk_train = split_speakers(config, 'train')
-    mix_k = random.randint(config.MIN_MIX, config.MAX_MIX)
-    maker = BatchMaker(config, train_or_test, mix_k, seed_offset=random.randrange(1 << 20))
+def prepare_data(mode, train_or_test, gain_rule=GAIN_RULE, cfg=None):
+    """gain_rule / cfg: the variants predata_multiAims (unit gains, ``config``) and
+    predata_multiAims_3dB (``config_WSJ0_dB``) share this generator."""
+    cfg = cfg or config
+    if cfg.MODE != 1 or cfg.DATASET != 'WSJ0':
+        raise ValueError('No such dataset:{} for Speech.'.format(cfg.DATASET))
+    all_spk_train = split_speakers(cfg, 'train')
+    mix_k = random.randint(cfg.MIN_MIX, cfg.MAX_MIX)
+    maker = BatchMaker(cfg, train_or_test, mix_k, seed_offset=random.randrange(1 << 20))
     while True:
-        dev = maker.make(config.BATCH_SIZE)
+        dev = maker.make(cfg.BATCH_SIZE, gain_rule=gain_rule)
         if mode == 'global':
             spk = sorted(all_spk_train)
             d2i = {s: i for i, s in enumerate(spk)}

@@ -27,7 +27,8 @@ ref_c1_mainrun.npz   Torch_multi/main_run.py:460-522 (BiGRU-2L, dense 101-channe
 ref_c3_crm.npz       TDAA_beta/main_run_sstune_cRM_EvalVer.py:645-752 (cRM branch,
                      inverse compression :688, complex MSE :720-743)
 ref_c4_3spk.npz      Torch_multi/main_run_multi_selfSS_dB.py:457-532 (3 speakers)
-ref_topk.npz         top_k_mask (EvalVer.py:390-405, GRID.py:227-244), multi_label_vector
+ref_inception_keys.npz  state_dict names / shapes of Torch_multi/myNet.py's Inception3
+ref_small.npz        top_k_mask (EvalVer.py:390-405, GRID.py:227-244), multi_label_vector
                      (TDAA_beta/test_multi_labels_speech.py:287-300), LR schedules
                      (EvalVer.py:570-575, selfSS_dB.py:442-444)
 """
@@ -538,11 +539,36 @@ def make_small(seed=15):
     return out
 
 
+def make_inception():
+    """Parameter / buffer names and shapes of Torch_multi/myNet.py's Inception3 (the module
+    imports under py3; its init loop's flat copy_ into N-d weights, :66-67, raises, so
+    copy_ is made shape-tolerant while it is constructed)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("ref_myNet", os.path.join(REF, "Torch_multi/myNet.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    orig = torch.Tensor.copy_
+
+    def copy_(self, src, *a, **k):
+        return orig(self, src.view_as(self) if src.numel() == self.numel() else src, *a, **k)
+
+    torch.Tensor.copy_ = copy_
+    try:
+        net = mod.Inception3()
+    finally:
+        torch.Tensor.copy_ = orig
+    sd = net.state_dict()
+    out = {"names": np.array(list(sd)), "shapes": np.array([",".join(map(str, v.shape)) for v in sd.values()])}
+    np.savez_compressed(os.path.join(HERE, "ref_inception_keys.npz"), **out)
+    return {}
+
+
 def main():
     torch.manual_seed(1)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    which = sys.argv[1:] or ["small", "c2", "c1", "c3", "c4"]
-    fns = dict(small=make_small, c2=make_c2, c1=make_c1, c3=make_c3, c4=make_c4)
+    which = sys.argv[1:] or ["small", "c2", "c1", "c3", "c4", "inception"]
+    fns = dict(small=make_small, c2=make_c2, c1=make_c1, c3=make_c3, c4=make_c4, inception=make_inception)
     for w in which:
         sink = io.StringIO()
         with contextlib.redirect_stdout(sink):

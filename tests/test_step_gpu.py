@@ -298,3 +298,35 @@ def test_step_c2_full_size_pit_indices(dev, precision):
     print(json.dumps(rec))
     assert decided.all() and agree.all(), rec
     assert rel < 1e-3, rec
+
+
+@pytest.mark.parametrize("precision,mode", [("fp32", "label"), ("bf16", "pit")])
+def test_dp_mean_of_half_batch_gradients_equals_full_batch(dev, precision, mode):
+    """The data-parallel arithmetic of SepTrainer (dp.allreduce_mean_ of per-rank flat
+    gradients, each rank scaling its loss by its LOCAL batch: s1 = 1/(B_local K T F),
+    s2 = 0.5/(B_local T F)) at world size 1: the mean of the flat net.grad of two half-batch
+    steps equals the full-batch step's net.grad -- fused bias gradients, query / ADDJUST
+    gradients and the sum-to-one term included."""
+    B, K, N = 4, 2, 4000
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=21)
+    src, spk, u = gen.batch(B)
+    gains = synth.gains_for(u, K)
+    raw = torch.from_numpy(src.astype(np.float32)).to(dev)
+    g = torch.from_numpy(gains.astype(np.float32)).to(dev)
+    sp = torch.from_numpy(spk.astype(np.int32)).to(dev)
+    net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=13)
+
+    def grads(lo, hi):
+        tr = engine.SepTrainer(net, hi - lo, K, N, mode=mode, precision=precision)
+        tr.spk.copy_(sp[lo:hi])
+        tr.features(raw[lo:hi].contiguous(), g[lo:hi].contiguous())
+        tr.forward()
+        tr.loss_and_grad()
+        tr.backward()
+        tr.check()
+        return net.grad.detach().clone()
+
+    full = grads(0, B)
+    half = 0.5 * (grads(0, B // 2) + grads(B // 2, B))
+    err = float((half - full).abs().max() / full.abs().max())
+    assert err < (1e-5 if precision == "fp32" else 1e-3), err
