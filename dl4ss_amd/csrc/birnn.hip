@@ -781,7 +781,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef DBG_SAFE_ONLY
         __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);               // fast: plain, stays in L2
 #endif
+#ifndef DBG_FAST_ONLY
         __builtin_amdgcn_raw_buffer_store_b128(x, xr, off + slot_g * 8, 0, 16);  // safe: sc1 write-through
+#endif
       }
       if (tid == 0) TRACE(0, s);
       if (cval) {
@@ -1483,7 +1485,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
           const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules, fast copy
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);                // fast: plain
+#ifndef DBG_FAST_ONLY  // diagnostic build: no safe copy (measures its cost; hangs if the fast copy is not seen)
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, (off + copy_g) * 8, 0, 16);    // safe: sc1
+#endif
         }
       }
 #else
@@ -1514,7 +1518,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
           const int off = (((s & 1) * 2 * NG + w) * BC + col) * HG + (k >> 1);  // granules, fast copy
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);                // fast: plain
+#ifndef DBG_FAST_ONLY  // diagnostic build: no safe copy (measures its cost; hangs if the fast copy is not seen)
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, (off + copy_g) * 8, 0, 16);    // safe: sc1
+#endif
         }
       }
 #endif

@@ -1,0 +1,88 @@
+"""Parity at the FULL sizes of the other BASELINE.json configurations (the headline C2 is in
+test_step_gpu.py): the HIP step vs the CPU oracle on identical synthetic mixtures.
+
+* C1  Torch_multi/main_run.py: BiGRU-2L, B = 1, N = 40000 (5 s, T = 313), 101-channel loss,
+      no ADDJUST -- fp32 parity mode and the bf16 mode.
+* C3  cRM path: BiGRU-2L, B = 16, N = 32000 -- one step in fp32, and the step at which the
+      reference's inverse compression (cRM_EvalVer.py:688) first turns the loss non-finite
+      on a repeated batch, HIP vs oracle, on the same seed.
+* C4  3 speakers (predata_multiAims_3dB gains), BiGRU-2L without ADDJUST (selfSS_dB model),
+      B = 32, N = 32000 -- fp32 and bf16.
+* C5  recursive extraction at N = 32000 (T = 251) vs oracle/recursive.py: speaker ids
+      bit-exact, probabilities / masks as test_recursive_gpu.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model as om
+from oracle import recursive as orc
+from dl4ss_amd import engine, synth
+
+from test_step_gpu import _compare_step, _oracle_features, _setup  # noqa: E402
+from test_recursive_gpu import _feats, _models, _ours  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+BF16 = dict(precision="bf16", tol_loss=1e-2, tol_grad=5e-2, tol_pred=1e-2)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c1_full_size(dev, precision):
+    kw = BF16 if precision == "bf16" else {}
+    _compare_step(dev, "gru", 2, 1, 2, 40000, "label", loss_channels=101, adjust=False, **kw)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c4_full_size_3spk(dev, precision):
+    kw = BF16 if precision == "bf16" else {}
+    _compare_step(dev, "gru", 2, 32, 3, 32000, "label", adjust=False, **kw)
+
+
+def test_c3_full_size_step(dev):
+    _compare_step(dev, "gru", 2, 16, 2, 32000, "crm", tol_grad=5e-3)
+
+
+def test_c3_first_non_finite_step_matches_oracle(dev):
+    """The cRM inverse compression -1/C log((K - M)/(K + M)) is infinite once a compressed
+    mask reaches K (fp32 tanh(e) rounds to 1 for |e| >= 9.02).  Training the C3
+    configuration on one repeated batch, the HIP step and the oracle step must first produce a
+    non-finite loss at the same step (or both stay finite), and agree until then."""
+    B, K, N, S = 16, 2, 32000, 40
+    net, tr, src, spk, gains, ref = _setup(dev, "gru", 2, B, K, N, "crm", seed=3)
+    feats, X, Y = _oracle_features(src, gains, True)
+    idx = torch.from_numpy(spk)
+    opt = om.make_adam(ref)
+    raw = torch.from_numpy(src.astype(np.float32)).to(dev)
+    g = torch.from_numpy(gains.astype(np.float32)).to(dev)
+    sp = torch.from_numpy(spk.astype(np.int32)).to(dev)
+    torch.set_num_threads(16)
+    first_ours = first_ref = None
+    for s in range(S):
+        lo = float(tr.step(raw, g, sp)[0].item())
+        tr.check()
+        lr = float(om.train_step(ref, opt, feats, X, Y, idx, mode="crm")[0])
+        if first_ours is None and not np.isfinite(lo):
+            first_ours = s
+        if first_ref is None and not np.isfinite(lr):
+            first_ref = s
+        if first_ours is not None or first_ref is not None:
+            break
+        assert abs(lo - lr) <= 1e-3 * abs(lr), (s, lo, lr)
+    assert first_ours == first_ref, (first_ours, first_ref)
+
+
+def test_c5_full_length_recursive(dev):
+    B, n, seed = 1, 32000, 7
+    mix, cls, emb = _models(seed)
+    X = _feats(B, n, seed)
+    T = X.shape[1]
+    assert T == 251
+    with torch.no_grad():
+        ref = orc.recursive_extract(lambda x: mix(x), cls, emb.weight, X)
+    out = _ours(dev, mix, cls, emb, B, T, "fp32").run(X.to(dev))
+    torch.cuda.synchronize()
+    assert torch.equal(out["spk"].cpu().long(), ref["spk"]), (out["spk"], ref["spk"])
+    for s in range(2):
+        assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < 2e-5
+    assert (out["masks"].cpu() - ref["masks"]).abs().max() < 1e-4

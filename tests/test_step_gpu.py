@@ -103,7 +103,15 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
         ours = net.view(name).cpu()
         diff = (ours - p.detach()).abs()
         assert diff.max().item() <= 2.1 * 2e-4, name
-        assert (diff > 1e-6).float().mean().item() < 1e-3, name
+        moved = diff > 1e-6
+        if moved.any():
+            # Adam's first step is lr*g/(|g|+eps), i.e. sign-sensitive: a disagreeing weight must
+            # have a reference gradient no larger than that tensor's measured gradient error
+            # (itself <= tol_grad of the largest gradient), and such weights must be rare
+            gr = grads_ref[name]
+            err_abs = errs[name] * max(gr.abs().max().item(), 1e-30)
+            assert bool((gr.abs()[moved] <= err_abs).all()), (name, int(moved.sum()), gr[moved][:8])
+            assert moved.float().mean().item() < 1e-2, name
 
 
 def test_step_bilstm_label_order(dev):
