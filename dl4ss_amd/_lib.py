@@ -63,10 +63,12 @@ SIGNATURES = {
     "dl4ss_adam_guarded": [P, P, P, P, LL, F, F, F, F, I, P, P, P],
     "dl4ss_birnn_plan_info": [I, I, I, I, I, P],
     "dl4ss_debug_set_spin_limit": [ctypes.c_uint],
+    "dl4ss_debug_set_place_force": [ctypes.c_int],
 }
 # entry points that return a value rather than a hipError_t
 RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
-            "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None}
+            "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None,
+            "dl4ss_debug_set_place_force": None}
 
 _lib = None
 

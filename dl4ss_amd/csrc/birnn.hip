@@ -120,6 +120,19 @@ __device__ __forceinline__ float sum_partials(const float* p, int stride, int NG
     for (int i = 0; i < w; ++i) v[i] += v[i + w];
   return v[0];
 }
+// Sum of 16 producers' dh partials p[i * stride] for the packed BPTT, whose partial buffer
+// always holds 16 producer rows (rows >= NG stay zero): no index clamp, no select.  Same
+// pairwise tree as sum_partials, so the result is bitwise the same.
+__device__ __forceinline__ float sum_partials16(const float* p, int stride) {
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = p[i * stride];
+#pragma unroll
+  for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+    for (int i = 0; i < w; ++i) v[i] += v[i + w];
+  return v[0];
+}
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
   unsigned u = __float_as_uint(f);
@@ -153,6 +166,7 @@ struct RnnArgs {
   u64* xbuf;             // granules
   int* status;
   unsigned spin_limit;   // polls before a hand-off times out (SPIN_LIMIT; dl4ss_debug_set_spin_limit)
+  int place_force;       // packed kernels: 1 = write-through hand-off regardless of placement (test hook)
   u64* stamps;           // diagnostic build only
   // bf16 mode extras (packed kernels only; any may be null)
   unsigned short* outb;    // fwd (B,T,2H) bf16(h)          -- next layer's / Linear's GEMM operand
@@ -474,15 +488,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 //    two granules per 16-B store, 8 granules per (batch row, producer);
 //  * ONE wave polls, keeping two sweeps in flight (the older one is merged while
 //    the newer one travels): hand-off 2.3 -> 1.9 us;
-//  * a FAST copy written with plain stores and read with `sc1` loads: a plain store
+//  * granules written with PLAIN stores and read with `sc1` loads: a plain store
 //    lands in the producer XCD's L2, which same-XCD consumers read directly, while an
 //    `sc1` store drops the line from L2 and the reader goes to the Infinity Fabric:
 //    hand-off 1.9 -> 0.96 us, step 2.68 -> 1.64 us.  A group's workgroups are placed
-//    on one XCD (group_of), but placement is speed only: every granule is ALSO
-//    published with an `sc1` store to a SAFE copy (the validated write-through form,
-//    MI355X_MICROARCH.md, Valid forms R2), and a consumer that has not completed a
-//    poll of the fast copy after FAST_SPINS sweeps switches to the safe copy for the
-//    rest of the launch.  Every value is validated by its own tag either way.
+//    on one XCD (group_of), but placement is speed only, never correctness: at launch
+//    start every workgroup of a group publishes its XCC id (group_needs_write_through)
+//    and only a group found on ONE XCD uses plain stores; a group that spans XCDs writes
+//    every granule `sc1` (the validated write-through form, MI355X_MICROARCH.md, Valid
+//    forms R2).  (Round 1 wrote every granule twice, plain + `sc1`, and switched a
+//    consumer to the `sc1` copy after a stalled poll: the second store cost ~600 cycles
+//    of a BPTT step's publish.)  Every value is validated by its own tag either way.
 // Waves (FWD_NPW polling waves, default 2): 0-3 MFMA tiles 0-3 + cell update + publish +
 //        saved-state stores; 4 polls, and 7 (FWD_NPW >= 2) and 6 (FWD_NPW == 3) poll too
 //        (those waves hold no MFMA tile); the remaining waves of 5-7 run MFMA tiles 4..MT-1
@@ -504,10 +520,47 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 static_assert(FWD_MV_CHAINS >= 1 && FWD_MV_CHAINS <= 8, "FWD_MV_CHAINS: 1..KSMAX accumulator chains");
 static_assert(FWD_NPW >= 1 && FWD_NPW <= 3, "FWD_NPW: 1..3 polling waves");
 static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
-constexpr unsigned FAST_SPINS = 256;  // sweeps of the fast copy before the safe copy is polled
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xFu;
+}
+
+// Placement check at launch start (packed kernels).  A group's hand-off granules may be
+// written with PLAIN stores only when every workgroup of the group runs on one XCD: a plain
+// store stays in that XCD's L2, which serves the peers' `sc1` polls (MI355X_MICROARCH.md,
+// stores of each flavour); across XCDs only `sc1` write-through stores are visible.  HIP
+// promises no placement (bid % 8 -> XCD is observed, not guaranteed), so every workgroup
+// publishes its XCC id as one granule {tag 1, id} and the polling wave gathers the group's NG
+// ids.  Every workgroup of the group reads the same NG ids and so picks the same form.
+// Called by the polling wave; returns (wave-uniform) true when the granules must be written
+// through.  force: 1 = write-through regardless (test hook), 0 = by placement.
+__device__ __forceinline__ bool group_needs_write_through(const u64* place, int NG, int lane, unsigned limit,
+                                                          int* status, int force) {
+  unsigned id = 0;
+  bool ok = true;
+  if (lane < NG) {
+    u64 v = get_granule(place + lane);
+    unsigned spins = 0;
+    while ((unsigned)(v >> 32) != 1u) {
+      if (++spins > limit) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v = get_granule(place + lane);
+    }
+    id = (unsigned)v;
+  }
+  if (!ok) atomicOr(status, 4);
+  const unsigned id0 = __shfl(id, 0);
+  const bool same = !__any(lane < NG && (id != id0 || !ok));
+  return force == 1 || !same;
 }
 
 template <int CELL, int BC>
@@ -565,10 +618,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   for (int q = 0; q < NGATE; ++q) bh[q] = cval ? a.bhh[(long long)d * GH + q * H + cj] : 0.0f;
   float hst = 0.0f, cst = 0.0f;
 
-  // granules of this group: [2 slots][fast, safe][BC][NG][8] x 8 B
+  // granules of this group: [2 slots][hand-off, spare][BC][NG][8] x 8 B; the spare copy of
+  // slot 1 holds the placement granules
   const int slot_g = BC * NG * 8;
   u64* xg = a.xbuf + (long long)group * 4 * slot_g;
   const __amdgpu_buffer_rsrc_t xr = granule_rsrc(xg, (unsigned)(4 * slot_g * 8));
+  __shared__ int s_wt;
+  if (tid == 0) __hip_atomic_store(xg + 3 * slot_g + w, (1ull << 32) | xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wv == WPOLL) {
+    const bool wt = group_needs_write_through(xg + 3 * slot_g, NG, lane, a.spin_limit, a.status, a.place_force);
+    if (lane == 0) s_wt = wt;
+  }
 
   // ---- prefetch waves 5-7 (5-6 with FWD_NPW = 2: wave 7 polls too): input projection
   //      G[b][t][d][q*H + j] of every own (b, unit, gate)
@@ -590,6 +650,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   }
   if (pfw) ld.issue(d == 0 ? 0 : T - 1, T);
   __syncthreads();
+  const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
   STAMP_DECL
 
   auto matvec = [&]() {  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
@@ -598,6 +659,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     bf16x8 bv[KSMAX];
 #pragma unroll
     for (int ks = 0; ks < KSMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
+    // every B read issued before the first MFMA: one LDS round trip instead of one per pair
+    // (the scheduler otherwise interleaves reads and waits to save registers)
+    __builtin_amdgcn_sched_barrier(0);
     // FWD_MV_CHAINS independent accumulator chains over the k-steps (the chain length is
     // the matvec's latency), summed in fixed order
     f32x4 acc[FWD_MV_CHAINS];
@@ -633,21 +697,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       doff[g] = on ? b * SHB + k0 : 0;
       dlim[g] = on ? max(0, min(min(6, J - 6 * pp), H - k0)) : 0;
     }
-#ifdef DBG_SAFE_ONLY  // diagnostic build (tools/variant_lib.py safe -DDBG_SAFE_ONLY): the fallback copy only
-    bool safe = true;
-#else
-    bool safe = false;  // sticky: once the fast copy stalls, the rest of the launch polls the safe copy
-#endif
     for (int s = 0; s < T; ++s) {
       if (s > 0) {
         const unsigned tag = (unsigned)s & 0xFFFFu;
-        const int base = ((s - 1) & 1) * 2 * slot_g * 8;  // fast copy of the slot (bytes)
+        const int base = ((s - 1) & 1) * 2 * slot_g * 8;  // the slot's hand-off copy (bytes)
         TRACE(2, s);
         // two sweeps in flight: the older one is merged while the newer one travels;
         // a pair is taken from the first sweep that shows both its tags.  Relaxed agent
         // atomic 8-B loads (global_load_dwordx2 sc1): unlike the buffer intrinsics they
         // are never hoisted out of the spin loop or merged by the compiler.
-        const u64* src = xg + (base >> 3) + (safe ? slot_g : 0);
+        const u64* src = xg + (base >> 3);
         u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
         unsigned done = 0;
 #pragma unroll
@@ -689,10 +748,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
           if (++spins > a.spin_limit) {
             atomicOr(a.status, 1);
             return;
-          }
-          if (spins == FAST_SPINS && !safe) {  // the fast copy is not reaching this CU: poll the safe one
-            safe = true;
-            src += slot_g;
           }
         }
         u32x4 v[GLK];
@@ -778,12 +833,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
         const u32x4 x = {w01, (w23 & 0xFFFFu) | (tag << 16), (w23 >> 16) | (w45 << 16), (w45 >> 16) | (tag << 16)};
         const int off = ((s & 1) * 2 * slot_g + (cb * NG + w) * 8 + 2 * cu) * 8;
-#ifndef DBG_SAFE_ONLY
-        __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);               // fast: plain, stays in L2
-#endif
-#ifndef DBG_FAST_ONLY
-        __builtin_amdgcn_raw_buffer_store_b128(x, xr, off + slot_g * 8, 0, 16);  // safe: sc1 write-through
-#endif
+        if (wt)
+          __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 16);  // sc1 write-through (group spans XCDs)
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);   // plain: stays in the group's L2
       }
       if (tid == 0) TRACE(0, s);
       if (cval) {
@@ -1152,7 +1205,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 // relative error <= 2^-16, far below the bf16 rounding of dgh itself), two per
 // tagged 8-B granule:
 //   granule = { lo: p0 | (p1 & 0xFF) << 24, hi: (p1 >> 8) | tag << 16 }
-// one 16-B store per 4 units (two granules), fast (plain) + safe (`sc1`) copies,
+// one 16-B store per 4 units (two granules), plain or `sc1` by the group's placement,
 // buffer [slot][copy][producer][b][HG granules], HG = H/2 rounded up to even.
 // Waves: 0-3 cell backward (rows b = tid/32) + MFMA W^T dgh + publish;
 //        4 polls the NG producers' partials of the own J units into LDS;
@@ -1187,10 +1240,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   unsigned short* sdgb = reinterpret_cast<unsigned short*>(smem);  // [16][SDG] bf16 dgh B image
-  float* sdh = smem + 8 * SDG;                                      // [NG][BC][J] gathered partials
-  float* wsc = sdh + ((NG * BC * J + 3) & ~3);                      // [4 waves][BC][WSPAN]
+  float* sdh = smem + 8 * SDG;                                      // [16][BC][J] gathered partials (rows >= NG stay 0)
+  float* wsc = sdh + ((16 * BC * J + 3) & ~3);                      // [4 waves][BC][WSPAN]
   float* sop = wsc + 4 * BC * WSPAN;                                // [2][BC*32][8] per-step operands
-  for (int i = tid; i < 8 * SDG + NG * BC * J; i += NT) smem[i] = 0.0f;
+  for (int i = tid; i < 8 * SDG + 16 * BC * J; i += NT) smem[i] = 0.0f;
 
   // ---- W_hh^T tiles (waves 0-3): tile m = wv*MTWMAX + t, lane holds
   //      A[k = m*16 + (lane&15)][r = ks*32 + 8(lane>>4) + j] = W[row(r)][k]
@@ -1219,10 +1272,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   float dc_next = 0.0f, dh_dir = 0.0f;
   const float doutb = (cval && a.dOutB) ? a.dOutB[(long long)bg * 2 * H + d * H + cj] : 0.0f;
 
-  // partial-sum granules of this group: [2 slots][fast, safe][NG][BC][HG] x 8 B
+  // partial-sum granules of this group: [2 slots][hand-off, spare][NG][BC][HG] x 8 B; the
+  // spare copy of slot 1 holds the placement granules
   const int copy_g = NG * BC * HG;
   u64* xg = a.xbuf + (long long)group * 4 * copy_g;
   const __amdgpu_buffer_rsrc_t xr = granule_rsrc(xg, (unsigned)(4 * copy_g * 8));
+  __shared__ int s_wt;
+  if (tid == 0) __hip_atomic_store(xg + 3 * copy_g + w, (1ull << 32) | xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wv == WPOLL) {
+    const bool wt = group_needs_write_through(xg + 3 * copy_g, NG, lane, a.spin_limit, a.status, a.place_force);
+    if (lane == 0) s_wt = wt;
+  }
 
   // ---- prefetch waves WPF..7: per-step operands of every own (b, unit): 8 slots per cell
   //   0 dOut, 1..4 act, 5 c (LSTM) / h_prev (GRU), 6 c_prev (LSTM), 7 unused
@@ -1259,6 +1319,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   }
   if (wv >= WPF) ld.issue(d == 0 ? T - 1 : 0, T);
   __syncthreads();
+  const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
   STAMP_DECL
 
   if (wv >= WPOLL && wv < WPF) {
@@ -1278,11 +1339,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       loff[g] = on[g] ? pb * HG + (j0 >> 1) + 2 * qd : 0;  // granule offset within a copy
       doff[g] = on[g] ? pb * J + 4 * qd : 0;               // sdh[(p * BC + b) * J + u]
     }
-    bool safe = false;
     for (int s = 0; s < T; ++s) {
       if (s > 0) {
         const unsigned tag = (unsigned)s & 0xFFFFu;
-        const u64* src = xg + ((s - 1) & 1) * 2 * copy_g + (safe ? copy_g : 0);
+        const u64* src = xg + ((s - 1) & 1) * 2 * copy_g;
         u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
         unsigned done = 0;
 #pragma unroll
@@ -1321,10 +1381,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           if (++spins > a.spin_limit) {
             atomicOr(a.status, 2);
             return;
-          }
-          if (spins == FAST_SPINS && !safe) {
-            safe = true;
-            src += copy_g;
           }
         }
 #pragma unroll
@@ -1397,12 +1453,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 #pragma unroll
       for (int q = 0; q < NGATE; ++q) dgi[q] = dgh[q] = 0.0f;
       if (cval) {
-        float dh_rec = 0.0f;
-        if (s > 0) dh_rec = sum_partials(sdh + cb * J + cu, BC * J, NG);
         // two 16-B reads per lane: the 8-float operand record read as scalars is an 8-way
-        // bank conflict (lanes 32 B apart)
+        // bank conflict (lanes 32 B apart); issued first, with the 16 partial reads behind
+        // them in the same LDS round trip (sdh is zero before the first gather)
         const float4 o0 = *reinterpret_cast<const float4*>(sop + (s & 1) * BC * 32 * 8 + tid * 8);
         const float4 o1 = *reinterpret_cast<const float4*>(sop + (s & 1) * BC * 32 * 8 + tid * 8 + 4);
+        const float dh_rec = sum_partials16(sdh + cb * J + cu, BC * J);
         const float dout = o0.x + doutb;
         const float act[4] = {o0.y, o0.z, o0.w, o1.x};
         const float c = o1.y, cprev = o1.z, hprev = o1.y;
@@ -1463,12 +1519,19 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       for (int ks = 0; ks < KSRMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
       float* wsw = wsc + wv * BC * WSPAN;
       const int col = lane & 15;
+      // k-step-major over the wave's tiles: MTWMAX independent chains in flight
+      f32x4 acc[MTWMAX];
 #pragma unroll
-      for (int t2 = 0; t2 < MTWMAX; ++t2) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int t2 = 0; t2 < MTWMAX; ++t2) acc[t2] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < KSRMAX; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t2][ks], bv[ks], acc, 0, 0, 0);
-        if (col < BC) *reinterpret_cast<f32x4*>(wsw + col * WSPAN + t2 * 16 + 4 * (lane >> 4)) = acc;
+      for (int ks = 0; ks < KSRMAX; ++ks)
+#pragma unroll
+        for (int t2 = 0; t2 < MTWMAX; ++t2)
+          acc[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t2][ks], bv[ks], acc[t2], 0, 0, 0);
+      if (col < BC) {
+#pragma unroll
+        for (int t2 = 0; t2 < MTWMAX; ++t2)
+          *reinterpret_cast<f32x4*>(wsw + col * WSPAN + t2 * 16 + 4 * (lane >> 4)) = acc[t2];
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
@@ -1483,11 +1546,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           const float4 v = *reinterpret_cast<const float4*>(wsw + bb * WSPAN + (k - wv * WSPAN));
           const unsigned r0 = pack24(v.x), r1 = pack24(v.y), r2 = pack24(v.z), r3 = pack24(v.w);
           const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
-          const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules, fast copy
-          __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);                // fast: plain
-#ifndef DBG_FAST_ONLY  // diagnostic build: no safe copy (measures its cost; hangs if the fast copy is not seen)
-          __builtin_amdgcn_raw_buffer_store_b128(x, xr, (off + copy_g) * 8, 0, 16);    // safe: sc1
-#endif
+          const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules
+          if (wt)
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 16);  // sc1 write-through (group spans XCDs)
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);   // plain: stays in the group's L2
         }
       }
 #else
@@ -1516,11 +1579,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           const unsigned r0 = pack24(acc[t2][0]), r1 = pack24(acc[t2][1]), r2 = pack24(acc[t2][2]),
                          r3 = pack24(acc[t2][3]);
           const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
-          const int off = (((s & 1) * 2 * NG + w) * BC + col) * HG + (k >> 1);  // granules, fast copy
-          __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);                // fast: plain
-#ifndef DBG_FAST_ONLY  // diagnostic build: no safe copy (measures its cost; hangs if the fast copy is not seen)
-          __builtin_amdgcn_raw_buffer_store_b128(x, xr, (off + copy_g) * 8, 0, 16);    // safe: sc1
-#endif
+          const int off = (((s & 1) * 2 * NG + w) * BC + col) * HG + (k >> 1);  // granules
+          if (wt)
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 16);  // sc1 write-through (group spans XCDs)
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);   // plain: stays in the group's L2
         }
       }
 #endif
@@ -1668,7 +1731,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) 
     p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
     p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= (FWD_NPW == 3 ? 5 : FWD_NPW == 2 ? 6 : 7);
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
-    p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((NG * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16) + 2 * BC * 32 * 8);
+    p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((16 * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16) + 2 * BC * 32 * 8);
     p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
     return true;
   }
@@ -1740,9 +1803,11 @@ u64* g_stamps = nullptr;
 #endif
 
 unsigned g_spin_limit = SPIN_LIMIT;  // dl4ss_debug_set_spin_limit (tests force a hand-off timeout)
+int g_place_force = 0;               // dl4ss_debug_set_place_force (tests force write-through granules)
 
 void fill_args(RnnArgs& a, const Plan& p, int B, int T, int H) {
   a.spin_limit = g_spin_limit;
+  a.place_force = g_place_force;
 #if defined(RNN_STAMPS) || defined(RNN_TRACE)
   a.stamps = g_stamps;
 #endif
@@ -1801,6 +1866,10 @@ static long long handoff_bytes(const Plan& p, int H) {
 // the launch still completes).  0 restores the default (SPIN_LIMIT, ~1 s).  Test hook: a
 // tiny limit forces the timeout path that the Adam guard (dl4ss_adam_guarded) must catch.
 DL4SS_API void dl4ss_debug_set_spin_limit(unsigned limit) { g_spin_limit = limit ? limit : SPIN_LIMIT; }
+
+// 1: the packed kernels write every granule through (`sc1`) as if the group spanned XCDs (test
+// hook for the cross-XCD form); 0: plain stores wherever the group was found on one XCD.
+DL4SS_API void dl4ss_debug_set_place_force(int force) { g_place_force = force == 1 ? 1 : 0; }
 
 // The recurrence plan for (cell, B, H) under a co-residency budget of max_wg workgroups
 // (<= 0: the current device's, see wg_limit): info = {BC, NG, J, nchunk, grid}.  Host-only

@@ -131,6 +131,9 @@ long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
 int dl4ss_birnn_plan_info(int cell, int B, int H, int precision, int max_wg, int* info);
 /* Test hook: polls before a recurrence hand-off times out (0 = default, ~1 s of polling). */
 void dl4ss_debug_set_spin_limit(unsigned limit);
+/* Test hook: 1 = the packed (bf16) recurrence kernels write every hand-off granule through
+ * (`sc1`), as for a group whose workgroups span XCDs; 0 = by the placement found at launch. */
+void dl4ss_debug_set_place_force(int force);
 /* One layer, both directions: G (B,T,2,NG*H) = X W_ih^T + b_ih (NG = 4 LSTM / 3 GRU),
  * W_hh (2, NG*H, H), b_hh (2, NG*H) -> out (B,T,2H) [fwd | reverse], hprev (B,T,2H)
  * (h_{t-1} per step), act (B,T,2,4H) gate activations, cs (B,T,2,H) LSTM cells.

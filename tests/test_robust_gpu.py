@@ -54,3 +54,34 @@ def test_device_plan_within_residency_budget(dev):
     assert p is not None and p["grid"] <= cu - cu // 16
     if cu >= 256:
         assert p["grid"] == 240 and p["BC"] == 4
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_write_through_handoff_matches_plain(dev, cell):
+    """A recurrence group found on one XCD hands off with plain stores; one that spans XCDs
+    writes every granule through (`sc1`).  Forcing the write-through form
+    (dl4ss_debug_set_place_force) must give the bitwise-identical bf16 step from the same
+    saved state: only the transport differs, never a value.  (B = 4: 120 workgroups in groups
+    of 15, the same hand-offs as the B = 32 plan.)"""
+    B, K, N = 4, 2, 8000
+    lib = _lib.lib()
+    net = engine.SepNet(cell=cell, num_layers=2, device=dev, seed=11)
+    tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+    batch = _batch(dev, B, K, N, 21)
+    tr.step(*batch)  # GEMM plans and workspaces exist from here on
+    tr.check()
+    state = (net.flat.detach().clone(), tr.m.clone(), tr.v.clone(), tr.step_count)
+    out = []
+    for force in (0, 1):
+        net.flat.copy_(state[0]); tr.m.copy_(state[1]); tr.v.copy_(state[2]); tr.step_count = state[3]
+        lib.dl4ss_debug_set_place_force(force)
+        try:
+            loss = tr.step(*batch).clone()
+            tr.check()
+        finally:
+            lib.dl4ss_debug_set_place_force(0)
+        out.append((loss, net.grad.detach().clone(), net.flat.detach().clone()))
+    (l0, g0, p0), (l1, g1, p1) = out
+    assert torch.equal(l0, l1)
+    assert torch.equal(g0, g1)
+    assert torch.equal(p0, p1)

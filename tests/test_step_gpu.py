@@ -105,12 +105,14 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
         assert diff.max().item() <= 2.1 * 2e-4, name
         moved = diff > 1e-6
         if moved.any():
-            # Adam's first step is lr*g/(|g|+eps), i.e. sign-sensitive: a disagreeing weight must
-            # have a reference gradient no larger than that tensor's measured gradient error
-            # (itself <= tol_grad of the largest gradient), and such weights must be rare
+            # Adam's first step is lr*g/(|g|+eps): sign-sensitive, and for |g| near eps = 1e-8
+            # a 1e-11 change of g moves the weight by > 1e-6.  A disagreeing weight must have a
+            # reference gradient within that tensor's measured gradient error (itself <= tol_grad
+            # of the largest gradient) or within 10 eps, and such weights must be rare
             gr = grads_ref[name]
             err_abs = errs[name] * max(gr.abs().max().item(), 1e-30)
-            assert bool((gr.abs()[moved] <= err_abs).all()), (name, int(moved.sum()), gr[moved][:8])
+            lim = max(err_abs, 1e-7)
+            assert bool((gr.abs()[moved] <= lim).all()), (name, int(moved.sum()), gr[moved][:8])
             assert moved.float().mean().item() < 1e-2, name
 
 
@@ -226,14 +228,14 @@ def test_graph_step_matches_eager(dev, precision, mode):
         assert float(dp.max()) <= 2 * 2e-4 and int((dp > 1e-6).sum()) <= max(1, dp.numel() // 10000)
 
 
-@pytest.mark.parametrize("precision,mode", [("bf16", "pit"), ("bf16", "label")])
-def test_step_bitwise_reproducible(dev, precision, mode):
+@pytest.mark.parametrize("precision,mode,B", [("bf16", "pit", 4), ("bf16", "label", 4), ("bf16", "pit", 32)])
+def test_step_bitwise_reproducible(dev, precision, mode, B):
     """The bf16 throughput step: two steps from the same saved state on the same batch give
     bit-identical losses, gradients and parameters (every reduction has a fixed order; the
     BiRNN bias gradients go through per-row partials and bias_reduce_kernel, not float
     atomics).  The fp32 parity mode is not covered: its split-K GEMMs (gemm.hip) and
     fp32 BPTT accumulate with atomics."""
-    B, K, N = 4, 2, 8000
+    K, N = 2, 8000
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=9)
     src, spk, u = gen.batch(B)
     batch = (torch.from_numpy(src.astype(np.float32)).to(dev),
@@ -251,7 +253,8 @@ def test_step_bitwise_reproducible(dev, precision, mode):
         out.append((loss, net.grad.detach().clone(), net.flat.detach().clone()))
     (l0, g0, p0), (l1, g1, p1) = out
     assert torch.equal(l0, l1)
-    assert torch.equal(g0, g1)
+    diff = [n for n in net.named_parameters() if not torch.equal(net.view(n, g0), net.view(n, g1))]
+    assert not diff, diff
     assert torch.equal(p0, p1)
 
 
