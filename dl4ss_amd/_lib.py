@@ -29,6 +29,8 @@ SIGNATURES = {
     "dl4ss_f32_to_bf16": [P, P, LL, P],
     "dl4ss_f32_to_bf16_2d": [P, LL, I, I, P, LL, P],
     "dl4ss_colsum_bf16": [P, LL, I, I, P, P],
+    "dl4ss_colsum_bf16_part_bytes": [I, I],
+    "dl4ss_colsum_bf16_det": [P, LL, I, I, P, P, LL, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_bwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_mask_attn_loss_ex": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
@@ -66,7 +68,7 @@ SIGNATURES = {
     "dl4ss_debug_set_place_force": [ctypes.c_int],
 }
 # entry points that return a value rather than a hipError_t
-RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
+RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_colsum_bf16_part_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
             "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None,
             "dl4ss_debug_set_place_force": None}
 

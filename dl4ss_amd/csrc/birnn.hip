@@ -520,6 +520,15 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 static_assert(FWD_MV_CHAINS >= 1 && FWD_MV_CHAINS <= 8, "FWD_MV_CHAINS: 1..KSMAX accumulator chains");
 static_assert(FWD_NPW >= 1 && FWD_NPW <= 3, "FWD_NPW: 1..3 polling waves");
 static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
+// s_sleep units (64 clocks) a polling wave waits before its first sweep of a step: the own
+// workgroup's granules (every consumer gathers its own publish too) cannot land before the
+// cell / matvec phase that follows the barrier, so earlier sweeps only load the L2
+#ifndef FWD_POLL_DELAY
+#define FWD_POLL_DELAY 0
+#endif
+#ifndef BWD_POLL_DELAY
+#define BWD_POLL_DELAY 0
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
@@ -703,9 +712,47 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         const int base = ((s - 1) & 1) * 2 * slot_g * 8;  // the slot's hand-off copy (bytes)
         TRACE(2, s);
         // two sweeps in flight: the older one is merged while the newer one travels;
-        // a pair is taken from the first sweep that shows both its tags.  Relaxed agent
-        // atomic 8-B loads (global_load_dwordx2 sc1): unlike the buffer intrinsics they
-        // are never hoisted out of the spin loop or merged by the compiler.
+        // a pair is taken from the first sweep that shows both its tags.  One 16-B `sc1`
+        // buffer load per granule pair; the empty asm with a memory clobber before each
+        // sweep keeps the loads inside the spin loop (POLL8: 8-B relaxed agent atomics).
+#ifndef POLL8
+        u32x4 v[GLK], qa[GLK], qb[GLK];
+        unsigned done = 0;
+        if (FWD_POLL_DELAY > 0) __builtin_amdgcn_s_sleep(FWD_POLL_DELAY);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+        unsigned spins = 0;
+        while (true) {
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) qb[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((qa[g].y >> 16) == tag) & ((qa[g].w >> 16) == tag) & !((done >> g) & 1);
+            v[g] = m ? qa[g] : v[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+#ifdef RNN_TRACE
+          if (spins == 0) TRACE(3, s);
+#endif
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((qb[g].y >> 16) == tag) & ((qb[g].w >> 16) == tag) & !((done >> g) & 1);
+            v[g] = m ? qb[g] : v[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+          if (++spins > a.spin_limit) {
+            atomicOr(a.status, 1);
+            return;
+          }
+        }
+#else
         const u64* src = xg + (base >> 3);
         u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
         unsigned done = 0;
@@ -754,6 +801,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #pragma unroll
         for (int g = 0; g < GLK; ++g)
           v[g] = u32x4{(unsigned)lo[g], (unsigned)(lo[g] >> 32), (unsigned)hi[g], (unsigned)(hi[g] >> 32)};
+#endif
 #pragma unroll
         for (int g = 0; g < GLK; ++g) {
           const u32x4 x = v[g];
@@ -1342,6 +1390,56 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     for (int s = 0; s < T; ++s) {
       if (s > 0) {
         const unsigned tag = (unsigned)s & 0xFFFFu;
+        if (wv == WPOLL) TRACE(2, s);
+#ifndef POLL8  // POLL8: the round-1 8-B atomic loads (A/B builds)
+        // 16-B `sc1` buffer loads, one per granule pair (half the requests of the 8-B atomic
+        // loads: BPTT 4800 -> 4153, forward 3302 -> 3111 cycles per step); the empty asm with a
+        // memory clobber keeps every sweep inside the loop (the buffer intrinsic is a plain
+        // read-only load to the compiler: hoisted out of the spin loop without it)
+        const int sb = ((s - 1) & 1) * 2 * copy_g * 8;  // the slot's hand-off copy (bytes)
+        u32x4 q[GLK], qa[GLK], qb[GLK];
+        unsigned done = 0;
+        if (BWD_POLL_DELAY > 0) __builtin_amdgcn_s_sleep(BWD_POLL_DELAY);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, sb + loff[g] * 8, 0, 16);
+        unsigned spins = 0;
+        while (true) {
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) qb[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, sb + loff[g] * 8, 0, 16);
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((qa[g].y >> 16) == tag) & ((qa[g].w >> 16) == tag) & !((done >> g) & 1);
+            q[g] = m ? qa[g] : q[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, sb + loff[g] * 8, 0, 16);
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((qb[g].y >> 16) == tag) & ((qb[g].w >> 16) == tag) & !((done >> g) & 1);
+            q[g] = m ? qb[g] : q[g];
+            done |= (unsigned)m << g;
+          }
+          if (done == (1u << GLK) - 1) break;
+          if (++spins > a.spin_limit) {
+            atomicOr(a.status, 2);
+            return;
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) {
+          if (on[g]) {
+            const unsigned l0 = q[g].x, l1 = q[g].y, h0 = q[g].z, h1 = q[g].w;
+            const float4 v = make_float4(unpack24(l0 & 0xFFFFFFu), unpack24((l0 >> 24) | ((l1 & 0xFFFFu) << 8)),
+                                         unpack24(h0 & 0xFFFFFFu), unpack24((h0 >> 24) | ((h1 & 0xFFFFu) << 8)));
+            *reinterpret_cast<float4*>(sdh + doff[g]) = v;  // 16-B aligned: J % 4 == 0
+          }
+        }
+#else
         const u64* src = xg + ((s - 1) & 1) * 2 * copy_g;
         u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
         unsigned done = 0;
@@ -1393,6 +1491,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             *reinterpret_cast<float4*>(sdh + doff[g]) = v;  // 16-B aligned: J % 4 == 0
           }
         }
+#endif
+        if (wv == WPOLL) TRACE(1, s);
       }
       STAMP(0)
       __syncthreads();  // B1
@@ -1448,6 +1548,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     STAMP(0)
     __syncthreads();  // B1
     STAMP(1)
+    if (tid == 0) TRACE(3, s);
     if (tid < BC * 32) {
       float dgi[NGATE], dgh[NGATE];
 #pragma unroll
@@ -1553,6 +1654,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);   // plain: stays in the group's L2
         }
       }
+      if (wv == 3) TRACE(0, s);
 #else
       // the 16 x 16 accumulator lane holds 4 consecutive units 4(lane>>4) + i of batch column
       // lane & 15: one packed quad, published straight from the registers (every tile's MFMA

@@ -475,10 +475,13 @@ __global__ __launch_bounds__(256) void f32_to_bf16_multi_kernel(CvtSegs sg) {
 }
 
 // out[n] += sum_m A[m*lda + n] for bf16 A (bias gradients from bf16 dPre); VEC: 8 columns per
-// lane with 16-B loads (lda % 8 == 0, aligned base), a 64-lane row segment covers 512 columns
+// lane with 16-B loads (lda % 8 == 0, aligned base), a 64-lane row segment covers 512 columns.
+// part == nullptr: float atomics into out (order-dependent); else every row block stores its
+// sums to part[blockIdx.y][N] and colsum_reduce_kernel adds the blocks in fixed order.
 template <bool VEC>
 __global__ __launch_bounds__(256) void colsum_bf16_v_kernel(const unsigned short* __restrict__ A, long long lda, int M,
-                                                            int N, int rows_per_block, float* __restrict__ out) {
+                                                            int N, int rows_per_block, float* __restrict__ out,
+                                                            float* __restrict__ part) {
   constexpr int CPL = VEC ? 8 : 1;
   __shared__ float s[4][64 * CPL];
   const int c0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * CPL;
@@ -510,8 +513,23 @@ __global__ __launch_bounds__(256) void colsum_bf16_v_kernel(const unsigned short
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       const int l = (threadIdx.x & 63) * CPL + j;
-      if (c0 + j < N) atomicAdd(out + c0 + j, (s[0][l] + s[1][l]) + (s[2][l] + s[3][l]));
+      if (c0 + j >= N) continue;
+      const float v = (s[0][l] + s[1][l]) + (s[2][l] + s[3][l]);
+      if (part)
+        part[(long long)blockIdx.y * N + c0 + j] = v;
+      else
+        atomicAdd(out + c0 + j, v);
     }
+}
+
+// out[n] += sum_{y < nby} part[y][n], y in order (the deterministic colsum's second pass)
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int nby, int N,
+                                                            float* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f;
+  for (int y = 0; y < nby; ++y) a += part[(long long)y * N + n];
+  out[n] += a;
 }
 
 }  // namespace
@@ -535,19 +553,43 @@ DL4SS_API int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int 
   return 0;
 }
 
-DL4SS_API int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, void* stream) {
-  DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
-  if (M == 0 || N == 0) return 0;
+static int colsum_bf16_launch(const void* A, long long lda, int M, int N, float* out, float* part, void* stream) {
   const int rpb = 256;
   const auto* a = reinterpret_cast<const unsigned short*>(A);
   if (lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && lda >= ((N + 7) & ~7))  // 16-B rows, padding readable
     hipLaunchKernelGGL(colsum_bf16_v_kernel<true>, dim3(cdiv(N, 512), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
-                       a, lda, M, N, rpb, out);
+                       a, lda, M, N, rpb, out, part);
   else
     hipLaunchKernelGGL(colsum_bf16_v_kernel<false>, dim3(cdiv(N, 64), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
-                       a, lda, M, N, rpb, out);
+                       a, lda, M, N, rpb, out, part);
   DL4SS_CHECK_LAUNCH();
+  if (part) {
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cdiv(N, 256)), dim3(256), 0, as_stream(stream), part, cdiv(M, rpb), N,
+                       out);
+    DL4SS_CHECK_LAUNCH();
+  }
   return 0;
+}
+
+DL4SS_API int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, void* stream) {
+  DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
+  if (M == 0 || N == 0) return 0;
+  return colsum_bf16_launch(A, lda, M, N, out, nullptr, stream);
+}
+
+// Bytes of the partial-sum workspace dl4ss_colsum_bf16_det needs for an M x N operand.
+DL4SS_API long long dl4ss_colsum_bf16_part_bytes(int M, int N) {
+  return M > 0 && N > 0 ? (long long)cdiv(M, 256) * N * 4 : 0;
+}
+
+// Deterministic dl4ss_colsum_bf16: per-256-row-block partial sums, then a fixed-order reduce
+// (the bf16 step's Linear bias gradient: bitwise reproducible run to run).
+DL4SS_API int dl4ss_colsum_bf16_det(const void* A, long long lda, int M, int N, float* out, float* part,
+                                    long long part_bytes, void* stream) {
+  DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
+  if (M == 0 || N == 0) return 0;
+  DL4SS_REQUIRE(part && part_bytes >= dl4ss_colsum_bf16_part_bytes(M, N));
+  return colsum_bf16_launch(A, lda, M, N, out, part, stream);
 }
 
 DL4SS_API int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ldx, const int* rows,

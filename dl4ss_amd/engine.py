@@ -201,6 +201,9 @@ class SepTrainer:
             self.dGb = self.dGb2[0]
             self.dGhb = self.dGhb2[0] if self.dGhb2 else None
             self.dPreb = torch.empty(BT, p8(F * net.E), **bf)
+            # partial sums of the deterministic Linear-bias colsum (dl4ss_colsum_bf16_det)
+            pb = _lib.query("dl4ss_colsum_bf16_part_bytes", BT, F * net.E)
+            self.colsum_part = torch.empty(max(1, pb // 4), device=dev, dtype=torch.float32)
             self.Vb = torch.empty(BT, F * net.E, **bf)  # V = tanh(Linear) in bf16 (even row length)
             self.wb_ih = [torch.empty(2 * NGH, p8(F if l == 0 else 2 * H), **bf) for l in range(net.L)]
             self.wb_lin = torch.empty(F * net.E, p8(2 * H), **bf)
@@ -363,8 +366,9 @@ class SepTrainer:
                 ops.gemm_bf16_lt(dPreb, hLb, net.view("mix.Linear.weight", g), transA=True, beta=1.0)
             else:
                 ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
-            _lib.call("dl4ss_colsum_bf16", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
-                      _lib.ptr(net.view("mix.Linear.bias", g)), _lib.stream_ptr())
+            _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+                      _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part), self.colsum_part.numel() * 4,
+                      _lib.stream_ptr())
 
         on_side(linear_grads)
         hp8 = self.p8(H)

@@ -105,6 +105,11 @@ int dl4ss_gemm_bf16_set_tile(int tile);
 int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, void* stream);
 /* out[n] += sum_m A[m*lda + n] for a bf16 matrix A (bias gradient from bf16 dPre). */
 int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, void* stream);
+/* Deterministic form: per-256-row-block partials in part (dl4ss_colsum_bf16_part_bytes(M, N)
+ * bytes), then a fixed-order reduce into out (bitwise reproducible bias gradients). */
+long long dl4ss_colsum_bf16_part_bytes(int M, int N);
+int dl4ss_colsum_bf16_det(const void* A, long long lda, int M, int N, float* out, float* part, long long part_bytes,
+                          void* stream);
 /* n (<= 8) dl4ss_f32_to_bf16_2d conversions in one launch (host arrays of per-segment
  * arguments): the step's bf16 weight copies (W_ih of every layer, the Linear). */
 int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ldx, const int* rows, const int* cols,

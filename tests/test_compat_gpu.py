@@ -118,7 +118,9 @@ def test_top_k_mask_device_vs_oracle(dev):
 def test_prepare_data_contract_and_features(dev):
     import predata_multiAims_dB as pdb
 
-    config.BATCH_SIZE, config.MAX_LEN = 3, 8000
+    c = pdb.config  # config_WSJ0_dB (predata_multiAims_dB.py:7), a copy of config's constants
+    bs, ml = c.BATCH_SIZE, c.MAX_LEN
+    c.BATCH_SIZE, c.MAX_LEN = 3, 8000
     try:
         g = pdb.prepare_data('global', 'train')
         spk, d2i, i2d, T, F, frames, n = next(g)
@@ -145,7 +147,7 @@ def test_prepare_data_contract_and_features(dev):
                 # peak-normalised then gained: max|x| is 1 or the dB gain 10^(5/20 u) <= 1.78
                 assert 0.999 < np.abs(w).max() < 1.7783
     finally:
-        config.BATCH_SIZE, config.MAX_LEN = 16, 40000
+        c.BATCH_SIZE, c.MAX_LEN = bs, ml
 
 
 def test_fromlist_crm_loader(dev):

@@ -1,0 +1,3 @@
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out &&
+timeout -k 10 300 python -u -m pytest tests/test_step_gpu.py tests/test_compat_gpu.py tests/test_configs_full_gpu.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/t2.log 2>&1; [ $? -le 1 ] &&
+TAG=r02_prof_a bash tools/prof_round.sh

@@ -1,4 +1,4 @@
-"""Diagnostic: hand-off latency and producer skew of the packed forward BiRNN kernel.
+"""Diagnostic: hand-off latency and producer skew of the packed BiRNN kernels (fwd; `bwd`: BPTT).
 
 Builds a separate library with -DRNN_TRACE (never the shipped one); every workgroup
 records s_memrealtime (100 MHz) at its publish and at its completed poll, per step.
@@ -77,7 +77,7 @@ def main():
             lat.extend((seen[:, s] - last).tolist())
             step.append(float(pub[:, s].max() - pub[:, s - 1].max()))
             st0, first = tb[m, s, 2], tb[m, s, 3]
-            for i in range(len(m)):
+            for i in range(len(m) if not bwd else 0):
                 if first[i] > 0:
                     rtt.append(float(first[i] - st0[i]))
                 else:
@@ -87,11 +87,18 @@ def main():
     q = lambda v, p: sorted(v)[int(p * (len(v) - 1))]
     print(f"step period (max publish to max publish) ns: median {st.median(step):.0f}  p10 {q(step, .1):.0f}  p90 {q(step, .9):.0f}")
     print(f"publish skew across producers ns: median {st.median(skew):.0f}  p90 {q(skew, .9):.0f}")
-    if bwd:
+    if bwd:  # slots: 0 publish issued (wave 3), 1 poll complete (wave 4), 2 poll start, 3 cell start (after B1)
+        print(f"last publish -> poll complete (wave 4) ns: median {st.median(lat):.0f}  p10 {q(lat, .1):.0f}  "
+              f"p90 {q(lat, .9):.0f}  min {min(lat):.0f}")
+        b1 = []
+        for g in range(ngroups):
+            m = members[g]
+            for s in range(2, T - 1):
+                last = tb[m, s - 1, 0].max()
+                b1.extend((tb[m, s, 3] - last).tolist())
+        print(f"last publish -> cell start (B1 exit) ns: median {st.median(b1):.0f}  p90 {q(b1, .9):.0f}")
         cp = [float(tb[m, s, 0] - tb[m, s, 3]) for m in range(grid) for s in range(2, T - 1)]
-        print(f"bwd cell start (after B1) -> own publish done ns: median {st.median(cp):.0f}  p90 {q(cp, .9):.0f}")
-        pc = [float(tb[m, s, 3] - tb[m, s, 1]) for m in range(grid) for s in range(2, T - 1)]
-        print(f"bwd poll complete -> cell start ns: median {st.median(pc):.0f}")
+        print(f"cell start -> own publish issued ns: median {st.median(cp):.0f}  p90 {q(cp, .9):.0f}")
         return
     print(f"first sweep round trip (poll start -> first re-poll) ns: median {st.median(rtt):.0f} p90 {q(rtt, .9):.0f}; "
           f"polls satisfied by the first sweep: {nospin}")
