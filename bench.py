@@ -30,7 +30,26 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_FILE = "profiles/r01_prof_k_pmc.json"
+PMC_TAG = "r02_prof_b"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
+PMC_FILE = f"profiles/{PMC_TAG}_pmc.json"
+MFMA_FILE = f"profiles/{PMC_TAG}_mfma.json"
+
+
+def pmc_mfma_busy(kernel):
+    """MFMA-busy fraction of `kernel` (every instantiation, all its dispatches) from the
+    committed MFMA / LDS counter pass: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024
+    SIMDs); None if absent."""
+    try:
+        with open(os.path.join(ROOT, MFMA_FILE)) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, KeyError, ValueError):
+        return None
+    busy = gui = 0.0
+    for name, k in ks.items():
+        if name == kernel or name.startswith(kernel + "<"):
+            busy += k["counters"].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+            gui += k["counters"].get("GRBM_GUI_ACTIVE", 0.0)
+    return busy / (gui / 8 * 1024) if gui > 0 else None
 
 
 def stft_grid_threads(n_sig, T):
@@ -261,11 +280,13 @@ def main():
     bih = net.cat_view("bias_ih", 1)
     if tr.fast:
         xb, wb = tr.outb[0][:, :2 * net.H], tr.wb_ih[1][:, :2 * net.H]
-        run_gemm = lambda: ops.gemm_bf16(xb, wb, transB=True, bias=bih, out=tr.G)  # noqa: E731
-        gemm_name = "gemm_bb_kernel (bf16 operands, in-step BiLSTM layer-2 input projection 8032x2400x600 + bias)"
+        run_gemm = lambda: tr._gemm_fwd(xb, wb, bih, tr.G)  # noqa: E731
+        gemm_kernel = "gemm_gl_kernel<true, true, 0, false>" if tr.gemm_path == "gl" else "gemm_bb_kernel"
+        gemm_name = f"{gemm_kernel} (bf16 operands, in-step BiLSTM layer-2 input projection 8032x2400x600 + bias)"
     else:
         x, wih = tr.out[0].view(B * T, -1), net.cat_view("weight_ih", 1)
         run_gemm = lambda: ops.gemm(x, wih, transB=True, bias=bih, out=tr.G, precision=args.precision)  # noqa: E731
+        gemm_kernel = "gemm_kernel"
         gemm_name = "gemm_kernel (fp32 operands, BiLSTM layer-2 input projection 8032x2400x600 + bias)"
     for _ in range(3):
         run_gemm()
@@ -336,7 +357,8 @@ def main():
                                 "traffic_source": PMC_FILE, "launch_ms": stft_ms, "algorithmic_bytes": stft_bytes},
             "roofline_mfma": {"bound": "mfma", "kernel": gemm_name,
                               "achieved": gemm_tf, "peak": MFMA_PEAK[args.precision], "unit": "TFLOP/s",
-                              "frac": gemm_tf / MFMA_PEAK[args.precision], "launch_ms": gemm_ms},
+                              "frac": gemm_tf / MFMA_PEAK[args.precision], "launch_ms": gemm_ms,
+                              "mfma_busy": pmc_mfma_busy(gemm_kernel), "mfma_busy_source": MFMA_FILE},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args, N, K)

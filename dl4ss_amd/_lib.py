@@ -31,6 +31,8 @@ SIGNATURES = {
     "dl4ss_colsum_bf16": [P, LL, I, I, P, P],
     "dl4ss_colsum_bf16_part_bytes": [I, I],
     "dl4ss_colsum_bf16_det": [P, LL, I, I, P, P, LL, P],
+    "dl4ss_gemm_bf16_gl_ws_bytes": [I, I, I, I, I],
+    "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_bwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_mask_attn_loss_ex": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
@@ -68,7 +70,8 @@ SIGNATURES = {
     "dl4ss_debug_set_place_force": [ctypes.c_int],
 }
 # entry points that return a value rather than a hipError_t
-RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_colsum_bf16_part_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
+RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_colsum_bf16_part_bytes": ctypes.c_longlong,
+            "dl4ss_gemm_bf16_gl_ws_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
             "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None,
             "dl4ss_debug_set_place_force": None}
 

@@ -1,0 +1,390 @@
+// bf16-operand MFMA GEMM with LDS-DMA staging (gfx950): C[M,N] (fp32) (+)= op(A) . op(B)
+// (+ bias) (tanh / tanh -> bf16), both operands already bf16 in HBM -- the second
+// generation of gemm_bb.hip for the separation step's GEMMs.
+//
+// Why a new kernel: gemm_bb stages operands global -> VGPR -> ds_write_b128.  On gfx950 a
+// ds_write_b128 moves ~79 B/clk/CU (MI355X_MICROARCH.md, LDS table), so refilling two
+// 128 x 64 bf16 tiles per k-tile for two workgroups costs ~810 LDS cycles against 1024
+// MFMA cycles, on top of the fragment reads: the 128 x 128 tile was LDS-bound at ~350
+// TFLOP/s.  Here the tiles go global -> LDS by `global_load_lds_dwordx4` (LDS-DMA, no
+// VGPR round trip, no ds_write), four 1-KB wave instructions per operand per wave and
+// k-tile, double-buffered: the next k-tile's DMA is issued before the current tile's
+// fragment reads and MFMAs.
+//
+// Operands are described as A(m, k) and B(n, k) (C = A . B^T in those terms); each is
+// either KC (k contiguous: X[row * ld + k]) or KM (k-major: X[k * ld + row]).  LDS images
+// (lane-linear, so every swizzle is applied to the per-lane SOURCE address and to the
+// read, MI355X rule 21):
+//   KC: [128 rows][64 k], 128-B rows; 16-B chunk c of row r stored at c ^ ((r >> 1) & 7):
+//       the 16 rows of a ds_read_b128 lane group land on 16 distinct bank slots.
+//       Fragment of v_mfma_f32_16x16x32_bf16 (lane l: row l & 15, k 8 (l >> 4) .. +7):
+//       one ds_read_b128.
+//   KM: [64 k-rows][128 rows], 256-B k-rows; chunk c of k-row k stored at
+//       c ^ (((k & 3) << 2) | ((k >> 2) & 3)) (cdna_hip_programming.md T10, image (b)).
+//       Fragment: two ds_read_b64_tr_b16 (the hardware transpose read), 4 k each.
+// Waves: 4 x (64 x 64), 4 x 4 accumulators of 16 x 16 per wave, 32 MFMAs per k-tile.
+// k beyond K reads a zero line (g_zero_line) instead of the operand, so partial k-tiles
+// need no masking pass; rows beyond M / N read clamped addresses (their outputs are not
+// stored).  Split-K (grid.z) stores fp32 partial slabs that gemm_gl_reduce_kernel adds in
+// fixed order (deterministic, unlike the atomics of gemm_bb's split-K).
+#include "common.h"
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int IMG = BM * BK;  // bf16 elements per operand image (16 KB)
+enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2 };
+
+// 64 zero bytes every out-of-range k chunk is loaded from (16 B per lane)
+__device__ __attribute__((aligned(64))) const unsigned g_zero_line[16] = {0};
+
+__device__ __forceinline__ float ftanh_fast(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
+
+__device__ __forceinline__ int km_xor(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+
+// Per-lane source pointers of one operand's four DMA instructions (this wave's share of a
+// 128 x 64 tile) at k-tile start kbeg; advanced by `step` elements per k-tile.
+template <bool KC>
+struct Stager {
+  const unsigned short* src[4];
+  int kpos[4];  // k of this lane's chunk (KC) or k-row (KM) relative to the k-tile start
+  long long step;
+  __device__ __forceinline__ void init(const unsigned short* G, long long ld, int r0, int rmax, int kbeg, int wave,
+                                       int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave * 4 + i;  // 1-KB instruction index within the tile
+      if (KC) {
+        const int r = 8 * j + (lane >> 3), cp = lane & 7;
+        const int c = cp ^ ((r >> 1) & 7);
+        const int gr = min(r0 + r, rmax - 1);
+        src[i] = G + (long long)gr * ld + kbeg + 8 * c;
+        kpos[i] = 8 * c;
+      } else {
+        const int k = 4 * j + (lane >> 4), cp = lane & 15;
+        const int c = cp ^ km_xor(k);
+        int gc = r0 + 8 * c;
+        if (gc >= rmax) gc = 0;  // a chunk wholly past the last row: any valid address
+        src[i] = G + (long long)(kbeg + k) * ld + gc;
+        kpos[i] = k;
+      }
+    }
+    step = KC ? BK : (long long)BK * ld;
+  }
+  // issue this wave's four 1-KB DMAs of k-tile t (k0 = kbeg + t * BK) into image dst
+  __device__ __forceinline__ void issue(unsigned short* dst, int wave, int t, int k0_rel, int kspan) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool in = k0_rel + kpos[i] < kspan;
+      const void* p = in ? (const void*)(src[i] + t * step) : (const void*)g_zero_line;
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + (wave * 4 + i) * 512), 16, 0, 0);
+    }
+  }
+};
+
+// fragment (8 k-values of one row) of k-step kk (0, 1) for tile row `row` (0..127)
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int kk, int lane) {
+  if (KC) {
+    const int c = 4 * kk + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + row * BK + 8 * (c ^ ((row >> 1) & 7)));
+  } else {
+    // group g = lane >> 4 reads k-rows 32 kk + 8 g + 4 h + q (q = 0..3) for rows c0 .. c0 + 15,
+    // lane 4 q + p of the group addressing columns c0 + 4 p .. + 3 (c0 = row - (lane & 15))
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int c0 = row - (lane & 15);
+    bf16x4 h[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int k = 32 * kk + 8 * g + 4 * hh + q;
+      const int ch = ((c0 >> 3) + (p >> 1)) ^ km_xor(k);
+      h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + k * BM + 8 * ch + 4 * (p & 1)));
+    }
+    return bf16x8{h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool SPLIT>
+__global__ __launch_bounds__(NT, 2) void gemm_gl_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
+                                                        long long lda, const unsigned short* __restrict__ B,
+                                                        long long ldb, float* __restrict__ C, long long ldc,
+                                                        const float* __restrict__ bias, float beta, int k_per_split,
+                                                        int grid_m, int grid_n, long long sa, long long sb,
+                                                        long long sc, float* __restrict__ part) {
+  // one LDS array (a second __shared__ object can make hipcc drain vmcnt before every ds_read)
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * IMG];
+  A += blockIdx.y * sa;
+  B += blockIdx.y * sb;
+  C += blockIdx.y * sc;
+
+  // XCD-major grouped tile order (8 M-tiles x all N-tiles per group), bijective remap
+  const int ntiles = grid_m * grid_n;
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
+  if (tile >= ntiles) return;
+  constexpr int GROUP = 8;
+  const int gsize = GROUP * grid_n;
+  const int first_m = (tile / gsize) * GROUP;
+  const int gm_here = min(grid_m - first_m, GROUP);
+  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  if (kbeg >= kend) return;
+  const int kspan = kend - kbeg;
+  const int nk = (kspan + BK - 1) / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  Stager<A_KC> sa_;
+  Stager<B_KC> sb_;
+  sa_.init(A, lda, m0, M, kbeg, wave, lane);
+  sb_.init(B, ldb, n0, N, kbeg, wave, lane);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  sa_.issue(smem, wave, 0, 0, kspan);
+  sb_.issue(smem + IMG, wave, 0, 0, kspan);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned short* ia = smem + (kt & 1) * 2 * IMG;
+    const unsigned short* ib = ia + IMG;
+    if (kt + 1 < nk) {  // next k-tile's DMA into the other buffer (last read before the previous barrier)
+      unsigned short* na = smem + ((kt + 1) & 1) * 2 * IMG;
+      sa_.issue(na, wave, kt + 1, (kt + 1) * BK, kspan);
+      sb_.issue(na + IMG, wave, kt + 1, (kt + 1) * BK, kspan);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<A_KC>(ia, wm + 16 * i + (lane & 15), kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<B_KC>(ib, wn + 16 * j + (lane & 15), kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of k-tile kt + 1 landed
+    __syncthreads();  // ... and every wave's; every wave is done reading buffer kt & 1
+  }
+
+  // epilogue: acc[i][j][e] = C(wm + 16 i + 4 (lane >> 4) + e, wn + 16 j + (lane & 15)).  Each
+  // wave stages 32 rows (i = 2h, 2h + 1) of its 64 x 64 sub-tile at a time in LDS (free
+  // after the last barrier; 32 x 68 fp32 per wave) and writes rows back as 16-B stores.
+  constexpr int SLD = 68;
+  float* stage = reinterpret_cast<float*>(smem) + wave * 32 * SLD;
+  const int c4 = 4 * (lane & 15);
+  const int col = n0 + wn + c4;
+  const bool add_bias = !SPLIT && bias != nullptr;
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (add_bias) {
+    bv.x = col < N ? bias[col] : 0.f;
+    bv.y = col + 1 < N ? bias[col + 1] : 0.f;
+    bv.z = col + 2 < N ? bias[col + 2] : 0.f;
+    bv.w = col + 3 < N ? bias[col + 3] : 0.f;
+  }
+  // split-K slab of (batch member y, split z): part[y][z][M][N]
+  float* out = SPLIT ? part + ((long long)blockIdx.y * gridDim.z + blockIdx.z) * M * N : C;
+  const long long ldo = SPLIT ? N : ldc;
+  const bool vec_c = (ldo % 4 == 0) && ((((uintptr_t)out) & 15) == 0) && col + 4 <= N;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          stage[(16 * i2 + 4 * (lane >> 4) + e) * SLD + 16 * j + (lane & 15)] = acc[2 * h + i2][j][e];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll 4
+    for (int rr = 0; rr < 32; rr += 4) {
+      const int rl = rr + (lane >> 4);
+      const int row = m0 + wm + 32 * h + rl;
+      if (row >= M) continue;
+      float4 x = *reinterpret_cast<const float4*>(stage + rl * SLD + c4);
+      x.x += bv.x; x.y += bv.y; x.z += bv.z; x.w += bv.w;
+      if constexpr (EPI == EPI_TANH_BF16) {  // V of the Linear, written directly as bf16 pairs (ldc even)
+        unsigned short* cb = reinterpret_cast<unsigned short*>(C) + (long long)row * ldc + col;
+        const float xs[4] = {ftanh_fast(x.x), ftanh_fast(x.y), ftanh_fast(x.z), ftanh_fast(x.w)};
+        unsigned short hb[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const unsigned u = __float_as_uint(xs[c]);
+          hb[c] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+        }
+        if (col + 4 <= N) {  // two 4-B stores: ldc is only required even (V rows of F * E = 6450)
+          *reinterpret_cast<unsigned*>(cb) = hb[0] | ((unsigned)hb[1] << 16);
+          *reinterpret_cast<unsigned*>(cb + 2) = hb[2] | ((unsigned)hb[3] << 16);
+        } else {
+          for (int c = 0; c < 4 && col + c < N; ++c) cb[c] = hb[c];
+        }
+        continue;
+      }
+      float* cp = out + (long long)row * ldo + col;
+      if (vec_c) {
+        if (!SPLIT && beta != 0.0f) {
+          const float4 o = *reinterpret_cast<const float4*>(cp);
+          x.x += beta * o.x; x.y += beta * o.y; x.z += beta * o.z; x.w += beta * o.w;
+        }
+        if (EPI == EPI_TANH) { x.x = ftanh_fast(x.x); x.y = ftanh_fast(x.y); x.z = ftanh_fast(x.z); x.w = ftanh_fast(x.w); }
+        *reinterpret_cast<float4*>(cp) = x;
+      } else {
+        const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (col + c >= N) break;
+          float y = xs[c];
+          if (!SPLIT && beta != 0.0f) y += beta * cp[c];
+          if (EPI == EPI_TANH) y = ftanh_fast(y);
+          cp[c] = y;
+        }
+      }
+    }
+  }
+}
+
+// C[b] = beta C[b] + sum_{z < S} part[b][z] (+ bias), z in order: the split-K combine.  VEC:
+// four columns per thread with 16-B loads / stores (N % 4 == 0, ldc % 4 == 0, aligned C), the
+// S slab loads of a thread issued together (8 at a time) before they are summed in order.
+template <bool VEC>
+__global__ __launch_bounds__(256) void gemm_gl_reduce_kernel(int M, int N, int S, const float* __restrict__ part,
+                                                             float* __restrict__ C, long long ldc, long long sc,
+                                                             const float* __restrict__ bias, float beta) {
+  constexpr int W = VEC ? 4 : 1;
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * W;
+  const long long mn = (long long)M * N;
+  if (i >= mn) return;
+  const int b = blockIdx.y;
+  const float* p = part + (long long)b * S * mn + i;
+  const int r = (int)(i / N), c = (int)(i - (long long)r * N);
+  float* cp = C + b * sc + (long long)r * ldc + c;
+  if constexpr (VEC) {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z0 = 0; z0 < S; z0 += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = z0 + u < S ? *reinterpret_cast<const float4*>(p + (long long)(z0 + u) * mn) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (z0 + u < S) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+      }
+    }
+    if (bias) { a.x += bias[c]; a.y += bias[c + 1]; a.z += bias[c + 2]; a.w += bias[c + 3]; }
+    if (beta != 0.0f) {
+      const float4 o = *reinterpret_cast<const float4*>(cp);
+      a.x += beta * o.x; a.y += beta * o.y; a.z += beta * o.z; a.w += beta * o.w;
+    }
+    *reinterpret_cast<float4*>(cp) = a;
+  } else {
+    float a = 0.f;
+    for (int z = 0; z < S; ++z) a += p[(long long)z * mn];
+    if (bias) a += bias[c];
+    *cp = beta != 0.0f ? a + beta * *cp : a;
+  }
+}
+
+template <bool A_KC, bool B_KC>
+int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
+           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
+           long long sb, long long sc, float* ws, long long ws_bytes, hipStream_t st) {
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  int kps = (K + splitk - 1) / splitk;
+  kps = (kps + BK - 1) / BK * BK;
+  splitk = (K + kps - 1) / kps;
+  const int ntiles = gm * gn;
+  dim3 grid(ntiles, batch, splitk);
+  if (splitk > 1) {
+    if (epi != EPI_NONE) return (int)hipErrorInvalidValue;
+    const long long need = (long long)batch * splitk * M * N * 4;
+    if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, C,
+                       ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
+    DL4SS_CHECK_LAUNCH();
+    if (N % 4 == 0 && ldc % 4 == 0 && sc % 4 == 0 && ((uintptr_t)C & 15) == 0)
+      hipLaunchKernelGGL(gemm_gl_reduce_kernel<true>, dim3(cdiv((long long)M * N / 4, 256), batch), dim3(256), 0, st, M,
+                         N, splitk, ws, C, ldc, sc, bias, beta);
+    else
+      hipLaunchKernelGGL(gemm_gl_reduce_kernel<false>, dim3(cdiv((long long)M * N, 256), batch), dim3(256), 0, st, M, N,
+                         splitk, ws, C, ldc, sc, bias, beta);
+    DL4SS_CHECK_LAUNCH();
+    return 0;
+  }
+#define GGL_LAUNCH(EPI_)                                                                                            \
+  hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, C, \
+                     ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr)
+  if (epi == EPI_TANH) GGL_LAUNCH(EPI_TANH);
+  else if (epi == EPI_TANH_BF16) GGL_LAUNCH(EPI_TANH_BF16);
+  else GGL_LAUNCH(EPI_NONE);
+#undef GGL_LAUNCH
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+// Workspace bytes dl4ss_gemm_bf16_gl needs for a split-K launch (0 without split-K).
+DL4SS_API long long dl4ss_gemm_bf16_gl_ws_bytes(int M, int N, int K, int splitk, int batch) {
+  if (splitk <= 1 || M <= 0 || N <= 0 || K <= 0 || batch < 1) return 0;
+  int kps = (K + splitk - 1) / splitk;
+  kps = (kps + BK - 1) / BK * BK;
+  const int s = (K + kps - 1) / kps;
+  return s > 1 ? (long long)batch * s * M * N * 4 : 0;
+}
+
+// C = op(A) op(B) (+ bias) (epilogue), bf16 operands, the conventions of dl4ss_gemm_bf16_batched
+// (transA: A stored K x M; transB: B stored N x K).  Requires 16-B aligned operand rows (ld %
+// 8 == 0, aligned bases, strides % 8 == 0); returns hipErrorInvalidValue otherwise.  k-major
+// operands are bounded per k-row (exact for any K); a k-contiguous operand is read in 8-element
+// chunks, so with K % 8 != 0 its rows must hold zeros in [K, K rounded up to 8) (ld >= that):
+// the producers' zero-padded bf16 rows.  splitk > 1: deterministic split-K through ws
+// (dl4ss_gemm_bf16_gl_ws_bytes), EPI_NONE only.
+DL4SS_API int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                                 const void* B, long long ldb, float* C, long long ldc, const float* bias, int epilogue,
+                                 float beta, int splitk, int batch, long long strideA, long long strideB,
+                                 long long strideC, void* ws, long long ws_bytes, void* stream) {
+  DL4SS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && A && B && C && batch >= 1 && batch <= 65535);
+  if (M == 0 || N == 0) return 0;
+  DL4SS_REQUIRE(K > 0 && lda % 8 == 0 && ldb % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
+                strideA % 8 == 0 && strideB % 8 == 0);
+  if (splitk < 1) splitk = 1;
+  const bool a_kc = !transA, b_kc = transB;
+  const int k8 = (K + 7) & ~7;
+  DL4SS_REQUIRE(!a_kc || lda >= k8);
+  DL4SS_REQUIRE(!b_kc || ldb >= k8);
+  // split points fall on 64-element k boundaries: a chunk straddles K only in the last split
+  // a KM operand's rows are read in 16-B chunks: the row stride must cover the chunk past the last row
+  DL4SS_REQUIRE(a_kc || lda >= ((M + 7) & ~7));
+  DL4SS_REQUIRE(b_kc || ldb >= ((N + 7) & ~7));
+  if (epilogue == EPI_TANH_BF16)
+    DL4SS_REQUIRE(beta == 0.0f && splitk == 1 && (ldc & 1) == 0 && ((uintptr_t)C & 3) == 0);
+  hipStream_t st = as_stream(stream);
+  const auto* a = reinterpret_cast<const unsigned short*>(A);
+  const auto* b = reinterpret_cast<const unsigned short*>(B);
+  float* w = reinterpret_cast<float*>(ws);
+#define GGL_ARGS M, N, K, a, lda, b, ldb, C, ldc, bias, epilogue, beta, splitk, batch, strideA, strideB, strideC, w, ws_bytes, st
+  if (a_kc && b_kc) return launch<true, true>(GGL_ARGS);
+  if (a_kc && !b_kc) return launch<true, false>(GGL_ARGS);
+  if (!a_kc && b_kc) return launch<false, true>(GGL_ARGS);
+  return launch<false, false>(GGL_ARGS);
+#undef GGL_ARGS
+}

@@ -178,13 +178,18 @@ class SepTrainer:
         # kernel writes bf16 dPre, the weights and the layer-0 features are converted once per
         # step.  Rows are padded to multiples of 8 (16-B aligned operand rows).
         self.fast = precision == "bf16" and self.rnn_precision == "bf16"
-        # bf16 mode: the plain backward GEMMs through hipBLASLt (DL4SS_GEMM_LT=0: the hand-written kernel)
-        self.use_lt = self.fast and os.environ.get("DL4SS_GEMM_LT", "1") != "0"
+        # bf16 mode GEMM path (DL4SS_GEMM): "gl" (default) every GEMM of the step on the
+        # hand-written LDS-DMA kernel (gemm_gl.hip; deterministic split-K); "lt" the round-1
+        # form: forward on gemm_bb.hip, plain backward GEMMs through hipBLASLt; "bb" all on gemm_bb
+        self.gemm_path = os.environ.get("DL4SS_GEMM", "gl") if self.fast else "bb"
+        if self.gemm_path not in ("gl", "lt", "bb"):
+            raise ValueError(f"DL4SS_GEMM={self.gemm_path}: expected gl, lt or bb")
+        self.use_lt = self.gemm_path == "lt"
         # DL4SS_OVERLAP=1: weight-gradient GEMMs of layer l on a side stream, concurrent with the
         # BPTT of layer l-1.  Off by default: measured 6.89 vs 6.41 ms per step -- the GEMM
         # workgroups share CUs with the persistent recurrence and slow every hand-off more
         # than the hidden GEMM time saves.
-        self.overlap = self.use_lt and os.environ.get("DL4SS_OVERLAP", "0") == "1"
+        self.overlap = self.gemm_path != "bb" and os.environ.get("DL4SS_OVERLAP", "0") == "1"
         self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
@@ -200,7 +205,17 @@ class SepTrainer:
             self.dGhb2 = [torch.empty(BT, 2 * NGH, **bf) for _ in range(2)] if net.cell == "gru" else None
             self.dGb = self.dGb2[0]
             self.dGhb = self.dGhb2[0] if self.dGhb2 else None
-            self.dPreb = torch.empty(BT, p8(F * net.E), **bf)
+            # zero row padding (never written): gemm_gl reads k-contiguous rows in 8-element chunks
+            self.dPreb = torch.zeros(BT, p8(F * net.E), **bf)
+            # gemm_gl split-K slabs (the largest split of _backward_fast: dH at 3; the side stream
+            # of DL4SS_OVERLAP gets its own)
+            FE_ = F * net.E
+            gl_need = max(_lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, FE_, 3, 1),
+                          _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", FE_, 2 * H, BT, 2, 1),
+                          _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", 2 * NGH, 2 * H, BT, 4, 1),
+                          _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", NGH, H, BT, 8, 2))
+            self.gl_ws = torch.empty(max(gl_need, 1), device=dev, dtype=torch.uint8)
+            self.gl_ws_side = torch.empty_like(self.gl_ws) if self.overlap else self.gl_ws
             # partial sums of the deterministic Linear-bias colsum (dl4ss_colsum_bf16_det)
             pb = _lib.query("dl4ss_colsum_bf16_part_bytes", BT, F * net.E)
             self.colsum_part = torch.empty(max(1, pb // 4), device=dev, dtype=torch.float32)
@@ -257,7 +272,7 @@ class SepTrainer:
         xb = self.xb0[:, :x.shape[1]]
         for l in range(net.L):
             D = xb.shape[1]
-            ops.gemm_bf16(xb, self.wb_ih[l][:, :D], transB=True, bias=net.cat_view("bias_ih", l), out=self.G)
+            self._gemm_fwd(xb, self.wb_ih[l][:, :D], net.cat_view("bias_ih", l), self.G)
             hp = self.hprev[l]
             _lib.call("dl4ss_birnn_fwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(self.G),
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
@@ -265,8 +280,12 @@ class SepTrainer:
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.outb[l]), _lib.ptr(self.hprevb[l]),
                       _lib.ptr(self._ws_slot(l, False)), self.ws_bytes, _lib.ptr(self.status), st)
             xb = self.outb[l][:, :2 * H]
-        ops.gemm_bf16(xb, self.wb_lin[:, :2 * H], transB=True, bias=net.view("mix.Linear.bias"),
-                      epilogue=ops.EPI_TANH_BF16, out=self.Vb)
+        self._gemm_fwd(xb, self.wb_lin[:, :2 * H], net.view("mix.Linear.bias"), self.Vb, ops.EPI_TANH_BF16)
+
+    def _gemm_fwd(self, x, w, bias, out, epilogue=ops.EPI_NONE):
+        """out = x w^T + bias (epilogue): the input projections and the Linear (+ tanh -> bf16 V)"""
+        f = ops.gemm_bf16_gl if self.gemm_path == "gl" else ops.gemm_bf16
+        f(x, w, transB=True, bias=bias, epilogue=epilogue, out=out)
 
     def forward(self, feats=None):
         net, B, T, H = self.net, self.B, self.T, self.net.H
@@ -355,14 +374,23 @@ class SepTrainer:
             with torch.cuda.stream(self.side):
                 fn()
 
+        gl = self.gemm_path == "gl"
+        # gemm_gl split-K factors, measured per shape at C2 (tools/gemm_gl_bench.py --sweep): dH
+        # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
+        # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
         dH = self.dH[0]
-        if lt:
+        if gl:
+            ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk=3, ws=self.gl_ws)  # input gradient first
+        elif lt:
             ops.gemm_bf16_lt(dPreb, self.wb_lin[:, :2 * H], dH)  # the input gradient first: BPTT waits on it
         else:
             ops.gemm_bf16(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk="auto")
 
         def linear_grads():
-            if lt:
+            if gl:
+                ops.gemm_bf16_gl(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk=2,
+                                 ws=self.gl_ws_side)
+            elif lt:
                 ops.gemm_bf16_lt(dPreb, hLb, net.view("mix.Linear.weight", g), transA=True, beta=1.0)
             else:
                 ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
@@ -387,7 +415,9 @@ class SepTrainer:
                       _lib.ptr(self.status), st)
             if l > 0:  # the input gradient first: it is all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
-                if lt:
+                if gl:
+                    ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next)
+                elif lt:
                     ops.gemm_bf16_lt(dGb, self.wb_ih[l][:, :2 * H], dH_next)
                 else:
                     ops.gemm_bf16(dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")
@@ -396,7 +426,17 @@ class SepTrainer:
             def weight_grads(l=l, dGb=dGb, dGhb=dGhb, xb=xb):
                 whh_g = net.cat_view("weight_hh", l, g)
                 # both directions' dW_hh in one launch: member d = columns d*NGH of dGh, d*pad8(H) of h_{t-1}
-                if lt:
+                if gl:
+                    ops.gemm_bf16_gl(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), beta=1.0, splitk=4,
+                                     ws=self.gl_ws_side)
+                    if NGH % 8 == 0:
+                        ops.gemm_bf16_gl(dGhb[:, :NGH], self.hprevb[l][:, :H], transA=True, out=whh_g[:NGH],
+                                         beta=1.0, splitk=8, batch=2, strideA=NGH, strideB=hp8, strideC=NGH * H,
+                                         M=NGH, N=H, K=BT, ws=self.gl_ws_side)
+                    else:  # GRU (NGH = 900): the reverse direction's columns are not 16-B aligned for LDS-DMA
+                        ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
+                                              NGH, H, BT, transA=True, beta=1.0, splitk="auto")
+                elif lt:
                     ops.gemm_bf16_lt(dGb, xb, net.cat_view("weight_ih", l, g), transA=True, beta=1.0)
                     ops.gemm_bf16_lt(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], transA=True, beta=1.0,
                                      batch=2, strideA=NGH, strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT)

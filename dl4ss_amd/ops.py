@@ -141,6 +141,7 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
 
 
 GEMM_BF16_TARGET_WGS = 256  # measured best on MI355X (tools/gemm_bench_bf16.py sweep: 256/512/768)
+GEMM_GL_TARGET_WGS = 512  # gemm_gl (2 workgroups per CU): split-K to about two per CU
 
 
 def gemm_bf16_set_tile(tile):
@@ -191,6 +192,61 @@ def gemm_bf16(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, be
     _lib.call("dl4ss_gemm_bf16", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
               _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue,
               float(beta), int(splitk), _lib.stream_ptr())
+    return out
+
+
+_gl_ws = {}
+
+
+def _gl_workspace(dev, nbytes):
+    """split-K slab workspace of dl4ss_gemm_bf16_gl, one per device and stream, grown on demand
+    (never inside a graph capture: the eager warm-up step sizes it)"""
+    key = (dev, torch.cuda.current_stream().cuda_stream)
+    ws = _gl_ws.get(key)
+    if ws is None or ws.numel() < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("gemm_bf16_gl: split-K workspace must be sized before graph capture")
+        ws = _gl_ws[key] = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+    return ws
+
+
+def gemm_bf16_gl(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.0, out=None, splitk=1,
+                 batch=1, strideA=0, strideB=0, strideC=0, M=None, N=None, K=None, ws=None):
+    """out (fp32, or bf16 with EPI_TANH_BF16) = op(A) @ op(B) (+ bias) (epilogue) (+ beta*out)
+    with bf16 A and B through the LDS-DMA MFMA kernel (dl4ss_gemm_bf16_gl, gemm_gl.hip).
+    Layout conventions as gemm_bf16; split-K is deterministic (fp32 slabs + fixed-order
+    reduce); batch > 1 takes raw element strides from the first-member views.  ws: the
+    caller's split-K workspace (a uint8 tensor), else a per-device/stream one grown on demand."""
+    _mat_bf16(A, "gemm_bf16_gl(A)")
+    _mat_bf16(B, "gemm_bf16_gl(B)")
+    if M is None:
+        M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
+        Kb, N = (B.shape[1], B.shape[0]) if transB else (B.shape[0], B.shape[1])
+        if K != Kb:
+            raise RuntimeError(f"gemm_bf16_gl: inner dims differ ({K} vs {Kb})")
+    if out is None:
+        if beta != 0.0:
+            raise RuntimeError("gemm_bf16_gl: accumulation needs an output tensor")
+        out = torch.empty(M, N, device=A.device,
+                          dtype=torch.bfloat16 if epilogue == EPI_TANH_BF16 else torch.float32)
+    if epilogue == EPI_TANH_BF16:
+        _mat_bf16(out, "gemm_bf16_gl(out, bf16 epilogue)")
+    else:
+        _mat(out, "gemm_bf16_gl(out)")
+    if batch == 1 and tuple(out.shape) != (M, N):
+        raise RuntimeError(f"gemm_bf16_gl: out shape {tuple(out.shape)} != {(M, N)}")
+    if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
+        raise RuntimeError("gemm_bf16_gl: bias must be contiguous with N elements")
+    if splitk == "auto":
+        splitk = auto_splitk(M, N, K, target_wgs=max(1, GEMM_GL_TARGET_WGS // batch)) if epilogue == EPI_NONE else 1
+    nb = _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", M, N, K, int(splitk), int(batch))
+    if nb > 0 and ws is not None and ws.numel() < nb:
+        raise RuntimeError(f"gemm_bf16_gl: workspace of {ws.numel()} bytes < {nb}")
+    ws = (ws if ws is not None else _gl_workspace(A.device, nb)) if nb > 0 else None
+    _lib.call("dl4ss_gemm_bf16_gl", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
+              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue,
+              float(beta), int(splitk), int(batch), int(strideA), int(strideB), int(strideC), _lib.ptr(ws),
+              ws.numel() if ws is not None else 0, _lib.stream_ptr())
     return out
 
 

@@ -90,6 +90,17 @@ int dl4ss_gemm_bf16_batched(int transA, int transB, int M, int N, int K, const v
                             long long strideC, void* stream);
 /* y[i] = bf16(x[i]) (round to nearest even), n elements; x 16-B aligned, y 8-B aligned. */
 int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream);
+/* bf16-operand GEMM with LDS-DMA staging (gemm_gl.hip; replaces hipBLASLt and gemm_bb on the
+ * step's GEMMs): semantics of dl4ss_gemm_bf16_batched plus a deterministic split-K (fp32
+ * slabs in ws, dl4ss_gemm_bf16_gl_ws_bytes bytes, then a fixed-order reduce; EPI_NONE only).
+ * Needs lda / ldb / strides % 8 == 0, 16-B aligned A / B, for a k-major operand a row stride
+ * >= its row count rounded up to 8, and for a k-contiguous one a row stride >= K rounded up
+ * to 8 with zeros in that padding; hipErrorInvalidValue otherwise. */
+long long dl4ss_gemm_bf16_gl_ws_bytes(int M, int N, int K, int splitk, int batch);
+int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
+                       long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta,
+                       int splitk, int batch, long long strideA, long long strideB, long long strideC, void* ws,
+                       long long ws_bytes, void* stream);
 /* Plain bf16-operand GEMM (no epilogue) through hipBLASLt: the backward pass's weight /
  * input gradients (dW_lin, dH, dW_ih, dW_hh, dX of EvalVer.py:673's autograd).  Semantics
  * of dl4ss_gemm_bf16_batched with epilogue NONE and no split-K; workspace (may be NULL when

@@ -101,6 +101,34 @@ def main(src, tag, out="profiles", warmup=1, steps=3):
                   "| kernel | dispatches | avg MB / launch |", "|---|---|---|"]
         for k, v in sorted(res.items(), key=lambda kv: -kv[1]["avg_traffic_bytes"]):
             lines.append(f"| `{k}` | {v['dispatches']} | {v['avg_traffic_bytes'] / 1e6:.2f} |")
+    # MFMA / LDS counter pass (pmc_mfma): per kernel, MFMA-busy fraction of the CU-SIMD cycles
+    # the kernel held = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), and
+    # LDS bank-conflict cycles as a share of all LDS-array cycles (MI355X_MICROARCH.md §LDS)
+    f = os.path.join(src, "pmc_mfma", "run_counter_collection.csv")
+    if os.path.exists(f):
+        acc = collections.defaultdict(lambda: collections.defaultdict(float))
+        cnt = collections.defaultdict(int)
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                cnt[k] += 1
+        mf = {}
+        for k, d in acc.items():
+            gui = d.get("GRBM_GUI_ACTIVE", 0.0)
+            if gui <= 0:
+                continue
+            mf[k] = {"dispatches": cnt[k],
+                     "mfma_busy_frac": d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (gui / 8 * 1024),
+                     "lds_bank_conflict_frac": d.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, d.get("SQ_LDS_IDX_ACTIVE", 0.0)),
+                     "counters": dict(d)}
+        json.dump({"source": src, "formula": "MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)", "kernels": mf},
+                  open(os.path.join(out, f"{tag}_mfma.json"), "w"), indent=1)
+        lines += ["", "## MFMA busy and LDS bank conflicts (PMC pass pmc_mfma)", "",
+                  "| kernel | dispatches | MFMA busy | LDS conflict cycles / LDS cycles |", "|---|---|---|---|"]
+        for k, v in sorted(mf.items(), key=lambda kv: -kv[1]["counters"].get("SQ_VALU_MFMA_BUSY_CYCLES", 0)):
+            if v["counters"].get("SQ_VALU_MFMA_BUSY_CYCLES", 0) > 0:
+                lines.append(f"| `{k}` | {v['dispatches']} | {v['mfma_busy_frac']:.3f} | {v['lds_bank_conflict_frac']:.3f} |")
     open(os.path.join(out, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines[:40]))
 
