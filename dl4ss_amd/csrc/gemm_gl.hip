@@ -110,15 +110,19 @@ __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int k
   }
 }
 
-template <bool A_KC, bool B_KC, int EPI, bool SPLIT>
-__global__ __launch_bounds__(NT, 2) void gemm_gl_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
+// STG LDS stages: 2 = double buffer, one k-tile of DMA in flight, vmcnt(0) + __syncthreads per
+// k-tile, 64 KB (two workgroups per CU); 3 = two k-tiles in flight across a raw s_barrier with
+// a counted vmcnt (the wave's 8 DMAs of the newest tile may stay outstanding), 96 KB (one
+// workgroup per CU).
+template <bool A_KC, bool B_KC, int EPI, bool SPLIT, int STG>
+__global__ __launch_bounds__(NT, STG == 2 ? 2 : 1) void gemm_gl_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
                                                         long long lda, const unsigned short* __restrict__ B,
                                                         long long ldb, float* __restrict__ C, long long ldc,
                                                         const float* __restrict__ bias, float beta, int k_per_split,
                                                         int grid_m, int grid_n, long long sa, long long sb,
                                                         long long sc, float* __restrict__ part) {
   // one LDS array (a second __shared__ object can make hipcc drain vmcnt before every ds_read)
-  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * 2 * IMG];
+  __shared__ __attribute__((aligned(16))) unsigned short smem[STG * 2 * IMG];
   A += blockIdx.y * sa;
   B += blockIdx.y * sb;
   C += blockIdx.y * sc;
@@ -155,18 +159,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_gl_kernel(int M, int N, int K, con
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  sa_.issue(smem, wave, 0, 0, kspan);
-  sb_.issue(smem + IMG, wave, 0, 0, kspan);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned short* ia = smem + (kt & 1) * 2 * IMG;
+  auto compute = [&](const unsigned short* ia) {
     const unsigned short* ib = ia + IMG;
-    if (kt + 1 < nk) {  // next k-tile's DMA into the other buffer (last read before the previous barrier)
-      unsigned short* na = smem + ((kt + 1) & 1) * 2 * IMG;
-      sa_.issue(na, wave, kt + 1, (kt + 1) * BK, kspan);
-      sb_.issue(na + IMG, wave, kt + 1, (kt + 1) * BK, kspan);
-    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[4], bfr[4];
@@ -179,8 +173,37 @@ __global__ __launch_bounds__(NT, 2) void gemm_gl_kernel(int M, int N, int K, con
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of k-tile kt + 1 landed
-    __syncthreads();  // ... and every wave's; every wave is done reading buffer kt & 1
+  };
+  auto dma = [&](int t) {  // this wave's 8 DMAs of k-tile t into LDS stage t % STG
+    unsigned short* na = smem + (t % STG) * 2 * IMG;
+    sa_.issue(na, wave, t, t * BK, kspan);
+    sb_.issue(na + IMG, wave, t, t * BK, kspan);
+  };
+  if constexpr (STG == 2) {
+    dma(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) dma(kt + 1);  // into the other buffer (last read before the previous barrier)
+      compute(smem + (kt & 1) * 2 * IMG);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of k-tile kt + 1 landed
+      __syncthreads();  // ... and every wave's; every wave is done reading buffer kt & 1
+    }
+  } else {
+    dma(0);
+    if (nk > 1) dma(1);
+    for (int kt = 0; kt < nk; ++kt) {
+      // this wave's DMAs of tile kt landed (tile kt + 1's 8 may stay in flight), then the raw
+      // barrier: every wave's tile kt landed and every wave is done reading tile kt - 1's stage
+      if (kt + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) dma(kt + 2);  // into the stage tile kt - 1 used
+      compute(smem + (kt % 3) * 2 * IMG);
+    }
+    __syncthreads();  // every wave is done with the stages before the epilogue reuses LDS
   }
 
   // epilogue: acc[i][j][e] = C(wm + 16 i + 4 (lane >> 4) + e, wn + 16 j + (lane & 15)).  Each
@@ -303,6 +326,8 @@ __global__ __launch_bounds__(256) void gemm_gl_reduce_kernel(int M, int N, int S
   }
 }
 
+int g_gl_stages = 0;  // 0: per-shape default (2); DL4SS_GL_STAGES / dl4ss_gemm_gl_set_stages for A/B runs
+
 template <bool A_KC, bool B_KC>
 int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
            float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
@@ -317,8 +342,12 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
     if (epi != EPI_NONE) return (int)hipErrorInvalidValue;
     const long long need = (long long)batch * splitk * M * N * 4;
     if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, C,
-                       ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
+    if (g_gl_stages == 3)
+      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true, 3>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb,
+                         C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
+    else
+      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true, 2>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb,
+                         C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
     DL4SS_CHECK_LAUNCH();
     if (N % 4 == 0 && ldc % 4 == 0 && sc % 4 == 0 && ((uintptr_t)C & 15) == 0)
       hipLaunchKernelGGL(gemm_gl_reduce_kernel<true>, dim3(cdiv((long long)M * N / 4, 256), batch), dim3(256), 0, st, M,
@@ -329,9 +358,15 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
     DL4SS_CHECK_LAUNCH();
     return 0;
   }
-#define GGL_LAUNCH(EPI_)                                                                                            \
-  hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_, false>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, C, \
-                     ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr)
+#define GGL_LAUNCH(EPI_)                                                                                              \
+  do {                                                                                                              \
+    if (g_gl_stages == 3)                                                                                           \
+      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_, false, 3>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, \
+                         C, ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr);                                      \
+    else                                                                                                            \
+      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_, false, 2>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, \
+                         C, ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr);                                      \
+  } while (0)
   if (epi == EPI_TANH) GGL_LAUNCH(EPI_TANH);
   else if (epi == EPI_TANH_BF16) GGL_LAUNCH(EPI_TANH_BF16);
   else GGL_LAUNCH(EPI_NONE);
@@ -341,6 +376,13 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
 }
 
 }  // namespace
+
+// Tuning knob (tools/gemm_gl_bench.py): LDS stages of gemm_gl (2 or 3; 0 = default).
+DL4SS_API int dl4ss_gemm_gl_set_stages(int stages) {
+  DL4SS_REQUIRE(stages == 0 || stages == 2 || stages == 3);
+  g_gl_stages = stages;
+  return 0;
+}
 
 // Workspace bytes dl4ss_gemm_bf16_gl needs for a split-K launch (0 without split-K).
 DL4SS_API long long dl4ss_gemm_bf16_gl_ws_bytes(int M, int N, int K, int splitk, int batch) {

@@ -8,7 +8,7 @@ import sys
 import torch
 
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
-from dl4ss_amd import ops  # noqa: E402
+from dl4ss_amd import _lib, ops  # noqa: E402
 
 dev = torch.device("cuda")
 BT, H, F, E = 8032, 300, 129, 50
@@ -73,8 +73,15 @@ for name, (flop, kw) in shapes.items():
     ta, tb = kw.get("transA", False), kw.get("transB", False)
     epi = kw.get("epilogue", ops.EPI_NONE)
     beta = kw.get("beta", 0.0)
+    SPLIT = {"dH": 3, "dW_lin": 2, "dX": 1, "dW_ih": 4, "dW_ih0": 4}.get(name.split()[0], 1)
+
+    def gl(stages):
+        def f():
+            _lib.call("dl4ss_gemm_gl_set_stages", stages)
+            ops.gemm_bf16_gl(A, B, out=out, splitk=SPLIT, **kw)
+        return f
     paths = {"gemm_bb": lambda: ops.gemm_bf16(A, B, out=out, splitk="auto" if beta == 1.0 else 1, **kw),
-             "gemm_gl": lambda: ops.gemm_bf16_gl(A, B, out=out, splitk="auto" if beta == 1.0 else 1, **kw)}
+             "gemm_gl": gl(2), "gemm_gl_3stage": gl(3)}
     if epi == ops.EPI_NONE and kw.get("bias") is None:
         paths["hipblaslt"] = lambda: ops.gemm_bf16_lt(A, B, out, transA=ta, transB=tb, beta=beta)
     for pname, fn in paths.items():
@@ -89,10 +96,11 @@ flop = 2 * BT * 1200 * H * 2
 fns = {"gemm_bb": lambda: ops.gemm_bf16_batched(dG[:, :1200], hp[:, :H], dWhh[:1200], 2, 1200, p8(H), 1200 * H, 1200,
                                                 H, BT, transA=True, beta=1.0, splitk="auto"),
        "gemm_gl": lambda: ops.gemm_bf16_gl(dG[:, :1200], hp[:, :H], transA=True, out=dWhh[:1200], beta=1.0,
-                                           splitk="auto", batch=2, strideA=1200, strideB=p8(H), strideC=1200 * H,
+                                           splitk=8, batch=2, strideA=1200, strideB=p8(H), strideC=1200 * H,
                                            M=1200, N=H, K=BT),
        "hipblaslt": lambda: ops.gemm_bf16_lt(dG[:, :1200], hp[:, :H], dWhh[:1200], transA=True, beta=1.0, batch=2,
                                              strideA=1200, strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT)}
+_lib.call("dl4ss_gemm_gl_set_stages", 0)
 for pname, fn in fns.items():
     us = timeit(fn)
     print(json.dumps({"shape": "dW_hh 2x1200x300x8032", "path": pname, "us": round(us, 2),
