@@ -39,9 +39,11 @@ def _time(fn, steps, warmup):
 
 
 def train_config(name, cell, L, B, K, N, mode, precision, steps, warmup, loss_channels=None, adjust=True,
-                 eval_istft=False):
+                 eval_istft=False, emb_scale=1.0):
     dev = torch.device("cuda")
     net = engine.SepNet(cell=cell, num_layers=L, crm=mode == "crm", adjust=adjust, device=dev, seed=1)
+    if emb_scale != 1.0:  # the query embedding (N(0,1) rows at init) scaled: logits stay below saturation
+        net.view("emb.layer.weight").mul_(emb_scale)
     tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision, loss_channels=loss_channels)
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1)
     src, spk, u = gen.batch(B)
@@ -61,11 +63,24 @@ def train_config(name, cell, L, B, K, N, mode, precision, steps, warmup, loss_ch
                       _lib.stream_ptr())
         return loss
 
-    dt, loss = _time(step, steps, warmup)
+    losses = []
+
+    def step_rec():
+        loss = step()
+        losses.append(loss[:1].clone())  # device copy: read after the timed window
+        return loss
+
+    dt, loss = _time(step_rec, steps, warmup)
     tr.check()
-    lv = float(loss[0].item())
+    timed = [float(x.item()) for x in losses[warmup:]]
+    lv = timed[-1]
     r = {"config": name, "value": B / dt, "unit": "mixtures/s", "ms_per_step": dt * 1e3, "batch": B,
-         "precision": precision, "loss": lv, "data": "synthetic", "n_gpus": 1}
+         "precision": precision, "loss": lv, "timed_losses": timed,
+         "window_finite": bool(np.all(np.isfinite(timed))), "data": "synthetic", "n_gpus": 1}
+    if emb_scale != 1.0:
+        r["init"] = (f"query embedding scaled by {emb_scale} at init so every cRM logit stays below the 9.02 "
+                     "saturation of the inverse compression in the timed window (the work per step does not "
+                     "depend on the values)")
     if not np.isfinite(lv):  # reference-faithful: the cRM inverse compression is non-finite for logits >= 9.02
         r["note"] = "loss non-finite: cRM inverse compression saturates at |logit| >= 9.02 (SURVEY R11)"
     return r
@@ -111,9 +126,11 @@ def main():
         if c == "c1":
             r = train_config("C1: BiGRU-2L, B=1, 101-channel loss, N=40000", "gru", 2, 1, 2, 40000, "label",
                              a.precision, a.steps, a.warmup, loss_channels=101, adjust=False)
-        elif c == "c3":
+        elif c == "c3":  # with the reference's N(0,1) query embedding the cRM logits saturate at init
+            # (cRM_EvalVer.py:688: the loss is non-finite from the first steps, as in the reference);
+            # the throughput is timed on a finite window (emb_scale) and reports every timed loss
             r = train_config("C3: cRM BiGRU-2L, B=16, N=32000, + mask-apply iSTFT", "gru", 2, 16, 2, 32000, "crm",
-                             a.precision, a.steps, a.warmup, eval_istft=True)
+                             a.precision, a.steps, a.warmup, eval_istft=True, emb_scale=0.1)
         elif c == "c4":
             r = train_config("C4: 3-spk mixed SNR BiGRU-2L, B=32, N=32000", "gru", 2, 32, 3, 32000, "label",
                              a.precision, a.steps, a.warmup)
