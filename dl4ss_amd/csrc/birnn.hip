@@ -1932,10 +1932,23 @@ __global__ __launch_bounds__(256) void bias_reduce_kernel(const float* __restric
   if (i >= 2 * GH) return;
   const int d = i / GH, g = i - d * GH;
   float si = 0.0f, sh = 0.0f;
-  for (int b = 0; b < B; ++b) {
-    const float* pp = part + (long long)(b * 2 + d) * 2 * GH + g;
-    si += pp[0];
-    sh += pp[GH];
+  // rows in chunks of 8 with every load of a chunk issued before its adds (a row-by-row
+  // loop paid one dependent L2 round trip per row: 12 us per launch at B = 32)
+  for (int b0 = 0; b0 < B; b0 += 8) {
+    float vi[8], vh[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = min(b0 + u, B - 1);
+      const float* pp = part + (long long)(b * 2 + d) * 2 * GH + g;
+      vi[u] = pp[0];
+      vh[u] = pp[GH];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b0 + u < B) {
+        si += vi[u];
+        sh += vh[u];
+      }
   }
   if (dbi) dbi[i] += si;
   if (dbh) dbh[i] += sh;
