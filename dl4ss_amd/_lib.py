@@ -32,7 +32,7 @@ SIGNATURES = {
     "dl4ss_colsum_bf16_part_bytes": [I, I],
     "dl4ss_colsum_bf16_det": [P, LL, I, I, P, P, LL, P],
     "dl4ss_gemm_bf16_gl_ws_bytes": [I, I, I, I, I],
-    "dl4ss_gemm_gl_set_stages": [I],
+    "dl4ss_gemm_gl_set_config": [I],
     "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_bwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P],

@@ -37,8 +37,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int IMG = BM * BK;  // bf16 elements per operand image (16 KB)
+constexpr int BN = 128, BK = 64;
+constexpr int PAN = 128 * BK;  // bf16 elements of one 128-row operand panel image (16 KB)
+
+// Tile configurations: BM x 128 output tile, BM / 32 waves of 64 x 64, STG LDS stages.
+//   Cfg<128, 2>: 256 threads, 64 KB, two workgroups per CU, one k-tile of DMA in flight each
+//   Cfg<256, 3>: 512 threads, 144 KB, one workgroup per CU, two k-tiles in flight (a counted
+//                vmcnt across a raw s_barrier), 25 % fewer operand bytes per MFMA
+template <int BM_, int STG_>
+struct Cfg {
+  static constexpr int BM = BM_, STG = STG_, NT = 2 * BM_, NW = NT / 64;
+  static constexpr int CPW_A = BM_ / 8 / NW, CPW_B = BN / 8 / NW;  // 1-KB DMAs per wave per k-tile
+  static constexpr int IMG_A = BM_ * BK, IMG_B = BN * BK, STAGE = IMG_A + IMG_B;
+};
 enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2 };
 
 // 64 zero bytes every out-of-range k chunk is loaded from (16 B per lane)
@@ -48,28 +59,29 @@ __device__ __forceinline__ float ftanh_fast(float x) { return 1.0f - 2.0f * __bu
 
 __device__ __forceinline__ int km_xor(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
 
-// Per-lane source pointers of one operand's four DMA instructions (this wave's share of a
-// 128 x 64 tile) at k-tile start kbeg; advanced by `step` elements per k-tile.
-template <bool KC>
+// Per-lane source pointers of one operand's CPW DMA instructions (this wave's share of a
+// ROWS x 64 tile, ROWS / 128 panels of 16 1-KB instructions) at k-tile start kbeg; advanced
+// by `step` elements per k-tile.  Instruction j fills panel j >> 4, piece j & 15.
+template <bool KC, int CPW>
 struct Stager {
-  const unsigned short* src[4];
-  int kpos[4];  // k of this lane's chunk (KC) or k-row (KM) relative to the k-tile start
+  const unsigned short* src[CPW];
+  int kpos[CPW];  // k of this lane's chunk (KC) or k-row (KM) relative to the k-tile start
   long long step;
   __device__ __forceinline__ void init(const unsigned short* G, long long ld, int r0, int rmax, int kbeg, int wave,
                                        int lane) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = wave * 4 + i;  // 1-KB instruction index within the tile
+    for (int i = 0; i < CPW; ++i) {
+      const int j = wave * CPW + i, pan = j >> 4, jj = j & 15;
       if (KC) {
-        const int r = 8 * j + (lane >> 3), cp = lane & 7;
+        const int r = 8 * jj + (lane >> 3), cp = lane & 7;  // row within the panel
         const int c = cp ^ ((r >> 1) & 7);
-        const int gr = min(r0 + r, rmax - 1);
+        const int gr = min(r0 + 128 * pan + r, rmax - 1);
         src[i] = G + (long long)gr * ld + kbeg + 8 * c;
         kpos[i] = 8 * c;
       } else {
-        const int k = 4 * j + (lane >> 4), cp = lane & 15;
+        const int k = 4 * jj + (lane >> 4), cp = lane & 15;
         const int c = cp ^ km_xor(k);
-        int gc = r0 + 8 * c;
+        int gc = r0 + 128 * pan + 8 * c;
         if (gc >= rmax) gc = 0;  // a chunk wholly past the last row: any valid address
         src[i] = G + (long long)(kbeg + k) * ld + gc;
         kpos[i] = k;
@@ -77,20 +89,22 @@ struct Stager {
     }
     step = KC ? BK : (long long)BK * ld;
   }
-  // issue this wave's four 1-KB DMAs of k-tile t (k0 = kbeg + t * BK) into image dst
+  // issue this wave's CPW 1-KB DMAs of k-tile t (k0 = kbeg + t * BK) into image dst
   __device__ __forceinline__ void issue(unsigned short* dst, int wave, int t, int k0_rel, int kspan) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < CPW; ++i) {
       const bool in = k0_rel + kpos[i] < kspan;
       const void* p = in ? (const void*)(src[i] + t * step) : (const void*)g_zero_line;
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + (wave * 4 + i) * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + (wave * CPW + i) * 512), 16, 0, 0);
     }
   }
 };
 
-// fragment (8 k-values of one row) of k-step kk (0, 1) for tile row `row` (0..127)
+// fragment (8 k-values of one row) of k-step kk (0, 1) for tile row `row`
 template <bool KC>
 __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int kk, int lane) {
+  img += (row >> 7) * PAN;  // 128-row panel
+  row &= 127;
   if (KC) {
     const int c = 4 * kk + (lane >> 4);
     return *reinterpret_cast<const bf16x8*>(img + row * BK + 8 * (c ^ ((row >> 1) & 7)));
@@ -104,42 +118,43 @@ __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int k
     for (int hh = 0; hh < 2; ++hh) {
       const int k = 32 * kk + 8 * g + 4 * hh + q;
       const int ch = ((c0 >> 3) + (p >> 1)) ^ km_xor(k);
-      h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + k * BM + 8 * ch + 4 * (p & 1)));
+      h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + k * 128 + 8 * ch + 4 * (p & 1)));
     }
     return bf16x8{h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
   }
 }
 
-// STG LDS stages: 2 = double buffer, one k-tile of DMA in flight, vmcnt(0) + __syncthreads per
-// k-tile, 64 KB (two workgroups per CU); 3 = two k-tiles in flight across a raw s_barrier with
-// a counted vmcnt (the wave's 8 DMAs of the newest tile may stay outstanding), 96 KB (one
-// workgroup per CU).
-template <bool A_KC, bool B_KC, int EPI, bool SPLIT, int STG>
-__global__ __launch_bounds__(NT, STG == 2 ? 2 : 1) void gemm_gl_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
-                                                        long long lda, const unsigned short* __restrict__ B,
-                                                        long long ldb, float* __restrict__ C, long long ldc,
-                                                        const float* __restrict__ bias, float beta, int k_per_split,
-                                                        int grid_m, int grid_n, long long sa, long long sb,
-                                                        long long sc, float* __restrict__ part) {
+template <bool A_KC, bool B_KC, int EPI, bool SPLIT, class CF>
+__global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_gl_kernel(
+    int M, int N, int K, const unsigned short* __restrict__ A, long long lda, const unsigned short* __restrict__ B,
+    long long ldb, float* __restrict__ C, long long ldc, const float* __restrict__ bias, float beta, int k_per_split,
+    int grid_m, int grid_n, long long sa, long long sb, long long sc, float* __restrict__ part) {
+  constexpr int BM = CF::BM, STG = CF::STG, IMG_A = CF::IMG_A, STAGE = CF::STAGE;
   // one LDS array (a second __shared__ object can make hipcc drain vmcnt before every ds_read)
-  __shared__ __attribute__((aligned(16))) unsigned short smem[STG * 2 * IMG];
-  A += blockIdx.y * sa;
-  B += blockIdx.y * sb;
-  C += blockIdx.y * sc;
-
-  // XCD-major grouped tile order (8 M-tiles x all N-tiles per group), bijective remap
+  __shared__ __attribute__((aligned(16))) unsigned short smem[STG * STAGE];
+  // XCD-major order over the WHOLE grid (tiles x batch members x k-splits): workgroups are
+  // dealt round-robin over the 8 XCDs in dispatch order (x fastest, then y, then z; speed
+  // only, never correctness), so the dispatch index L is remapped bijectively to R, giving
+  // each XCD a contiguous range of R: mostly one (split, member) and 8 M-tiles x all N-tiles
+  // groups of it, whose operand panels then stay in that XCD's L2
   const int ntiles = grid_m * grid_n;
-  const int nwg = gridDim.x;
-  const int xcd = blockIdx.x % 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
-  if (tile >= ntiles) return;
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = L % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int R = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+  const int zsplit = R / (ntiles * (int)gridDim.y);
+  const int ymem = (R / ntiles) % (int)gridDim.y;
+  const int tile = R % ntiles;
+  A += ymem * sa;
+  B += ymem * sb;
+  C += ymem * sc;
   constexpr int GROUP = 8;
   const int gsize = GROUP * grid_n;
   const int first_m = (tile / gsize) * GROUP;
   const int gm_here = min(grid_m - first_m, GROUP);
   const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * k_per_split;
+  const int kbeg = zsplit * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   if (kbeg >= kend) return;
   const int kspan = kend - kbeg;
@@ -148,8 +163,8 @@ __global__ __launch_bounds__(NT, STG == 2 ? 2 : 1) void gemm_gl_kernel(int M, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
-  Stager<A_KC> sa_;
-  Stager<B_KC> sb_;
+  Stager<A_KC, CF::CPW_A> sa_;
+  Stager<B_KC, CF::CPW_B> sb_;
   sa_.init(A, lda, m0, M, kbeg, wave, lane);
   sb_.init(B, ldb, n0, N, kbeg, wave, lane);
 
@@ -160,7 +175,7 @@ __global__ __launch_bounds__(NT, STG == 2 ? 2 : 1) void gemm_gl_kernel(int M, in
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](const unsigned short* ia) {
-    const unsigned short* ib = ia + IMG;
+    const unsigned short* ib = ia + IMG_A;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[4], bfr[4];
@@ -168,24 +183,31 @@ __global__ __launch_bounds__(NT, STG == 2 ? 2 : 1) void gemm_gl_kernel(int M, in
       for (int i = 0; i < 4; ++i) af[i] = frag<A_KC>(ia, wm + 16 * i + (lane & 15), kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag<B_KC>(ib, wn + 16 * j + (lane & 15), kk, lane);
+#ifndef GGL_NO_MFMA  // diagnostic builds: GGL_NO_MFMA (fragments read, no MFMA), GGL_NO_DMA (first tile only)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#else
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" :: "v"(af[i]), "v"(bfr[i]));
+#endif
     }
   };
-  auto dma = [&](int t) {  // this wave's 8 DMAs of k-tile t into LDS stage t % STG
-    unsigned short* na = smem + (t % STG) * 2 * IMG;
+  auto dma = [&](int t) {  // this wave's DMAs of k-tile t into LDS stage t % STG
+    unsigned short* na = smem + (t % STG) * STAGE;
     sa_.issue(na, wave, t, t * BK, kspan);
-    sb_.issue(na + IMG, wave, t, t * BK, kspan);
+    sb_.issue(na + IMG_A, wave, t, t * BK, kspan);
   };
   if constexpr (STG == 2) {
     dma(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
+#ifndef GGL_NO_DMA
       if (kt + 1 < nk) dma(kt + 1);  // into the other buffer (last read before the previous barrier)
-      compute(smem + (kt & 1) * 2 * IMG);
+#endif
+      compute(smem + (kt & 1) * STAGE);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of k-tile kt + 1 landed
       __syncthreads();  // ... and every wave's; every wave is done reading buffer kt & 1
     }
@@ -196,12 +218,12 @@ __global__ __launch_bounds__(NT, STG == 2 ? 2 : 1) void gemm_gl_kernel(int M, in
       // this wave's DMAs of tile kt landed (tile kt + 1's 8 may stay in flight), then the raw
       // barrier: every wave's tile kt landed and every wave is done reading tile kt - 1's stage
       if (kt + 1 < nk)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CF::CPW_A + CF::CPW_B) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (kt + 2 < nk) dma(kt + 2);  // into the stage tile kt - 1 used
-      compute(smem + (kt % 3) * 2 * IMG);
+      compute(smem + (kt % 3) * STAGE);
     }
     __syncthreads();  // every wave is done with the stages before the epilogue reuses LDS
   }
@@ -222,7 +244,7 @@ __global__ __launch_bounds__(NT, STG == 2 ? 2 : 1) void gemm_gl_kernel(int M, in
     bv.w = col + 3 < N ? bias[col + 3] : 0.f;
   }
   // split-K slab of (batch member y, split z): part[y][z][M][N]
-  float* out = SPLIT ? part + ((long long)blockIdx.y * gridDim.z + blockIdx.z) * M * N : C;
+  float* out = SPLIT ? part + ((long long)ymem * gridDim.z + zsplit) * M * N : C;
   const long long ldo = SPLIT ? N : ldc;
   const bool vec_c = (ldo % 4 == 0) && ((((uintptr_t)out) & 15) == 0) && col + 4 <= N;
 #pragma unroll
@@ -326,13 +348,22 @@ __global__ __launch_bounds__(256) void gemm_gl_reduce_kernel(int M, int N, int S
   }
 }
 
-int g_gl_stages = 0;  // 0: per-shape default (2); DL4SS_GL_STAGES / dl4ss_gemm_gl_set_stages for A/B runs
+typedef Cfg<128, 2> C128;  // 128 x 128, double buffer, two workgroups per CU (the round-2 default)
+typedef Cfg<256, 3> C256;  // 256 x 128, three stages, one workgroup per CU
+typedef Cfg<128, 3> C128S3;  // 128 x 128, three stages (measured slower: A/B knob only)
+// tile configuration: 0 = per shape (gl_cfg_for), 1 = C128, 2 = C256, 3 = C128S3
+int g_gl_cfg = 0;
 
-template <bool A_KC, bool B_KC>
-int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
-           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
-           long long sb, long long sc, float* ws, long long ws_bytes, hipStream_t st) {
-  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+int gl_cfg_for(int M, int N, int K, int splitk, int batch) {
+  (void)M; (void)N; (void)K; (void)splitk; (void)batch;
+  return 1;
+}
+
+template <bool A_KC, bool B_KC, class CF>
+int launch_cfg(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
+               float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
+               long long sb, long long sc, float* ws, long long ws_bytes, hipStream_t st) {
+  const int gm = (M + CF::BM - 1) / CF::BM, gn = (N + BN - 1) / BN;
   int kps = (K + splitk - 1) / splitk;
   kps = (kps + BK - 1) / BK * BK;
   splitk = (K + kps - 1) / kps;
@@ -342,12 +373,8 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
     if (epi != EPI_NONE) return (int)hipErrorInvalidValue;
     const long long need = (long long)batch * splitk * M * N * 4;
     if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
-    if (g_gl_stages == 3)
-      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true, 3>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb,
-                         C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
-    else
-      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true, 2>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb,
-                         C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
+    hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true, CF>), grid, dim3(CF::NT), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
     DL4SS_CHECK_LAUNCH();
     if (N % 4 == 0 && ldc % 4 == 0 && sc % 4 == 0 && ((uintptr_t)C & 15) == 0)
       hipLaunchKernelGGL(gemm_gl_reduce_kernel<true>, dim3(cdiv((long long)M * N / 4, 256), batch), dim3(256), 0, st, M,
@@ -358,15 +385,9 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
     DL4SS_CHECK_LAUNCH();
     return 0;
   }
-#define GGL_LAUNCH(EPI_)                                                                                              \
-  do {                                                                                                              \
-    if (g_gl_stages == 3)                                                                                           \
-      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_, false, 3>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, \
-                         C, ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr);                                      \
-    else                                                                                                            \
-      hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_, false, 2>), grid, dim3(NT), 0, st, M, N, K, A, lda, B, ldb, \
-                         C, ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr);                                      \
-  } while (0)
+#define GGL_LAUNCH(EPI_)                                                                                         \
+  hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_, false, CF>), grid, dim3(CF::NT), 0, st, M, N, K, A, lda, B, \
+                     ldb, C, ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr)
   if (epi == EPI_TANH) GGL_LAUNCH(EPI_TANH);
   else if (epi == EPI_TANH_BF16) GGL_LAUNCH(EPI_TANH_BF16);
   else GGL_LAUNCH(EPI_NONE);
@@ -375,12 +396,25 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
   return 0;
 }
 
+template <bool A_KC, bool B_KC>
+int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
+           float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
+           long long sb, long long sc, float* ws, long long ws_bytes, hipStream_t st) {
+  const int cfg = g_gl_cfg ? g_gl_cfg : gl_cfg_for(M, N, K, splitk, batch);
+#define GGL_ARGS M, N, K, A, lda, B, ldb, C, ldc, bias, epi, beta, splitk, batch, sa, sb, sc, ws, ws_bytes, st
+  if (cfg == 2) return launch_cfg<A_KC, B_KC, C256>(GGL_ARGS);
+  if (cfg == 3) return launch_cfg<A_KC, B_KC, C128S3>(GGL_ARGS);
+  return launch_cfg<A_KC, B_KC, C128>(GGL_ARGS);
+#undef GGL_ARGS
+}
+
 }  // namespace
 
-// Tuning knob (tools/gemm_gl_bench.py): LDS stages of gemm_gl (2 or 3; 0 = default).
-DL4SS_API int dl4ss_gemm_gl_set_stages(int stages) {
-  DL4SS_REQUIRE(stages == 0 || stages == 2 || stages == 3);
-  g_gl_stages = stages;
+// Tuning knob (tools/gemm_gl_bench.py): tile configuration of gemm_gl (0 = per shape, 1 =
+// 128 x 128 double buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages).
+DL4SS_API int dl4ss_gemm_gl_set_config(int cfg) {
+  DL4SS_REQUIRE(cfg >= 0 && cfg <= 3);
+  g_gl_cfg = cfg;
   return 0;
 }
 

@@ -97,8 +97,9 @@ int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream);
  * >= its row count rounded up to 8, and for a k-contiguous one a row stride >= K rounded up
  * to 8 with zeros in that padding; hipErrorInvalidValue otherwise. */
 long long dl4ss_gemm_bf16_gl_ws_bytes(int M, int N, int K, int splitk, int batch);
-/* Tuning knob: LDS stages of dl4ss_gemm_bf16_gl (2 or 3; 0 = the default). */
-int dl4ss_gemm_gl_set_stages(int stages);
+/* Tuning knob: tile configuration of dl4ss_gemm_bf16_gl (0 = per shape, 1 = 128 x 128 double
+ * buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages). */
+int dl4ss_gemm_gl_set_config(int cfg);
 int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
                        long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta,
                        int splitk, int batch, long long strideA, long long strideB, long long strideC, void* ws,

@@ -7,9 +7,17 @@ tolerance is 2e-6 of sum |a||b| per output (the accumulation-order bound at K <=
 import pytest
 import torch
 
-from dl4ss_amd import ops
+from dl4ss_amd import _lib, ops
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "c128x128", "c256x128_3stage", "c128x128_3stage"], autouse=True)
+def gl_config(request):
+    """every tile configuration of gemm_gl.hip (forced through dl4ss_gemm_gl_set_config)"""
+    _lib.call("dl4ss_gemm_gl_set_config", request.param)
+    yield request.param
+    _lib.call("dl4ss_gemm_gl_set_config", 0)
 
 SHAPES = [(300, 200, 128), (2008, 600, 600), (130, 257, 1000), (64, 72, 8), (8, 8, 8), (515, 136, 80),
           (250, 130, 136), (129, 1, 64)]

@@ -75,13 +75,15 @@ for name, (flop, kw) in shapes.items():
     beta = kw.get("beta", 0.0)
     SPLIT = {"dH": 3, "dW_lin": 2, "dX": 1, "dW_ih": 4, "dW_ih0": 4}.get(name.split()[0], 1)
 
-    def gl(stages):
+    def gl(cfg, split=None):
         def f():
-            _lib.call("dl4ss_gemm_gl_set_stages", stages)
-            ops.gemm_bf16_gl(A, B, out=out, splitk=SPLIT, **kw)
+            _lib.call("dl4ss_gemm_gl_set_config", cfg)
+            ops.gemm_bf16_gl(A, B, out=out, splitk=SPLIT if split is None else split, **kw)
         return f
     paths = {"gemm_bb": lambda: ops.gemm_bf16(A, B, out=out, splitk="auto" if beta == 1.0 else 1, **kw),
-             "gemm_gl": gl(2), "gemm_gl_3stage": gl(3)}
+             "gemm_gl": gl(1), "gemm_gl_256x128": gl(2)}
+    if SPLIT > 1:
+        paths["gemm_gl_256x128_halfsplit"] = gl(2, max(1, SPLIT // 2))
     if epi == ops.EPI_NONE and kw.get("bias") is None:
         paths["hipblaslt"] = lambda: ops.gemm_bf16_lt(A, B, out, transA=ta, transB=tb, beta=beta)
     for pname, fn in paths.items():
@@ -100,7 +102,7 @@ fns = {"gemm_bb": lambda: ops.gemm_bf16_batched(dG[:, :1200], hp[:, :H], dWhh[:1
                                            M=1200, N=H, K=BT),
        "hipblaslt": lambda: ops.gemm_bf16_lt(dG[:, :1200], hp[:, :H], dWhh[:1200], transA=True, beta=1.0, batch=2,
                                              strideA=1200, strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT)}
-_lib.call("dl4ss_gemm_gl_set_stages", 0)
+_lib.call("dl4ss_gemm_gl_set_config", 0)
 for pname, fn in fns.items():
     us = timeit(fn)
     print(json.dumps({"shape": "dW_hh 2x1200x300x8032", "path": pname, "us": round(us, 2),
