@@ -125,7 +125,7 @@ __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int k
 }
 
 template <bool A_KC, bool B_KC, int EPI, bool SPLIT, class CF>
-__global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_gl_kernel(
+__global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) void gemm_gl_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, long long lda, const unsigned short* __restrict__ B,
     long long ldb, float* __restrict__ C, long long ldc, const float* __restrict__ bias, float beta, int k_per_split,
     int grid_m, int grid_n, long long sa, long long sb, long long sc, float* __restrict__ part) {

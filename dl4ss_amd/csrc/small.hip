@@ -103,21 +103,32 @@ __global__ __launch_bounds__(64) void query_bwd_dh_kernel(const float* __restric
   dh_bcast[(long long)b * D + c] = (g0 + g1) / (float)T;
 }
 
+// d_emb[id] += sum over the rows bk with idx[bk] == id, in bk order: the block of the first
+// such row owns the label and sums every row of it (no atomics: a speaker drawn twice in a
+// batch gets the same bits on every run)
 __global__ __launch_bounds__(64) void query_bwd_emb_kernel(const float* __restrict__ dq, const int* __restrict__ idx,
-                                                           const float* __restrict__ wadj, int D, int W,
+                                                           int BK, const float* __restrict__ wadj, int D, int W,
                                                            float* __restrict__ demb) {
   const int bk = blockIdx.x;
-  const float* dqr = dq + (long long)bk * W;
   const int id = idx[bk];
+  if (id < 0) return;
+  for (int j = 0; j < bk; ++j)
+    if (idx[j] == id) return;  // an earlier row owns this label
   for (int c = threadIdx.x; c < W; c += 64) {
-    float g = dqr[c];
-    if (wadj) {
-      float g1 = 0.f;
+    float acc = 0.f;
+    for (int r = bk; r < BK; ++r) {
+      if (idx[r] != id) continue;
+      const float* dqr = dq + (long long)r * W;
+      float g = dqr[c];
+      if (wadj) {
+        float g1 = 0.f;
 #pragma unroll 5
-      for (int o = 0; o < W; ++o) g1 = fmaf(wadj[(long long)o * (D + W) + D + c], dqr[o], g1);
-      g += g1;
+        for (int o = 0; o < W; ++o) g1 = fmaf(wadj[(long long)o * (D + W) + D + c], dqr[o], g1);
+        g += g1;
+      }
+      acc += g;
     }
-    if (id >= 0) atomicAdd(demb + (long long)id * W + c, g);
+    demb[(long long)id * W + c] += acc;
   }
 }
 
@@ -255,7 +266,7 @@ DL4SS_API int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* i
   DL4SS_REQUIRE(dq && idx && B > 0 && K > 0 && W > 0);
   hipStream_t st = as_stream(stream);
   if (d_emb) {
-    hipLaunchKernelGGL(query_bwd_emb_kernel, dim3(B * K), dim3(64), 0, st, dq, idx, w_adj, D, W, d_emb);
+    hipLaunchKernelGGL(query_bwd_emb_kernel, dim3(B * K), dim3(64), 0, st, dq, idx, B * K, w_adj, D, W, d_emb);
     DL4SS_CHECK_LAUNCH();
   }
   if (w_adj && dh_bcast) {
