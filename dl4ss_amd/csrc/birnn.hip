@@ -574,6 +574,9 @@ __device__ __forceinline__ bool group_needs_write_through(const u64* place, int 
 
 template <int CELL, int BC>
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
+#ifdef RNN_PRIO  // experiment: the recurrence waves win SIMD arbitration over co-resident GEMM waves
+  __builtin_amdgcn_s_setprio(3);
+#endif
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
   constexpr int KSMAX = HMAX / 32;
   constexpr int SHB = KSMAX * 32 + 8;  // bf16 row stride of the B image (k >= H stays zero)
@@ -1267,6 +1270,9 @@ __device__ __forceinline__ float unpack24(unsigned r) { return __uint_as_float(r
 
 template <int CELL, int BC>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
+#ifdef RNN_PRIO  // experiment: the recurrence waves win SIMD arbitration over co-resident GEMM waves
+  __builtin_amdgcn_s_setprio(3);
+#endif
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
   constexpr int MTWMAX = (HMAX / 16 + 3) / 4;  // MFMA unit tiles per wave (5)
   constexpr int KSRMAX = (4 * 20 + 31) / 32;   // MFMA K-steps over gate rows (3)

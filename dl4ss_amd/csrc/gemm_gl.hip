@@ -307,6 +307,272 @@ __global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) vo
   }
 }
 
+// One epilogue store of four consecutive columns col .. col + 3 of output row `row` (row < M
+// checked by the caller): + bias, + beta C, tanh, bf16 (EPI_TANH_BF16) or an fp32 split-K slab.
+template <int EPI, bool SPLIT>
+__device__ __forceinline__ void store4(float4 x, int row, int col, int N, float* C, long long ldc, float* out,
+                                       long long ldo, bool vec_c, float beta, const float4& bv) {
+  x.x += bv.x; x.y += bv.y; x.z += bv.z; x.w += bv.w;
+  if constexpr (EPI == EPI_TANH_BF16) {  // V of the Linear, written directly as bf16 pairs (ldc even)
+    unsigned short* cb = reinterpret_cast<unsigned short*>(C) + (long long)row * ldc + col;
+    const float xs[4] = {ftanh_fast(x.x), ftanh_fast(x.y), ftanh_fast(x.z), ftanh_fast(x.w)};
+    unsigned short hb[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const unsigned u = __float_as_uint(xs[c]);
+      hb[c] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    }
+    if (col + 4 <= N) {  // two 4-B stores: ldc is only required even (V rows of F * E = 6450)
+      *reinterpret_cast<unsigned*>(cb) = hb[0] | ((unsigned)hb[1] << 16);
+      *reinterpret_cast<unsigned*>(cb + 2) = hb[2] | ((unsigned)hb[3] << 16);
+    } else {
+      for (int c = 0; c < 4 && col + c < N; ++c) cb[c] = hb[c];
+    }
+    return;
+  }
+  float* cp = out + (long long)row * ldo + col;
+  if (vec_c) {
+    if (!SPLIT && beta != 0.0f) {
+      const float4 o = *reinterpret_cast<const float4*>(cp);
+      x.x += beta * o.x; x.y += beta * o.y; x.z += beta * o.z; x.w += beta * o.w;
+    }
+    if (EPI == EPI_TANH) { x.x = ftanh_fast(x.x); x.y = ftanh_fast(x.y); x.z = ftanh_fast(x.z); x.w = ftanh_fast(x.w); }
+    *reinterpret_cast<float4*>(cp) = x;
+  } else {
+    const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (col + c >= N) break;
+      float y = xs[c];
+      if (!SPLIT && beta != 0.0f) y += beta * cp[c];
+      if (EPI == EPI_TANH) y = ftanh_fast(y);
+      cp[c] = y;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256 x 256 ping-pong configuration (cfg 4, gemm_pp_kernel).  Why: the 128 x 128 kernel above
+// moves 64 KB per k-tile per CU (two workgroups) for 4.2 MFLOP; measured at ~1.3 us per k-tile
+// on every shape (4096^3 and the step's), i.e. the per-CU LDS-DMA path (~50-70 GB/s per CU from
+// L2, MI355X_MICROARCH.md 'Indexed rows') sets the rate at 0.33 of the MFMA peak.  A 256 x 256
+// tile per CU moves the same 64 KB per k-tile for 8.4 MFLOP: the load path and the MFMA pipe
+// balance (cdna_hip_programming.md §5 'The 256^2 8-phase template').
+//
+// Structure (one workgroup of 8 waves per CU, 128 KB LDS):
+//  * LDS = 8 half-tile slots of 16 KB: k-tile t (64 deep) lives in slots (t & 1) x {A0, A1, B0,
+//    B1}, each one 128-row operand panel in the PAN images of gemm_gl_kernel (same swizzles,
+//    same Stager / frag code).
+//  * The 256 x 256 C tile is four 128 x 128 quadrants Q(a, b) = A half a x B half b; in phase p
+//    of a k-tile EVERY wave works on the same quadrant (wave w: rows 64 (w >> 2), columns
+//    32 (w & 3) of it: 4 x 2 tiles of 16 x 16, 16 MFMAs over K = 64), in the order Q00, Q01,
+//    Q11, Q10, so each phase reads one new operand half: p0 A0 + B0 (12 ds_read_b128-sized
+//    fragments), p1 B1, p2 A1, p3 nothing (B0 kept in registers) -- a half-tile slot is free
+//    as soon as its phase has passed.
+//  * One half-tile (2 LDS-DMA instructions per wave) is issued per phase: p0 B1(t+1), p1
+//    A1(t+1), p2 A0(t+2), p3 B0(t+2) -- each into a slot whose last read is >= 2 phases back.
+//    Before the barrier that precedes a phase with reads, every wave retires its own DMAs down
+//    to the 4 half-tiles issued after the one that phase reads: `s_waitcnt vmcnt(8)`, never 0
+//    in the loop; DMAs past the last k-tile read the zero line, so the count is uniform.
+//  * Ping-pong: waves 4-7 run one raw `s_barrier` behind waves 0-3, so on every SIMD one wave
+//    issues its fragment reads and DMAs while the other runs its MFMA cluster (s_setprio 1).
+//    A group-1 wave's reads of phase p sit between global barriers 2p+1 and 2p+2, group 0's
+//    between 2p and 2p+1; every wave's counted wait precedes barrier 2p (group 0: after its
+//    MFMAs of p-1, group 1: after its reads of p-1), so the data is in LDS for both groups.
+// ---------------------------------------------------------------------------------------------
+namespace pp {
+constexpr int BM = 256, NT = 512;
+constexpr int SLD = 36;  // epilogue staging row stride (floats) of a wave's 64 x 32 block
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+template <int VM>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <bool KC>
+__device__ __forceinline__ void read4(bf16x8 (&f)[4][2], const unsigned short* img, int r0, int lane) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i][kk] = frag<KC>(img, r0 + 16 * i + (lane & 15), kk, lane);
+}
+template <bool KC>
+__device__ __forceinline__ void read2(bf16x8 (&f)[2][2], const unsigned short* img, int r0, int lane) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) f[j][kk] = frag<KC>(img, r0 + 16 * j + (lane & 15), kk, lane);
+}
+__device__ __forceinline__ void mma(f32x4 (&acc)[4][2], const bf16x8 (&af)[4][2], const bf16x8 (&bf)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[i][j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+}  // namespace pp
+
+// SL half-tile slots (8: 128 KB, 10: the whole 160 KB).  Half-tiles are numbered in issue order
+// n = 4 t + {A0: 0, B0: 1, B1: 2, A1: 3} and live in slot n % SL; phase P = 4 t + p reads up to
+// n = P + 1 and issues n = P + AHEAD (AHEAD = SL - 2: the slot it overwrites held n - SL, last
+// read in phase <= P - 2), so AHEAD - 2 half-tiles = 2 (AHEAD - 2) DMAs stay in flight at
+// every counted wait.
+template <bool A_KC, bool B_KC, int EPI, bool SPLIT, int SL>
+__global__ __launch_bounds__(pp::NT, 1) void gemm_pp_kernel(
+    int M, int N, int K, const unsigned short* __restrict__ A, long long lda, const unsigned short* __restrict__ B,
+    long long ldb, float* __restrict__ C, long long ldc, const float* __restrict__ bias, float beta, int k_per_split,
+    int grid_m, int grid_n, long long sa, long long sb, long long sc, float* __restrict__ part) {
+  constexpr int AHEAD = SL - 2, VM = 2 * (AHEAD - 2);
+  __shared__ __attribute__((aligned(16))) unsigned short smem[SL * PAN];  // the only LDS object
+  // XCD-major remap of the whole grid, as gemm_gl_kernel
+  const int ntiles = grid_m * grid_n;
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = L % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int R = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+  const int zsplit = R / (ntiles * (int)gridDim.y);
+  const int ymem = (R / ntiles) % (int)gridDim.y;
+  const int tile = R % ntiles;
+  A += ymem * sa;
+  B += ymem * sb;
+  C += ymem * sc;
+  constexpr int GROUP = 4;
+  const int gsize = GROUP * grid_n;
+  const int first_m = (tile / gsize) * GROUP;
+  const int gm_here = min(grid_m - first_m, GROUP);
+  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
+  const int m0 = tm * pp::BM, n0 = tn * pp::BM;
+  const int kbeg = zsplit * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  if (kbeg >= kend) return;  // uniform over the workgroup
+  const int kspan = kend - kbeg;
+  const int nk = (kspan + BK - 1) / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);
+  const int wm = 64 * (wave >> 2), wn = 32 * (wave & 3);
+
+  Stager<A_KC, 2> sa0, sa1;
+  Stager<B_KC, 2> sb0, sb1;
+  sa0.init(A, lda, m0, M, kbeg, wave, lane);
+  sa1.init(A, lda, m0 + 128, M, kbeg, wave, lane);
+  sb0.init(B, ldb, n0, N, kbeg, wave, lane);
+  sb1.init(B, ldb, n0 + 128, N, kbeg, wave, lane);
+  auto slot = [&](int n) { return smem + (n % SL) * PAN; };
+  // issue half-tile n (its code n & 3 is a compile-time constant at every call site)
+  auto dma = [&](int n) {
+    const int t = n >> 2;
+    switch (n & 3) {
+      case 0: sa0.issue(slot(n), wave, t, t * BK, kspan); break;
+      case 1: sb0.issue(slot(n), wave, t, t * BK, kspan); break;
+      case 2: sb1.issue(slot(n), wave, t, t * BK, kspan); break;
+      default: sa1.issue(slot(n), wave, t, t * BK, kspan); break;
+    }
+  };
+
+  f32x4 acc[4][4][2];  // [quadrant a * 2 + b][row tile i][column tile j]
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+
+  // prologue: half-tiles 0 .. AHEAD - 1 (what phases -AHEAD .. -1 would have issued)
+#pragma unroll
+  for (int n = 0; n < AHEAD; ++n) dma(n);
+  pp::wait_vm<VM>();  // half-tiles 0, 1 (A0, B0 of k-tile 0) landed
+  pp::bar();          // global barrier 0
+  if (grp) pp::bar();  // waves 4-7 one barrier behind
+  for (int t = 0; t < nk; ++t) {
+    const int P = 4 * t;
+    // phase 0: Q00 -- reads A0, B0 of t
+    pp::read4<A_KC>(af, slot(P), wm, lane);
+    pp::read2<B_KC>(bf0, slot(P + 1), wn, lane);
+    dma(P + AHEAD);
+    if (grp) pp::wait_vm<VM>();  // B1(t) for phase 1
+    pp::bar();
+    pp::mma(acc[0], af, bf0);
+    if (!grp) pp::wait_vm<VM>();
+    pp::bar();
+    // phase 1: Q01 -- reads B1 of t
+    pp::read2<B_KC>(bf1, slot(P + 2), wn, lane);
+    dma(P + 1 + AHEAD);
+    if (grp) pp::wait_vm<VM>();  // A1(t) for phase 2
+    pp::bar();
+    pp::mma(acc[1], af, bf1);
+    if (!grp) pp::wait_vm<VM>();
+    pp::bar();
+    // phase 2: Q11 -- reads A1 of t
+    pp::read4<A_KC>(af, slot(P + 3), wm, lane);
+    dma(P + 2 + AHEAD);
+    pp::bar();
+    pp::mma(acc[3], af, bf1);
+    pp::bar();
+    // phase 3: Q10 -- no reads (B0 still in registers)
+    dma(P + 3 + AHEAD);
+    if (grp) pp::wait_vm<VM>();  // A0(t+1), B0(t+1) for the next phase 0
+    pp::bar();
+    pp::mma(acc[2], af, bf0);
+    if (!grp) pp::wait_vm<VM>();
+    pp::bar();
+  }
+  if (!grp) pp::bar();  // waves 0-3 catch up with the barrier waves 4-7 spent at the start
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-line DMAs past the last k-tile
+  __syncthreads();      // every wave is done with the slots before the epilogue reuses LDS
+
+  // epilogue: per quadrant, the wave's 64 x 32 block (acc[q][i][j][e] = row 16 i + 4 (lane >> 4) + e,
+  // column 16 j + (lane & 15)) is staged in its own LDS area and written back 8 rows per pass
+  float* stage = reinterpret_cast<float*>(smem) + wave * 64 * pp::SLD;
+  float* out = SPLIT ? part + ((long long)ymem * gridDim.z + zsplit) * M * N : C;
+  const long long ldo = SPLIT ? N : ldc;
+  const bool add_bias = !SPLIT && bias != nullptr;
+  const int c4 = 4 * (lane & 7);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int a = q >> 1, b = q & 1;
+    const int col = n0 + 128 * b + wn + c4;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (add_bias) {
+      bv.x = col < N ? bias[col] : 0.f;
+      bv.y = col + 1 < N ? bias[col + 1] : 0.f;
+      bv.z = col + 2 < N ? bias[col + 2] : 0.f;
+      bv.w = col + 3 < N ? bias[col + 3] : 0.f;
+    }
+    const bool vec_c = (ldo % 4 == 0) && ((((uintptr_t)out) & 15) == 0) && col + 4 <= N;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) stage[(16 * i + 4 * (lane >> 4) + e) * pp::SLD + 16 * j + (lane & 15)] = acc[q][i][j][e];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll 2
+    for (int rr = 0; rr < 64; rr += 8) {
+      const int rl = rr + (lane >> 3);
+      const int row = m0 + 128 * a + wm + rl;
+      if (row >= M) continue;
+      const float4 x = *reinterpret_cast<const float4*>(stage + rl * pp::SLD + c4);
+      store4<EPI, SPLIT>(x, row, col, N, C, ldc, out, ldo, vec_c, beta, bv);
+    }
+  }
+}
+
 // C[b] = beta C[b] + sum_{z < S} part[b][z] (+ bias), z in order: the split-K combine.  VEC:
 // four columns per thread with 16-B loads / stores (N % 4 == 0, ldc % 4 == 0, aligned C), the
 // S slab loads of a thread issued together (8 at a time) before they are summed in order.
@@ -351,7 +617,8 @@ __global__ __launch_bounds__(256) void gemm_gl_reduce_kernel(int M, int N, int S
 typedef Cfg<128, 2> C128;  // 128 x 128, double buffer, two workgroups per CU (the round-2 default)
 typedef Cfg<256, 3> C256;  // 256 x 128, three stages, one workgroup per CU
 typedef Cfg<128, 3> C128S3;  // 128 x 128, three stages (measured slower: A/B knob only)
-// tile configuration: 0 = per shape (gl_cfg_for), 1 = C128, 2 = C256, 3 = C128S3
+// tile configuration: 0 = per shape (gl_cfg_for), 1 = C128, 2 = C256, 3 = C128S3, 4 / 5 = 256 x 256
+// ping-pong with 8 / 10 half-tile slots
 int g_gl_cfg = 0;
 
 int gl_cfg_for(int M, int N, int K, int splitk, int batch) {
@@ -396,12 +663,57 @@ int launch_cfg(int M, int N, int K, const unsigned short* A, long long lda, cons
   return 0;
 }
 
+// split-K slabs + fixed-order reduce of a split launch (any configuration)
+int launch_reduce(int M, int N, int splitk, int batch, float* C, long long ldc, long long sc, const float* bias,
+                  float beta, float* ws, hipStream_t st) {
+  if (N % 4 == 0 && ldc % 4 == 0 && sc % 4 == 0 && ((uintptr_t)C & 15) == 0)
+    hipLaunchKernelGGL(gemm_gl_reduce_kernel<true>, dim3(cdiv((long long)M * N / 4, 256), batch), dim3(256), 0, st, M,
+                       N, splitk, ws, C, ldc, sc, bias, beta);
+  else
+    hipLaunchKernelGGL(gemm_gl_reduce_kernel<false>, dim3(cdiv((long long)M * N, 256), batch), dim3(256), 0, st, M, N,
+                       splitk, ws, C, ldc, sc, bias, beta);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+// the 256 x 256 ping-pong configuration (gemm_pp_kernel) with SL half-tile slots
+template <bool A_KC, bool B_KC, int SL>
+int launch_pp(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
+              float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
+              long long sb, long long sc, float* ws, long long ws_bytes, hipStream_t st) {
+  const int gm = (M + pp::BM - 1) / pp::BM, gn = (N + pp::BM - 1) / pp::BM;
+  int kps = (K + splitk - 1) / splitk;
+  kps = (kps + BK - 1) / BK * BK;
+  splitk = (K + kps - 1) / kps;
+  dim3 grid(gm * gn, batch, splitk);
+  if (splitk > 1) {
+    if (epi != EPI_NONE) return (int)hipErrorInvalidValue;
+    const long long need = (long long)batch * splitk * M * N * 4;
+    if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_pp_kernel<A_KC, B_KC, EPI_NONE, true, SL>), grid, dim3(pp::NT), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
+    DL4SS_CHECK_LAUNCH();
+    return launch_reduce(M, N, splitk, batch, C, ldc, sc, bias, beta, ws, st);
+  }
+#define GPP_LAUNCH(EPI_)                                                                                            \
+  hipLaunchKernelGGL((gemm_pp_kernel<A_KC, B_KC, EPI_, false, SL>), grid, dim3(pp::NT), 0, st, M, N, K, A, lda, B, ldb, \
+                     C, ldc, bias, beta, kps, gm, gn, sa, sb, sc, nullptr)
+  if (epi == EPI_TANH) GPP_LAUNCH(EPI_TANH);
+  else if (epi == EPI_TANH_BF16) GPP_LAUNCH(EPI_TANH_BF16);
+  else GPP_LAUNCH(EPI_NONE);
+#undef GPP_LAUNCH
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
 template <bool A_KC, bool B_KC>
 int launch(int M, int N, int K, const unsigned short* A, long long lda, const unsigned short* B, long long ldb,
            float* C, long long ldc, const float* bias, int epi, float beta, int splitk, int batch, long long sa,
            long long sb, long long sc, float* ws, long long ws_bytes, hipStream_t st) {
   const int cfg = g_gl_cfg ? g_gl_cfg : gl_cfg_for(M, N, K, splitk, batch);
 #define GGL_ARGS M, N, K, A, lda, B, ldb, C, ldc, bias, epi, beta, splitk, batch, sa, sb, sc, ws, ws_bytes, st
+  if (cfg == 4) return launch_pp<A_KC, B_KC, 8>(GGL_ARGS);
+  if (cfg == 5) return launch_pp<A_KC, B_KC, 10>(GGL_ARGS);
   if (cfg == 2) return launch_cfg<A_KC, B_KC, C256>(GGL_ARGS);
   if (cfg == 3) return launch_cfg<A_KC, B_KC, C128S3>(GGL_ARGS);
   return launch_cfg<A_KC, B_KC, C128>(GGL_ARGS);
@@ -411,9 +723,10 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
 }  // namespace
 
 // Tuning knob (tools/gemm_gl_bench.py): tile configuration of gemm_gl (0 = per shape, 1 =
-// 128 x 128 double buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages).
+// 128 x 128 double buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages, 4 = 256 x
+// 256 ping-pong, 128 KB LDS, 5 = the same with the whole 160 KB: six half-tiles in flight).
 DL4SS_API int dl4ss_gemm_gl_set_config(int cfg) {
-  DL4SS_REQUIRE(cfg >= 0 && cfg <= 3);
+  DL4SS_REQUIRE(cfg >= 0 && cfg <= 5);
   g_gl_cfg = cfg;
   return 0;
 }

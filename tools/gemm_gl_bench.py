@@ -81,9 +81,12 @@ for name, (flop, kw) in shapes.items():
             ops.gemm_bf16_gl(A, B, out=out, splitk=SPLIT if split is None else split, **kw)
         return f
     paths = {"gemm_bb": lambda: ops.gemm_bf16(A, B, out=out, splitk="auto" if beta == 1.0 else 1, **kw),
-             "gemm_gl": gl(1), "gemm_gl_256x128": gl(2)}
+             "gemm_gl": gl(1), "gemm_gl_256x128": gl(2), "gemm_gl_pp256": gl(4), "gemm_gl_pp256_10": gl(5)}
     if SPLIT > 1:
         paths["gemm_gl_256x128_halfsplit"] = gl(2, max(1, SPLIT // 2))
+    for s in (2, 3, 4, 6, 8, 12):
+        paths[f"gemm_gl_pp256 splitk={s}"] = gl(4, s)
+        paths[f"gemm_gl_pp256_10 splitk={s}"] = gl(5, s)
     if epi == ops.EPI_NONE and kw.get("bias") is None:
         paths["hipblaslt"] = lambda: ops.gemm_bf16_lt(A, B, out, transA=ta, transB=tb, beta=beta)
     for pname, fn in paths.items():
@@ -100,6 +103,12 @@ fns = {"gemm_bb": lambda: ops.gemm_bf16_batched(dG[:, :1200], hp[:, :H], dWhh[:1
        "gemm_gl": lambda: ops.gemm_bf16_gl(dG[:, :1200], hp[:, :H], transA=True, out=dWhh[:1200], beta=1.0,
                                            splitk=8, batch=2, strideA=1200, strideB=p8(H), strideC=1200 * H,
                                            M=1200, N=H, K=BT),
+       "gemm_gl_pp256 splitk=8": lambda: (_lib.call("dl4ss_gemm_gl_set_config", 4), ops.gemm_bf16_gl(
+           dG[:, :1200], hp[:, :H], transA=True, out=dWhh[:1200], beta=1.0, splitk=8, batch=2, strideA=1200,
+           strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT), _lib.call("dl4ss_gemm_gl_set_config", 0)),
+       "gemm_gl_pp256 splitk=12": lambda: (_lib.call("dl4ss_gemm_gl_set_config", 4), ops.gemm_bf16_gl(
+           dG[:, :1200], hp[:, :H], transA=True, out=dWhh[:1200], beta=1.0, splitk=12, batch=2, strideA=1200,
+           strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT), _lib.call("dl4ss_gemm_gl_set_config", 0)),
        "hipblaslt": lambda: ops.gemm_bf16_lt(dG[:, :1200], hp[:, :H], dWhh[:1200], transA=True, beta=1.0, batch=2,
                                              strideA=1200, strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT)}
 _lib.call("dl4ss_gemm_gl_set_config", 0)
