@@ -27,6 +27,69 @@ def _check_status(status, what):
         raise RuntimeError(f"{what}: BiRNN hand-off timed out (status {s})")
 
 
+def birnn_fwd_impl(x, w_ih, b_ih, w_hh, b_hh, cell, H, precision):
+    """One bidirectional layer's forward: (out (B,T,2H), hprev, act, cs or None).  Shared by
+    BiRNNLayerFn and the dl4ss::birnn_layer custom op (dl4ss_amd.library)."""
+    x = _c(x)
+    B, T, D = x.shape
+    cid = CELLS[cell]
+    dev = x.device
+    G = ops.gemm(x.view(B * T, D), _c(w_ih), transB=True, bias=_c(b_ih), precision=precision)
+    out = torch.empty(B, T, 2 * H, device=dev)
+    hprev = torch.empty_like(out)
+    act = torch.empty(B, T, 2, 4 * H, device=dev)
+    cs = torch.empty(B, T, 2, H, device=dev) if cell == "lstm" else None
+    wsn = _birnn_ws_bytes(cid, B, H)
+    ws = torch.empty((wsn + 7) // 8, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("dl4ss_birnn_fwd", cid, ops.PREC[precision], B, T, H, _lib.ptr(G), _lib.ptr(_c(w_hh)),
+              _lib.ptr(_c(b_hh)), _lib.ptr(out), _lib.ptr(hprev), _lib.ptr(act),
+              _lib.ptr(cs) if cs is not None else None, _lib.ptr(ws), wsn, _lib.ptr(status), _lib.stream_ptr())
+    _check_status(status, "dl4ss_birnn_fwd")
+    return out, hprev, act, cs
+
+
+def _birnn_ws_bytes(cid, B, H):
+    wsn = _lib.query("dl4ss_birnn_workspace_bytes", cid, B, H)
+    if wsn < 0:
+        raise RuntimeError(f"BiRNN shape unsupported (B={B}, H={H})")
+    return wsn
+
+
+def birnn_bwd_impl(dout, x, w_ih, w_hh, hprev, act, cs, cell, H, precision, need_dx=True):
+    """BPTT + the layer's weight / bias / input gradients: (dx or None, dw_ih, db_ih, dw_hh, db_hh)."""
+    B, T, D = x.shape
+    dev = x.device
+    NGH = (4 if cell == "lstm" else 3) * H
+    wsn = _birnn_ws_bytes(CELLS[cell], B, H)
+    dout = _c(dout.float())
+    dG = torch.empty(B * T, 2 * NGH, device=dev)
+    dGh = torch.empty_like(dG) if cell == "gru" else None
+    ws = torch.empty((wsn + 7) // 8, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("dl4ss_birnn_bwd", CELLS[cell], ops.PREC[precision], B, T, H, _lib.ptr(dout), None,
+              _lib.ptr(_c(w_hh)), _lib.ptr(act), _lib.ptr(cs) if cell == "lstm" else None, _lib.ptr(hprev),
+              _lib.ptr(dG), _lib.ptr(dGh) if dGh is not None else None, _lib.ptr(ws), wsn, _lib.ptr(status),
+              _lib.stream_ptr())
+    _check_status(status, "dl4ss_birnn_bwd")
+    dGh = dG if dGh is None else dGh
+    w_ih = _c(w_ih)
+    x2 = _c(x).view(B * T, D)
+    dx = ops.gemm(dG, w_ih, precision=precision).view(B, T, D) if need_dx else None
+    dw_ih = torch.zeros_like(w_ih)
+    ops.gemm(dG, x2, transA=True, out=dw_ih, beta=1.0, splitk="auto", precision=precision)
+    db_ih = torch.zeros(2 * NGH, device=dev)
+    ops.colsum(dG, db_ih)
+    dw_hh = torch.zeros_like(w_hh)
+    hp = hprev.view(B * T, 2 * H)
+    for d in range(2):
+        ops.gemm(dGh[:, d * NGH:(d + 1) * NGH], hp[:, d * H:(d + 1) * H], transA=True,
+                 out=dw_hh[d * NGH:(d + 1) * NGH], beta=1.0, splitk="auto", precision=precision)
+    db_hh = torch.zeros(2 * NGH, device=dev)
+    ops.colsum(dGh, db_hh)
+    return dx, dw_ih, db_ih, dw_hh, db_hh
+
+
 class BiRNNLayerFn(torch.autograd.Function):
     """One bidirectional LSTM/GRU layer (torch gate order / two-bias semantics).
 
@@ -38,61 +101,32 @@ class BiRNNLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_ih, b_ih, w_hh, b_hh, cell, H, precision):
-        x = _c(x)
-        B, T, D = x.shape
-        cid = CELLS[cell]
-        NGH = (4 if cell == "lstm" else 3) * H
-        dev = x.device
-        G = ops.gemm(x.view(B * T, D), _c(w_ih), transB=True, bias=_c(b_ih), precision=precision)
-        out = torch.empty(B, T, 2 * H, device=dev)
-        hprev = torch.empty_like(out)
-        act = torch.empty(B, T, 2, 4 * H, device=dev)
-        cs = torch.empty(B, T, 2, H, device=dev) if cell == "lstm" else None
-        wsn = _lib.query("dl4ss_birnn_workspace_bytes", cid, B, H)
-        if wsn < 0:
-            raise RuntimeError(f"BiRNN shape unsupported (B={B}, H={H})")
-        ws = torch.empty((wsn + 7) // 8, dtype=torch.int64, device=dev)
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
-        whh = _c(w_hh)
-        _lib.call("dl4ss_birnn_fwd", cid, ops.PREC[precision], B, T, H, _lib.ptr(G), _lib.ptr(whh),
-                  _lib.ptr(_c(b_hh)), _lib.ptr(out), _lib.ptr(hprev), _lib.ptr(act),
-                  _lib.ptr(cs) if cs is not None else None, _lib.ptr(ws), wsn, _lib.ptr(status), _lib.stream_ptr())
-        _check_status(status, "dl4ss_birnn_fwd")
-        ctx.save_for_backward(x, _c(w_ih), whh, hprev, act, cs if cs is not None else act)
-        ctx.meta = (cell, H, NGH, precision, wsn)
+        out, hprev, act, cs = birnn_fwd_impl(x, w_ih, b_ih, w_hh, b_hh, cell, H, precision)
+        ctx.save_for_backward(_c(x), _c(w_ih), _c(w_hh), hprev, act, cs if cs is not None else act)
+        ctx.meta = (cell, H, precision)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, w_ih, w_hh, hprev, act, cs = ctx.saved_tensors
-        cell, H, NGH, precision, wsn = ctx.meta
-        B, T, D = x.shape
-        dev = x.device
-        dout = _c(dout.float())
-        dG = torch.empty(B * T, 2 * NGH, device=dev)
-        dGh = torch.empty_like(dG) if cell == "gru" else None
-        ws = torch.empty((wsn + 7) // 8, dtype=torch.int64, device=dev)
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
-        _lib.call("dl4ss_birnn_bwd", CELLS[cell], ops.PREC[precision], B, T, H, _lib.ptr(dout), None,
-                  _lib.ptr(w_hh), _lib.ptr(act), _lib.ptr(cs) if cell == "lstm" else None, _lib.ptr(hprev),
-                  _lib.ptr(dG), _lib.ptr(dGh) if dGh is not None else None, _lib.ptr(ws), wsn, _lib.ptr(status),
-                  _lib.stream_ptr())
-        _check_status(status, "dl4ss_birnn_bwd")
-        dGh = dG if dGh is None else dGh
-        x2 = x.view(B * T, D)
-        dx = ops.gemm(dG, w_ih, precision=precision).view(B, T, D) if ctx.needs_input_grad[0] else None
-        dw_ih = torch.zeros_like(w_ih)
-        ops.gemm(dG, x2, transA=True, out=dw_ih, beta=1.0, splitk="auto", precision=precision)
-        db_ih = torch.zeros(2 * NGH, device=dev)
-        ops.colsum(dG, db_ih)
-        dw_hh = torch.zeros_like(w_hh)
-        hp = hprev.view(B * T, 2 * H)
-        for d in range(2):
-            ops.gemm(dGh[:, d * NGH:(d + 1) * NGH], hp[:, d * H:(d + 1) * H], transA=True,
-                     out=dw_hh[d * NGH:(d + 1) * NGH], beta=1.0, splitk="auto", precision=precision)
-        db_hh = torch.zeros(2 * NGH, device=dev)
-        ops.colsum(dGh, db_hh)
+        cell, H, precision = ctx.meta
+        dx, dw_ih, db_ih, dw_hh, db_hh = birnn_bwd_impl(dout, x, w_ih, w_hh, hprev, act,
+                                                        cs if cell == "lstm" else None, cell, H, precision,
+                                                        bool(ctx.needs_input_grad[0]))
         return dx, dw_ih, db_ih, dw_hh, db_hh, None, None, None
+
+
+def linear_tanh_bwd_impl(dv, x2d, w, v, precision, need_dx=True):
+    """(dx or None, dW, db) of V = tanh(x W^T + b), from the saved V."""
+    dv = _c(dv.float())
+    dpre = torch.empty_like(v)
+    _lib.call("dl4ss_tanh_bwd", _lib.ptr(v), _lib.ptr(dv), _lib.ptr(dpre), v.numel(), _lib.stream_ptr())
+    dw = torch.zeros_like(w)
+    ops.gemm(dpre, x2d, transA=True, out=dw, beta=1.0, splitk="auto", precision=precision)
+    db = torch.zeros(w.shape[0], device=w.device)
+    ops.colsum(dpre, db)
+    dx = ops.gemm(dpre, w, precision=precision) if need_dx else None
+    return dx, dw, db
 
 
 class LinearTanhFn(torch.autograd.Function):
@@ -109,14 +143,7 @@ class LinearTanhFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dv):
         x2d, w, v = ctx.saved_tensors
-        dv = _c(dv.float())
-        dpre = torch.empty_like(v)
-        _lib.call("dl4ss_tanh_bwd", _lib.ptr(v), _lib.ptr(dv), _lib.ptr(dpre), v.numel(), _lib.stream_ptr())
-        dw = torch.zeros_like(w)
-        ops.gemm(dpre, x2d, transA=True, out=dw, beta=1.0, splitk="auto", precision=ctx.precision)
-        db = torch.zeros(w.shape[0], device=w.device)
-        ops.colsum(dpre, db)
-        dx = ops.gemm(dpre, w, precision=ctx.precision) if ctx.needs_input_grad[0] else None
+        dx, dw, db = linear_tanh_bwd_impl(dv, x2d, w, v, ctx.precision, bool(ctx.needs_input_grad[0]))
         return dx, dw, db, None
 
 
@@ -145,6 +172,43 @@ class LinearFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def attention_dot_fwd_impl(V, q, crm):
+    """mask (Bq,R) = sigmoid(V . q), or (Bq,R,2) = 10 tanh(V . q_half) for the cRM branch."""
+    return torch.stack(_attention_dot_masks(V, q, crm), dim=-1) if crm else _attention_dot_masks(V, q, crm)[0]
+
+
+def _attention_dot_masks(V, q, crm):
+    V, q = _c(V.float()), _c(q.float())
+    Bq, R, E = V.shape
+    st = _lib.stream_ptr()
+    masks = []
+    for h in range(2 if crm else 1):
+        m = torch.empty(Bq, R, device=V.device)
+        _lib.call("dl4ss_attn_dot_fwd", _lib.ptr(V), ctypes.c_void_p(q.data_ptr() + 4 * h * E), q.shape[1], Bq, R,
+                  E, int(crm), _lib.ptr(m), st)
+        masks.append(m)
+    return masks
+
+
+def attention_dot_bwd_impl(dmask, V, q, masks, crm, need_dV=True):
+    """(dV or None, dq) from the per-half masks of the forward."""
+    V, q = _c(V.float()), _c(q.float())
+    Bq, R, E = V.shape
+    st = _lib.stream_ptr()
+    dV = torch.zeros_like(V) if need_dV else None
+    nblk = _lib.query("dl4ss_attn_dot_nblk", R)
+    part = torch.empty(Bq * nblk * E, device=V.device)
+    dq = torch.zeros_like(q)
+    dqh = torch.empty(Bq, E, device=V.device)
+    for h, m in enumerate(masks):
+        dm = _c(dmask[..., h].float()) if crm else _c(dmask.float())
+        _lib.call("dl4ss_attn_dot_bwd", _lib.ptr(V), ctypes.c_void_p(q.data_ptr() + 4 * h * E), q.shape[1],
+                  _lib.ptr(m), _lib.ptr(dm), Bq, R, E, int(crm), _lib.ptr(dV) if dV is not None else None,
+                  _lib.ptr(part), _lib.ptr(dqh), st)
+        dq[:, h * E:(h + 1) * E] = dqh
+    return dV, dq
+
+
 class AttentionDotFn(torch.autograd.Function):
     """ATTENTION 'dot' (EvalVer.py:216-226): mask (Bq,R) = sigmoid(V (Bq,R,E) . q (Bq,E));
     crm=True: the cRM branch (cRM_EvalVer.py:259-271), q (Bq,2E) split in halves,
@@ -153,15 +217,7 @@ class AttentionDotFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, V, q, crm):
         V, q = _c(V.float()), _c(q.float())
-        Bq, R, E = V.shape
-        st = _lib.stream_ptr()
-        halves = 2 if crm else 1
-        masks = []
-        for h in range(halves):
-            m = torch.empty(Bq, R, device=V.device)
-            _lib.call("dl4ss_attn_dot_fwd", _lib.ptr(V), ctypes.c_void_p(q.data_ptr() + 4 * h * E), q.shape[1], Bq, R,
-                      E, int(crm), _lib.ptr(m), st)
-            masks.append(m)
+        masks = _attention_dot_masks(V, q, crm)
         ctx.save_for_backward(V, q, *masks)
         ctx.crm = crm
         return torch.stack(masks, dim=-1) if crm else masks[0]
@@ -169,19 +225,7 @@ class AttentionDotFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dmask):
         V, q, *masks = ctx.saved_tensors
-        Bq, R, E = V.shape
-        st = _lib.stream_ptr()
-        dV = torch.zeros_like(V) if ctx.needs_input_grad[0] else None
-        nblk = _lib.query("dl4ss_attn_dot_nblk", R)
-        part = torch.empty(Bq * nblk * E, device=V.device)
-        dq = torch.zeros_like(q)
-        dqh = torch.empty(Bq, E, device=V.device)
-        for h, m in enumerate(masks):
-            dm = _c(dmask[..., h].float()) if ctx.crm else _c(dmask.float())
-            _lib.call("dl4ss_attn_dot_bwd", _lib.ptr(V), ctypes.c_void_p(q.data_ptr() + 4 * h * E), q.shape[1],
-                      _lib.ptr(m), _lib.ptr(dm), Bq, R, E, int(ctx.crm), _lib.ptr(dV) if dV is not None else None,
-                      _lib.ptr(part), _lib.ptr(dqh), st)
-            dq[:, h * E:(h + 1) * E] = dqh
+        dV, dq = attention_dot_bwd_impl(dmask, V, q, masks, ctx.crm, bool(ctx.needs_input_grad[0]))
         return dV, dq, None
 
 
