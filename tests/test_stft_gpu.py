@@ -52,6 +52,31 @@ def test_stft_logmag_and_conj(dev):
         np.testing.assert_allclose(Xc[i, ..., 1].cpu().numpy(), S.imag, atol=2e-4)
 
 
+@pytest.mark.parametrize("off_c,off_m", [(0, 0), (1, 1), (0, 2), (1, 3)])
+@pytest.mark.parametrize("flags", ["both", "complex", "mag", "logmag"])
+def test_stft_outputs_at_unaligned_offsets(dev, off_c, off_m, flags):
+    """The forward emits 16-B granules of each tile's contiguous output range; outputs
+    placed at 8-B / 4-B offsets inside larger buffers must be written bit-identically to
+    freshly allocated ones, and nothing outside the output range may be touched."""
+    x = torch.from_numpy(_sig(5, 5077, 11)).to(dev)  # T = 40: a full and a ragged tile per signal
+    kw = dict(complex_out=flags in ("both", "complex"), mag_out=flags != "complex", log=flags == "logmag")
+    Xr, mr = ops.stft(x, **kw)
+    T = ops.n_frames(x.shape[-1])
+    n_c, n_m = 5 * T * 129, 5 * T * 129
+    bc = torch.full((2 * n_c + 2 * off_c + 8,), float("nan"), device=dev)
+    bm = torch.full((n_m + off_m + 8,), float("nan"), device=dev)
+    oc = bc[2 * off_c:2 * off_c + 2 * n_c].view(5, T, 129, 2)
+    om_ = bm[off_m:off_m + n_m].view(5, T, 129)
+    ops.stft(x, out_c=oc if kw["complex_out"] else None, out_mag=om_ if kw["mag_out"] else None, **kw)
+    torch.cuda.synchronize()
+    if kw["complex_out"]:
+        assert torch.equal(oc, Xr)
+        assert torch.isnan(bc[:2 * off_c]).all() and torch.isnan(bc[2 * off_c + 2 * n_c:]).all()
+    if kw["mag_out"]:
+        assert torch.equal(om_, mr)
+        assert torch.isnan(bm[:off_m]).all() and torch.isnan(bm[off_m + n_m:]).all()
+
+
 def test_stft_frame_indices_bit_exact(dev):
     """An impulse at sample n must land exactly in the frames covering n."""
     N = 4000
