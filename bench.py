@@ -33,6 +33,18 @@ MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MF
 PMC_TAG = "r02_prof_b"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
 PMC_FILE = f"profiles/{PMC_TAG}_pmc.json"
 MFMA_FILE = f"profiles/{PMC_TAG}_mfma.json"
+BW_FILE = "profiles/r02_bw_probe.jsonl"  # tools/bw_probe.hip: plain 16-B streaming ceilings on MI355X
+
+
+def stream_ceiling(kind):
+    """Best GB/s of the `kind` stream mix in the committed probe (tools/bw_probe.hip), or None."""
+    try:
+        with open(os.path.join(ROOT, BW_FILE)) as f:
+            rows = [json.loads(l) for l in f if l.strip()]
+    except (OSError, ValueError):
+        return None
+    v = [r["GB/s"] for r in rows if r.get("kernel") == kind]
+    return max(v) if v else None
 
 
 def pmc_mfma_busy(kernel):
@@ -323,6 +335,10 @@ def main():
               "achieved": sa_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sa_gbs / HBM_PEAK_GBS,
               "traffic": pmc_traffic("stft_fwd_kernel", [stft_grid_threads(n_sa, T)]),
               "traffic_source": PMC_FILE, "launch_ms": sa_ms, "algorithmic_bytes": sa_bytes}
+        ceil = stream_ceiling("r1w3")
+        if ceil:  # the STFT moves 1 B in : 3 B out; plain streams of that mix peak here
+            sa.update({"stream_ceiling": ceil, "frac_of_stream_ceiling": sa_gbs / ceil,
+                       "stream_ceiling_source": BW_FILE + " (r1w3: one 16-B read : three 16-B write streams)"})
         del xs, Xs, Ms
 
     if rank == 0:
