@@ -35,6 +35,8 @@ SIGNATURES = {
     "dl4ss_gemm_gl_set_config": [I],
     "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
+    "dl4ss_birnn_fwd_xw": [I, I, I, I, P, I, LL, P, LL, P, P, P, P, P, P, P, P, P, P, LL, P, P, I],
+    "dl4ss_birnn_fwd_xw_supported": [I, I, I, I, I],
     "dl4ss_birnn_bwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_mask_attn_loss_ex": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
     "dl4ss_birnn_workspace_bytes": [I, I, I],

@@ -68,8 +68,11 @@ __device__ __forceinline__ u64 stamp_now() {
 }
 #define STAMP_DECL u64 st_prev = stamp_now(), st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define STAMP(i) { const u64 n_ = stamp_now(); st_acc[i] += n_ - st_prev; st_prev = n_; }
+#ifndef STAMP_T2
+#define STAMP_T2 NROLE  // the second recorded thread (320: the first prefetch wave of the packed forward)
+#endif
 #define STAMP_FLUSH                                                                   \
-  if (a.stamps && (threadIdx.x == 0 || threadIdx.x == NROLE))                        \
+  if (a.stamps && (threadIdx.x == 0 || threadIdx.x == STAMP_T2))                     \
     for (int i_ = 0; i_ < 8; ++i_) a.stamps[blockIdx.x * 16 + (threadIdx.x ? 8 : 0) + i_] = st_acc[i_];
 #else
 #define STAMP_DECL
@@ -177,6 +180,13 @@ struct RnnArgs {
   float* dbh;              // bwd: += sum_{b,t} dGh  (bias_hh gradient)
   float* dbpart;           // bwd: per-row bias sums [b][d][ih | hh][NGATE*H] (fixed-order reduce), or
                            //      null: float atomics straight into dbi / dbh
+  // fused input projection (packed forward, rnn_fwd_pk_kernel<.., true>): G is not read; each
+  // step's x_t W_ih^T + b_ih is formed in the kernel from the bf16 layer input
+  const unsigned short* Xb;    // (B*T, ldx) bf16 layer input rows, k < Kin (padding never read)
+  const unsigned short* Wihb;  // (2*NGATE*H, ldw) bf16 W_ih rows (direction-major), k < Kin
+  const float* bih;            // (2, NGATE*H)
+  int Kin;
+  long long ldx, ldw;
 };
 
 __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& group, int& w) {
@@ -213,6 +223,14 @@ struct StepLoader {
       if (dst[q] >= 0) lds[dst[q]] = v[q];
   }
 };
+
+// Fused input projection: the step's layer-input rows reach LDS by LDS-DMA (16 B per lane,
+// lane-linear 1-KB pieces): item i = b * 80 + c is 16-B chunk c (k = 8c .. 8c + 7) of batch row b
+// of the chunk, at element 8 i of a step buffer ([b][640] bf16).  Items past the data (c >= Kin / 8
+// rounded up, rows past B, the pad items of the last piece) read a global zero line.
+typedef __attribute__((address_space(3))) void lds_void_t;
+__device__ __attribute__((aligned(64))) const unsigned g_xzero_line[16] = {0};
+constexpr int XRING = 4;  // step buffers: x(s+1) consumed while x(s+2), x(s+3) are in flight
 
 // Poll the granules src[off[g]] (off < 0: nothing to read) until every tag == tag;
 // returns false on timeout.  Offsets are computed once per launch by the caller;
@@ -507,6 +525,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 // --------------------------------------------------------------------------
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int PKU = 24;     // staged h slots per (row, producer): 8 granules x 3
+constexpr int XKMAX = 2 * HMAX / 32;  // fused input projection: k-steps of 32 (Kin <= 2 HMAX)
+constexpr int SXB = XKMAX * 32;       // bf16 row stride of its B images (80 16-B chunks)
 constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
@@ -572,8 +592,9 @@ __device__ __forceinline__ bool group_needs_write_through(const u64* place, int 
   return force == 1 || !same;
 }
 
-template <int CELL, int BC>
+template <int CELL, int BC, int XK = 0>  // XK > 0: fused input projection over XK k-steps of 32
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
+  constexpr bool XW = XK > 0;
 #ifdef RNN_PRIO  // experiment: the recurrence waves win SIMD arbitration over co-resident GEMM waves
   __builtin_amdgcn_s_setprio(3);
 #endif
@@ -600,6 +621,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   float* sgate = smem + 8 * SHB;                                                        // [BC][MT*16]
   float* sin = sgate + BC * MT * 16;                                                    // [2][BC*32][4]
   unsigned short* spub = reinterpret_cast<unsigned short*>(sin + 2 * BC * 32 * 4);      // [BC][PKU]
+  // XW: XRING step buffers of the layer-input rows ([BC][SXB] bf16 + the pad items of the last
+  // DMA piece) and one zero row (the B-image rows >= BC), 16-B aligned
+  constexpr int NXQ = XW ? (BC * 80 + 127) / 128 : 1;  // DMA pieces per prefetch wave and step
+  constexpr int XBUF = NXQ * 128 * 8;                   // bf16 per step buffer
+  unsigned short* sxb = reinterpret_cast<unsigned short*>(
+      (reinterpret_cast<uintptr_t>(spub + BC * PKU) + 15) & ~static_cast<uintptr_t>(15));
+  unsigned short* sxz = sxb + XRING * XBUF;  // [SXB] zeros
 
   // ---- W_hh tile of this wave as bf16 A fragments: lane holds A[row tile*16 + (lane&15)][k]
   bf16x8 afrag[KSMAX];
@@ -618,6 +646,38 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   }
   for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;
   for (int i = tid; i < BC * PKU; i += NT) spub[i] = 0;
+  if (XW)
+    for (int i = tid; i < SXB / 2; i += NT) reinterpret_cast<unsigned*>(sxz)[i] = 0u;
+
+  // ---- XW: W_ih tile of this wave (the same gate rows as its W_hh tile) as bf16 A fragments,
+  //      A[row tile*16 + (lane&15)][k = ks*32 + 8(lane>>4) + j], k >= Kin zero; and the b_ih of
+  //      the lane's four output rows 4(lane>>4) + i
+  bf16x8 wfrag[XW ? XK : 1];
+  float bir[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (XW) {
+    const int rl = tile * 16 + (lane & 15);
+    const int q = rl / J, u = rl % J;
+    const bool rv = mv && rl < R && j0 + u < H;
+    const unsigned short* wrow = a.Wihb + ((long long)d * GH + q * H + j0 + u) * a.ldw;
+    // one 16-B load per fragment (rows 16-B aligned: ldw % 8 == 0); the chunk holding k = Kin
+    // element by element, chunks past it zero
+#pragma unroll
+    for (int ks = 0; ks < XK; ++ks) {
+      const int k0 = ks * 32 + 8 * (lane >> 4);
+      if (rv && k0 + 8 <= a.Kin) {
+        wfrag[ks] = *reinterpret_cast<const bf16x8*>(wrow + k0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wfrag[ks][j] = (short)((rv && k0 + j < a.Kin) ? wrow[k0 + j] : 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = tile * 16 + 4 * (lane >> 4) + i;
+      const int qq = rr / J, uu = rr % J;
+      bir[i] = (mv && rr < R && j0 + uu < H) ? a.bih[(long long)d * GH + qq * H + j0 + uu] : 0.0f;
+    }
+  }
 
   // ---- cell lanes (waves 0-3): row cb = tid / 32, unit cu = tid % 32 (< J)
   const int cb = tid >> 5, cu = tid & 31;
@@ -660,10 +720,86 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     ld.shift[q] = 0;
     ld.dst[q] = on ? ((cell / J) * 32 + iu) * 4 + gate : -1;
   }
-  if (pfw) ld.issue(d == 0 ? 0 : T - 1, T);
+  // XW: per-lane sources of this prefetch wave's DMA pieces (item i = q*128 + (wave-5)*64 + lane)
+  const unsigned short* xsrc[NXQ];
+  if constexpr (XW) {
+#pragma unroll
+    for (int q = 0; q < NXQ; ++q) {
+      const int i = q * 128 + (wv - WPOLL - 1) * 64 + lane;
+      const int b = i / 80, c = i % 80;
+      const bool on = pfw && b < BC && 8 * c < a.Kin && b0 + b < a.B;
+      xsrc[q] = on ? a.Xb + (long long)(b0 + b) * T * a.ldx + 8 * c : nullptr;
+    }
+  }
+  // DMA of step u's rows into ring buffer u % XRING (prefetch waves only)
+  auto xdma = [&](int u) {
+    const long long toff = (long long)(d == 0 ? u : T - 1 - u) * a.ldx;
+    unsigned short* dst = sxb + (u % XRING) * XBUF + (wv - WPOLL - 1) * 64 * 8;
+#pragma unroll
+    for (int q = 0; q < NXQ; ++q) {
+      const void* src = xsrc[q] ? (const void*)(xsrc[q] + toff) : (const void*)g_xzero_line;
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(dst + q * 128 * 8), 16, 0, 0);
+    }
+  };
+  // wait until step u's pieces landed; those of the `ahead` later steps issued after them (when
+  // < T) may stay in flight
+  auto xwait = [&](int u, int ahead) {
+    const int later = min(T - 1 - u, ahead);
+    if (later >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NXQ) : "memory");
+    else if (later == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NXQ) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  if (XW && pfw) {
+    for (int u = 0; u < min(T, XRING - 1); ++u) xdma(u);
+    xwait(0, XRING - 2);
+  } else if (!XW && pfw) {
+    ld.issue(d == 0 ? 0 : T - 1, T);
+  }
   __syncthreads();
   const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
   STAMP_DECL
+
+  // XW: G[b][rows of this tile] of the step whose inputs sit in B image `buf` -> sin[sb]:
+  // x W_ih^T as one accumulator chain over the k-steps in order, then + b_ih (the separate
+  // GEMM's arithmetic: gemm_gl's k-loop and bias epilogue)
+  auto xproj = [&](int buf, int sb) {
+    if (!mv) return;
+    const unsigned short* bp = ((lane & 15) < BC ? sxb + buf * XBUF + (lane & 15) * SXB : sxz) + 8 * (lane >> 4);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    // k-steps past Kin multiply zero fragments (exact); the B reads of batch i+1 are issued
+    // before the MFMAs of batch i, so the chain waits on MFMA latency, not on LDS round trips
+    constexpr int XB = 5, NB = (XK + XB - 1) / XB;
+    bf16x8 cur[XB], nxt[XB];
+#pragma unroll
+    for (int i = 0; i < XB; ++i) cur[i] = i < XK ? *reinterpret_cast<const bf16x8*>(bp + i * 32) : bf16x8{};
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+      if (bb + 1 < NB) {
+#pragma unroll
+        for (int i = 0; i < XB; ++i) {
+          const int ks = (bb + 1) * XB + i;
+          nxt[i] = ks < XK ? *reinterpret_cast<const bf16x8*>(bp + ks * 32) : bf16x8{};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < XB; ++i)
+        if (bb * XB + i < XK) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfrag[bb * XB + i], cur[i], acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < XB; ++i) cur[i] = nxt[i];
+    }
+    const int col = lane & 15;
+    if (col < BC) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = tile * 16 + 4 * (lane >> 4) + i;
+        if (rr < R) sin[sb * BC * 32 * 4 + (col * 32 + rr % J) * 4 + rr / J] = acc[i] + bir[i];
+      }
+    }
+  };
+  if (XW) xproj(0, 0);  // G of step 0 (its rows landed before the barrier above; the zero row too)
 
   auto matvec = [&]() {  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
     if (!mv) return;
@@ -828,12 +964,26 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   }
   if (pfw) {
     for (int s = 0; s < T; ++s) {
-      ld.commit(sin + (s & 1) * BC * 32 * 4);
-      if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
+      if (!XW) {
+        ld.commit(sin + (s & 1) * BC * 32 * 4);
+        if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
+      }
+      STAMP(0)
       __syncthreads();  // B1
+      STAMP(1)
       matvec();
+      // XW: step s+1's rows landed before B2 (xproj(s+1) follows it); step s+2's may be in flight
+      if (XW && s + 1 < T) xwait(s + 1, 1);
+      STAMP(2)
       __syncthreads();  // B2
+      STAMP(3)
+      if (XW && s + 1 < T) xproj((s + 1) % XRING, (s + 1) & 1);
+      // step s+3's rows into buffer (s+3) % XRING, issued after B2 (off the matvec -> B2 path); that
+      // buffer was last read by xproj of step s-1, before B1(s-1)
+      if (XW && s + XRING - 1 < T) xdma(s + XRING - 1);
+      STAMP(4)
     }
+    STAMP_FLUSH
     return;
   }
   for (int s = 0; s < T; ++s) {
@@ -908,6 +1058,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       hst = hn;
     }
     STAMP(4)
+    // XW: step s+1's input projection while the hand-off of step s travels (its B image was
+    // committed before B2; sin[(s+1)&1] was last read by the cell phase of step s-1)
+    if (XW && s + 1 < T) xproj((s + 1) % XRING, (s + 1) & 1);
   }
   STAMP_FLUSH
 }
@@ -1864,6 +2017,10 @@ int launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStr
       return launch_resident(rnn_fwd_kernel<CELL, BC, 0, false, HMAX_L>, grid, smem, st, a);
   }
   // compile-time k-slice lengths for the shipped H = 300 plans (LSTM J=20: 52, GRU J=20: 40)
+  if (mf && pk && a.Xb && a.Kin <= 5 * 32)  // the nets' first layer: 129 features
+    return launch_resident(rnn_fwd_pk_kernel<CELL, BC, 5>, grid, smem, st, a);
+  if (mf && pk && a.Xb)
+    return launch_resident(rnn_fwd_pk_kernel<CELL, BC, XKMAX>, grid, smem, st, a);
   if (mf && pk)
     return launch_resident(rnn_fwd_pk_kernel<CELL, BC>, grid, smem, st, a);
   else if (mf)
@@ -2062,6 +2219,59 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
   const size_t smem = pk ? p.smem_fwd_pk : mf ? p.smem_fwd_mf : p.smem_fwd;
   return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, mf, pk, p.BC, a, grid, smem, st)
                            : dispatch<CELL_GRU>(true, mf, pk, p.BC, a, grid, smem, st);
+}
+
+// 1 when the packed bf16 forward (the only one with the fused input projection) applies to
+// (cell, B, H, T) and the layer input width Kin: dl4ss_birnn_fwd_xw may be called
+DL4SS_API int dl4ss_birnn_fwd_xw_supported(int cell, int B, int T, int H, int Kin) {
+  if (!(cell == CELL_LSTM || cell == CELL_GRU) || B <= 0 || T <= 0 || H <= 0 || Kin <= 0) return 0;
+  Plan p;
+  if (!make_plan(cell, B, H, p, true)) return 0;
+  return (p.fwd_pk && T < 65535 && Kin <= XKMAX * 32) ? 1 : 0;
+}
+
+// dl4ss_birnn_fwd_ex with the input projection fused into the recurrence (bf16 mode only): instead
+// of reading G = X W_ih^T + b_ih from a separate GEMM, every workgroup forms its own gate rows of
+// step t+1 with MFMAs while step t's hand-off travels.  x_bf16: (B*T, ldx) bf16 layer input rows
+// (16-B chunks: padding up to the next multiple of 8 finite); W_ih_bf16: (2*NGATE*H, ldw) bf16 (direction-major rows, the GEMM's B operand); b_ih
+// (2, NGATE*H) fp32.  ldx, ldw multiples of 8 and both bases 16-B aligned.  Same summation order as
+// the GEMM path (one k-ordered MFMA chain, then + b_ih): the outputs match it bit for bit.
+DL4SS_API int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf16, int Kin, long long ldx,
+                                 const void* W_ih_bf16, long long ldw, const float* b_ih, const float* W_hh,
+                                 const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                                 void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream,
+                                 int ws_zeroed) {
+  DL4SS_REQUIRE(dl4ss_birnn_fwd_xw_supported(cell, B, T, H, Kin));
+  DL4SS_REQUIRE(x_bf16 && W_ih_bf16 && b_ih && W_hh && b_hh && out && act && workspace && status);
+  DL4SS_REQUIRE(cell == CELL_GRU || cs);
+  DL4SS_REQUIRE(hprev || cell == CELL_LSTM);
+  DL4SS_REQUIRE(ldx >= Kin && ldw >= Kin && ldx % 8 == 0 && ldw % 8 == 0);
+  DL4SS_REQUIRE((reinterpret_cast<uintptr_t>(x_bf16) & 15) == 0 && (reinterpret_cast<uintptr_t>(W_ih_bf16) & 15) == 0);
+  Plan p;
+  DL4SS_REQUIRE(make_plan(cell, B, H, p, true));
+  DL4SS_REQUIRE(ws_bytes >= workspace_bytes(p, H));
+  hipStream_t st = as_stream(stream);
+  const long long groups = 2LL * p.nchunk;
+  if (!ws_zeroed) {
+    hipError_t e = hipMemsetAsync(workspace, 0, groups * 4 * p.BC * p.NG * 8 * 8, st);
+    if (e != hipSuccess) return (int)e;
+  }
+  RnnArgs a{};
+  fill_args(a, p, B, T, H);
+  a.G = nullptr; a.Whh = W_hh; a.bhh = b_hh; a.out = out; a.hprev = hprev; a.act = act; a.cs = cs;
+  a.outb = reinterpret_cast<unsigned short*>(out_bf16);
+  a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
+  a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
+  a.status = status;
+  a.Xb = reinterpret_cast<const unsigned short*>(x_bf16);
+  a.Wihb = reinterpret_cast<const unsigned short*>(W_ih_bf16);
+  a.bih = b_ih;
+  a.Kin = Kin; a.ldx = ldx; a.ldw = ldw;
+  const int grid = (int)(groups * p.NG);
+  const int nxq = (p.BC * 80 + 127) / 128;
+  const size_t smem = (p.smem_fwd_pk + 15) / 16 * 16 + (XRING * nxq * 128 * 8 + SXB) * sizeof(unsigned short);
+  return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, true, true, p.BC, a, grid, smem, st)
+                           : dispatch<CELL_GRU>(true, true, true, p.BC, a, grid, smem, st);
 }
 
 DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, const float* dOut,

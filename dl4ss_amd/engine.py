@@ -190,6 +190,17 @@ class SepTrainer:
         # workgroups share CUs with the persistent recurrence and slow every hand-off more
         # than the hidden GEMM time saves.
         self.overlap = self.gemm_path != "bb" and os.environ.get("DL4SS_OVERLAP", "0") == "1"
+        # Forward input projections x W_ih^T + b_ih formed inside the packed recurrence kernel
+        # (dl4ss_birnn_fwd_xw) instead of a gemm_gl launch + a G buffer round trip; bitwise the same
+        # G (tests/test_rnn_xw_gpu.py).  DL4SS_RNN_XW: "l0" (default) the first layer only (129
+        # features, 5 MFMA k-steps per step: 341-352 us vs 333-338 + 30 us for recurrence + GEMM),
+        # "1" every layer (600-wide inputs, 20 k-steps: 423-435 vs 333-338 + 52 us -- the per-step
+        # MFMA chain of the cell waves outlasts the hand-off), "0" none.
+        xw = os.environ.get("DL4SS_RNN_XW", "l0")
+        if xw not in ("0", "1", "l0"):
+            raise ValueError(f"DL4SS_RNN_XW={xw}: expected 0, 1 or l0")
+        self.xw = self.fast and self.gemm_path == "gl" and xw != "0"
+        self.xw_kmax = 160 if xw == "l0" else 640
         self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
@@ -272,8 +283,18 @@ class SepTrainer:
         xb = self.xb0[:, :x.shape[1]]
         for l in range(net.L):
             D = xb.shape[1]
-            self._gemm_fwd(xb, self.wb_ih[l][:, :D], net.cat_view("bias_ih", l), self.G)
             hp = self.hprev[l]
+            if self.xw and D <= self.xw_kmax and _lib.query("dl4ss_birnn_fwd_xw_supported", cell, B, T, H, D) == 1:
+                wih = self.wb_ih[l]
+                _lib.call("dl4ss_birnn_fwd_xw", cell, B, T, H, _lib.ptr(xb, strided=True), D, xb.stride(0),
+                          _lib.ptr(wih), wih.stride(0), _lib.ptr(net.cat_view("bias_ih", l)),
+                          _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
+                          _lib.ptr(self.out[l]), _lib.ptr(hp), _lib.ptr(self.act[l]),
+                          _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.outb[l]), _lib.ptr(self.hprevb[l]),
+                          _lib.ptr(self._ws_slot(l, False)), self.ws_bytes, _lib.ptr(self.status), st, 1)
+                xb = self.outb[l][:, :2 * H]
+                continue
+            self._gemm_fwd(xb, self.wb_ih[l][:, :D], net.cat_view("bias_ih", l), self.G)
             _lib.call("dl4ss_birnn_fwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(self.G),
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
                       _lib.ptr(self.out[l]), _lib.ptr(hp), _lib.ptr(self.act[l]),

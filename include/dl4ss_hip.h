@@ -173,6 +173,22 @@ int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, const float* G
 int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
                        const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
                        void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream);
+/* dl4ss_birnn_fwd_ex with the input projection fused into the recurrence (bf16 packed kernel):
+ * no G buffer and no separate GEMM -- every workgroup forms x_t W_ih^T + b_ih of its own gate rows
+ * with MFMAs while the previous step's hand-off travels.  x_bf16 (B*T, ldx) bf16 layer input rows
+ * (read in 16-B chunks: the row padding up to the next multiple of 8 must be finite, e.g. zero), W_ih_bf16 (2*NGATE*H, ldw) bf16, b_ih (2, NGATE*H); ldx, ldw multiples of 8,
+ * x_bf16 and W_ih_bf16 16-B aligned.  Bitwise equal to gemm_gl (G = x W_ih^T + b_ih) followed by
+ * dl4ss_birnn_fwd_ex.  Replaces the same reference lines as dl4ss_birnn_fwd (the cuDNN LSTM / GRU of
+ * TDAA_beta/main_run_sstune_EvalVer.py:282-293, whose input projection is part of that call).
+ * ws_zeroed: the caller already zeroed the hand-off area. */
+int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf16, int Kin, long long ldx,
+                       const void* W_ih_bf16, long long ldw, const float* b_ih, const float* W_hh,
+                       const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                       void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream,
+                       int ws_zeroed);
+/* 1 when dl4ss_birnn_fwd_xw applies to (cell, B, T, H, Kin) (the packed bf16 plan exists, Kin <= 640);
+ * host-only. */
+int dl4ss_birnn_fwd_xw_supported(int cell, int B, int T, int H, int Kin);
 /* BPTT of one layer: dOut (B,T,2H) (+ dOut_bcast (B,2H) at every t, may be NULL) ->
  * dG (B,T,2,NG*H) grad of the input projection (pre-activation) and, for GRU, dGh
  * grad of W_hh h + b_hh (for LSTM they coincide; dGh may be NULL). */
