@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_TAG = "r02_prof_d"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
+PMC_TAG = "r02_prof_e"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
 PMC_FILE = f"profiles/{PMC_TAG}_pmc.json"
 MFMA_FILE = f"profiles/{PMC_TAG}_mfma.json"
 BW_FILE = "profiles/r02_bw_probe.jsonl"  # tools/bw_probe.hip: plain 16-B streaming ceilings on MI355X
