@@ -37,3 +37,15 @@ def test_grid_never_exceeds_budget(B):
             if p["BC"] > 1:
                 narrower = 2 * ((B + p["BC"] // 2 - 1) // (p["BC"] // 2)) * p["NG"]
                 assert narrower > budget
+
+
+def test_fused_projection_support_is_host_only():
+    """dl4ss_birnn_fwd_xw_supported answers from the plan alone (no device call): the packed
+    bf16 plan of the nets' H = 300 exists at any batch, input widths up to 2 HMAX = 640; the
+    H = 600 classifier has no packed plan."""
+    from dl4ss_amd import _lib
+    q = lambda *a: _lib.query("dl4ss_birnn_fwd_xw_supported", *a)
+    assert q(0, 32, 251, 300, 129) == 1 and q(0, 32, 251, 300, 600) == 1 and q(1, 1, 2, 300, 600) == 1
+    assert q(0, 32, 251, 300, 641) == 0
+    assert q(0, 32, 251, 600, 600) == 0
+    assert q(2, 32, 251, 300, 600) == 0 and q(0, 0, 251, 300, 600) == 0
