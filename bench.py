@@ -33,6 +33,8 @@ MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MF
 PMC_TAG = "r02_prof_e"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
 PMC_FILE = f"profiles/{PMC_TAG}_pmc.json"
 MFMA_FILE = f"profiles/{PMC_TAG}_mfma.json"
+# the in-step input-projection kernel as rocprofv3 names it (its MFMA-busy counter is looked up by it)
+GEMM_GL_INPROJ = "gemm_gl_kernel<true, true, 0, false, Cfg<128, 2> >"
 BW_FILE = "profiles/r02_bw_probe.jsonl"  # tools/bw_probe.hip: plain 16-B streaming ceilings on MI355X
 
 
@@ -287,13 +289,13 @@ def main():
     stft_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["stft"]]))
     stft_bytes = B * (K + 1) * (4 * N + 4 * T * F)  # mag-only STFT of mixture + K sources
     # input-projection GEMM of BiLSTM layer 2 (M = B*T, N = 2400, K = 600, bias fused), timed in
-    # isolation with the step's own kernel and operands: in bf16 mode gemm_bb.hip on the bf16 h
+    # isolation with the step's own kernel and operands: in bf16 mode gemm_gl.hip on the bf16 h
     # the layer-1 recurrence wrote and the bf16 W_ih copy (the in-step launch), else gemm.hip fp32
     bih = net.cat_view("bias_ih", 1)
     if tr.fast:
         xb, wb = tr.outb[0][:, :2 * net.H], tr.wb_ih[1][:, :2 * net.H]
         run_gemm = lambda: tr._gemm_fwd(xb, wb, bih, tr.G)  # noqa: E731
-        gemm_kernel = "gemm_gl_kernel<true, true, 0, false>" if tr.gemm_path == "gl" else "gemm_bb_kernel"
+        gemm_kernel = GEMM_GL_INPROJ if tr.gemm_path == "gl" else "gemm_bb_kernel"
         gemm_name = f"{gemm_kernel} (bf16 operands, in-step BiLSTM layer-2 input projection 8032x2400x600 + bias)"
     else:
         x, wih = tr.out[0].view(B * T, -1), net.cat_view("weight_ih", 1)
