@@ -612,6 +612,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const int j0 = w * J;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
+#ifdef RNN_CELLPRIO  // experiment: the cell / publish waves (0-3) win SIMD arbitration over the polling waves
+  if (wv < 4) __builtin_amdgcn_s_setprio(RNN_CELLPRIO);
+#endif
   const int GH = NGATE * H;
   const int tile = wv < WPOLL ? wv : wv - 1;
   const bool mv = wv != WPOLL && tile < MT;
@@ -828,6 +831,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   };
 
   if (pollw) {
+#ifdef RNN_POLLPRIO  // experiment: the polling waves win SIMD arbitration
+    __builtin_amdgcn_s_setprio(RNN_POLLPRIO);
+#endif
     // ---- polling wave(s): 16-B unit idx = (b * NG + producer) * 4 + pair; lane holds
     //      units lane + 64 (g FWD_NPW + pwv) (idle lanes re-read unit 0: every load is
     //      unconditional, so the compiler can keep a sweep in flight behind a counted vmcnt)
@@ -1441,6 +1447,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   const int j0 = w * J;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
+#ifdef RNN_CELLPRIO  // experiment: the cell / publish waves (0-3) win SIMD arbitration over the polling waves
+  if (wv < 4) __builtin_amdgcn_s_setprio(RNN_CELLPRIO);
+#endif
   const int GH = NGATE * H;
   const int AH = 4 * H;
   const int HG = ((H + 1) / 2 + 1) & ~1;  // granules per (producer, row), even: 16-B aligned rows
@@ -1530,6 +1539,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   STAMP_DECL
 
   if (wv >= WPOLL && wv < WPF) {
+#ifdef RNN_POLLPRIO
+    __builtin_amdgcn_s_setprio(RNN_POLLPRIO);
+#endif
     // ---- polling waves: 16-B unit idx = (producer * BC + b) * (J/4) + quad, wave pw
     //      takes the 64-unit blocks pw, pw + BWD_NPW, ...
     constexpr int GLK = (80 * BC + 64 * BWD_NPW - 1) / (64 * BWD_NPW);  // NG <= 16, J <= 20
