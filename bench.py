@@ -1,18 +1,33 @@
-"""Benchmark: mixtures/sec of the full separation training step on MI355X.
+"""Benchmark: mixtures/sec of the separation training step on MI355X, 1..8 GPUs of one node.
 
-Workload (BASELINE.json configs[1] "2-spk PIT BiLSTM magnitude mask bf16, batch=32",
-SURVEY section 8d C2): 2-speaker synthetic WSJ0-shaped mixtures, 8 kHz, 4 s
-(N = 32000 -> T = 251, F = 129), BiLSTM-4L (H = 300) mask net, Linear(600 -> 129*50)
-+ tanh, embedding + ADDJUST queries, PIT MSE + 0.5 sum-to-one loss, backward,
-(DP all-reduce), Adam; bf16 GEMM / recurrent-matvec operands with fp32 accumulate,
-fp32 state, loss, gradients and optimizer --
-32 mixtures per GPU per step (weak scaling).  Inputs (raw sources, gains,
-speaker ids) are resident in HBM before the timed region; the step starts at
-preprocessing + STFT.
+Workloads (BASELINE.json configs; ``--config``, default C2):
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32] [--mode pit|label]
+* C2 (default, the headline: configs[1] "2-spk PIT BiLSTM magnitude mask bf16, batch=32"):
+  2-speaker synthetic WSJ0-shaped mixtures, 8 kHz, 4 s (N = 32000 -> T = 251, F = 129),
+  BiLSTM-4L (H = 300) mask net, Linear(600 -> 129*50) + tanh, embedding + ADDJUST queries,
+  PIT MSE + 0.5 sum-to-one loss, backward, DP all-reduce, Adam; bf16 GEMM / recurrent-matvec
+  operands with fp32 accumulate, fp32 state, loss, gradients and optimizer -- 32 mixtures per
+  GPU per step (weak scaling).
+* C4 (configs[3] "3-spk mix at mixed SNR, DP over 8x MI355X with RCCL all-reduce"): 3-speaker
+  mixtures with the predata_multiAims_3dB gains, BiGRU-2L without ADDJUST (the selfSS_dB
+  model), K = 3 PIT, B = 32 per GPU, one flat RCCL gradient all-reduce per step.
+* C5 (configs[4] "recu path, DP over 8x MI355X"): recursive extraction (classifier BiLSTM-3L
+  H = 600 + BiGRU-2L mask net, 2 extraction steps, final masks, iSTFT of both estimates),
+  B = 1 mixture per replica per step (the reference's batch); replicas only -- no gradients,
+  no collective in the step -- and one all-gather of every rank's extracted speaker ids after
+  the timed region (the final metric gather).
 
-N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL).
+Inputs (raw sources, gains, speaker ids) are resident in HBM before the timed region; a
+training step starts at preprocessing + STFT.
+
+  python bench.py [--gpus N] [--config C2|C4|C5] [--steps K] [--warmup W] [--precision bf16|fp32]
+                  [--mode pit|label]
+
+With N > 1 and no WORLD_SIZE in the environment, this process starts the N ranks itself
+(``torch.distributed.run`` as a child process, before any GPU call here) and exits with its
+code; under torch.distributed.run (the driver's form) WORLD_SIZE must equal --gpus.
+``--standin`` replaces the GPU step by a small CPU oracle step over gloo: it exercises only the
+launcher, the barrier / max-over-ranks timing and the JSON line (tests/test_bench_launch_cpu.py).
 """
 import argparse
 import json
@@ -100,12 +115,25 @@ def pmc_traffic(kernel, grids):
     return total
 
 
-def parse():
+CONFIGS = {
+    # name: mask net, speakers, per-GPU batch, samples (SURVEY 8 "Configs")
+    "C2": dict(kind="train", cell="lstm", L=4, K=2, adjust=True, B=32, N=32000,
+               what="C2: 2-spk {mode} BiLSTM-4L magnitude mask (EvalVer model)"),
+    "C4": dict(kind="train", cell="gru", L=2, K=3, adjust=False, B=32, N=32000,
+               what="C4: 3-spk mixed-SNR {mode} BiGRU-2L magnitude mask (selfSS_dB model, 3dB gains)"),
+    "C5": dict(kind="recursive", K=2, B=1, N=32000,
+               what="C5: recursive extraction replicas (classifier BiLSTM-3L H=600 + BiGRU-2L mask net, "
+                    "2 steps, final masks + iSTFT)"),
+}
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--mode", default="pit", choices=["label", "pit"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,7 +144,40 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--dist", action="store_true",
                     help="initialise the RCCL process group even at world size 1 (exercises the DP path)")
-    return ap.parse_args()
+    ap.add_argument("--standin", action="store_true",
+                    help="CPU stand-in step over gloo (launcher / timing test only; not a measurement)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """Start n ranks of this script under torch.distributed.run (one process per GPU, RCCL) as
+    a CHILD process and return its exit code.  Nothing here has touched the GPU: the parent
+    only imported torch, so no initialised HIP runtime is replaced or inherited."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.run(cmd, env=env).returncode
+
+
+def world_from_env(gpus):
+    """(world, rank, local rank) of this process; fails loudly when --gpus and the launcher disagree."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch N ranks with --gpus N")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
 def cpu_threads():
@@ -135,19 +196,20 @@ def cpu_threads():
     return n
 
 
-def cpu_baseline(args, N, K, with_classifier=False):
+def cpu_baseline(args, cfg, with_classifier=False):
     """Reference CPU path (the oracle restatement, torch-CPU fp32 + numpy FFT) on a
-    bounded sample of the same workload: cpu_steps steps of the B = 32 batch.  With
+    bounded sample of the same workload: cpu_steps steps of the cpu_batch batch.  With
     ``with_classifier`` each step also runs the speaker classifier's forward (BiLSTM-3L,
     H = 600, EvalVer.py:592 / 305-326), which the reference computes and then discards
     (its output is replaced by the ground truth, :598-599): the reference-faithful cost."""
     from oracle import dsp, model as om, recursive as orec
     from dl4ss_amd import synth
 
+    K, N = cfg["K"], cfg["N"]
     cores = cpu_threads()
     torch.set_num_threads(cores)
     torch.manual_seed(1)
-    ref = om.SepModel(cell="lstm", num_layers=4)
+    ref = om.SepModel(cell=cfg["cell"], num_layers=cfg["L"], adjust=cfg["adjust"])
     opt = om.make_adam(ref)
     cls = orec.Classifier(hidden=600, num_layers=3) if with_classifier else None
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1)
@@ -174,30 +236,217 @@ def cpu_baseline(args, N, K, with_classifier=False):
         one_step()
     dt = time.perf_counter() - t0
     what = "+ classifier BiLSTM-3L H=600 fwd (reference-faithful) " if with_classifier else "(mask path) "
+    net = f"{'BiLSTM' if cfg['cell'] == 'lstm' else 'BiGRU'}-{cfg['L']}L"
     return {"value": args.cpu_batch * args.cpu_steps / dt, "unit": "mixtures/s", "cores": cores, "kind": "port",
-            "sample": f"{args.cpu_steps} step(s) of the B={args.cpu_batch} batch, oracle torch-CPU fp32 BiLSTM-4L "
-                      f"fwd+{args.mode} loss+bwd+Adam incl. numpy STFT features {what}on {cores} thread(s)",
+            "sample": f"{args.cpu_steps} step(s) of the B={args.cpu_batch} batch, oracle torch-CPU fp32 {net} "
+                      f"fwd+{args.mode} loss (K={K})+bwd+Adam incl. numpy STFT features {what}on {cores} thread(s)",
             "seconds": dt}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+def cpu_baseline_recursive(args, cfg):
+    """The oracle's recursive extraction (oracle/recursive.py, GRID.py:383-475) on the host cores,
+    one mixture at a time as the reference runs it: numpy STFT features, classifier BiLSTM-3L
+    H = 600 and BiGRU-2L mask net twice, final masks (no iSTFT: the GPU line's extra work)."""
+    from oracle import dsp, model as om, recursive as orec
+    from dl4ss_amd import synth
+
+    N = cfg["N"]
+    cores = cpu_threads()
+    torch.set_num_threads(cores)
+    torch.manual_seed(1)
+    mix = om.MixSpeech("gru", 129, 300, 2, 50)
+    cls = orec.Classifier(129, 600, 3, 101)
+    emb = torch.randn(101, 50)
+    gen = synth.SyntheticMixtures(n_samples=N, k=2, seed=5)
+    n = max(2, args.cpu_steps)
+    src, spk, u = gen.batch(n + 1)
+    gains = synth.gains_for(u, 2)
+
+    def one(b):
+        _, m = dsp.mix_sources([dsp.normalise_source(src[b, k], N) for k in range(2)], gains[b])
+        X = torch.from_numpy(np.asarray(dsp.magnitude(m), np.float32))[None]
+        with torch.no_grad():
+            orec.recursive_extract(lambda x: mix(x), cls, emb, X)
+
+    one(n)  # warm-up
+    t0 = time.perf_counter()
+    for b in range(n):
+        one(b)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "mixtures/s", "cores": cores, "kind": "port",
+            "sample": f"{n} single-mixture recursive extractions (oracle/recursive.py: classifier BiLSTM-3L H=600 + "
+                      f"BiGRU-2L, 2 steps, final masks), torch-CPU fp32 on {cores} thread(s)",
+            "seconds": dt}
+
+
+def standin_main(args, world, rank):
+    """--standin: the launcher / timing contract on CPU (gloo).  One 'step' = an oracle training
+    step of a tiny BiGRU on this rank's synthetic shard + the flat-gradient all-reduce + Adam."""
+    import torch.distributed as dist
+
+    from dl4ss_amd import dp, synth
+    from oracle import dsp, model as om
+
     pg = None
-    if world > 1 or args.dist:
+    if world > 1:
+        dist.init_process_group("gloo")
+        pg = dist.group.WORLD
+    torch.set_num_threads(1)
+    B, K, N = args.batch or 2, 2, 2000
+    torch.manual_seed(0)
+    model = om.SepModel(cell="gru", num_layers=1, hidden=32, emb=8)
+    params = list(model.parameters())
+    flat = torch.cat([p.detach().reshape(-1) for p in params])
+    dp.broadcast_params_(flat, pg)
+    off = 0
+    with torch.no_grad():
+        for p in params:
+            p.copy_(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+    opt = om.make_adam(model)
+    src, spk, u = synth.SyntheticMixtures(n_samples=N, k=K, seed=1, rank=rank).batch(B)
+    gains = synth.gains_for(u, K)
+    feats, Y = [], []
+    for b in range(B):
+        s, m = dsp.mix_sources([dsp.normalise_source(src[b, k], N) for k in range(K)], gains[b])
+        feats.append(dsp.magnitude(m))
+        Y.append(np.stack([dsp.magnitude(s[k]) for k in range(K)]))
+    f, Yt, sp = torch.from_numpy(np.array(feats)), torch.from_numpy(np.array(Y)), torch.from_numpy(spk)
+
+    def step():
+        opt.zero_grad()
+        mask, _, _, _ = model(f, sp)
+        loss, _ = om.loss_label_ordered(mask, f, Yt)
+        loss.backward()
+        g = dp.allreduce_mean_(torch.cat([p.grad.reshape(-1) for p in params]), pg)
+        o = 0
+        for p in params:
+            p.grad.copy_(g[o:o + p.numel()].view_as(p))
+            o += p.numel()
+        opt.step()
+        return float(loss)
+
+    for _ in range(args.warmup):
+        step()
+    if pg is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if pg is not None:
+        dist.barrier()
+    elapsed = dp.max_over_ranks(time.perf_counter() - t0, "cpu", pg)
+    # every rank holds the same weights after the synchronous steps
+    w = torch.cat([p.detach().reshape(-1) for p in params])
+    w_max = dp.max_over_ranks(float(w.sum()), "cpu", pg)
+    w_min = -dp.max_over_ranks(-float(w.sum()), "cpu", pg)
+    if rank == 0:
+        print(json.dumps({"metric": "mixtures/sec (CPU stand-in step; launcher test only, not a measurement)",
+                          "value": B * world * args.steps / elapsed, "unit": "mixtures/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                          "data": "synthetic, CPU stand-in (oracle tiny BiGRU step over gloo)",
+                          "config": {"workload": "standin", "global_batch": B * world, "parallelism": f"dp{world}"},
+                          "loss": loss, "replicas_in_sync": w_max == w_min}), flush=True)
+    if pg is not None:
+        dist.destroy_process_group()
+
+
+def stft_instep_graph(tr, B, K, N, reps=10):
+    """The in-step STFT pair (mixtures, then sources; magnitude only) as the step runs it: both
+    launches captured `reps` times into one HIP graph and replayed between two events on the
+    stream the graph runs on, so the per-pair time is kernel time plus in-graph gaps, not the
+    host launch path of eager re-launches."""
+    from dl4ss_amd import ops
+
+    def pair():
+        ops.stft(tr.mix, complex_out=False, mag_out=True, out_mag=tr.mag_mix)
+        ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
+
+    pair()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            pair()
+    g.replay()  # untimed first replay
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / (3 * reps)
+
+
+def stft_standalone(dev, N, T):
+    """The north-star STFT roofline measurement: one launch over 4096 signals of N samples,
+    complex + magnitude out (>= 2048 signals, ~2.1 GB of traffic per launch), HIP-event average
+    of 10 launches on the launch stream (torch's current stream)."""
+    from dl4ss_amd import ops
+
+    n_sa = 4096
+    xs = torch.randn(n_sa, N, device=dev)
+    Xs = torch.empty(n_sa, T, 129, 2, device=dev)
+    Ms = torch.empty(n_sa, T, 129, device=dev)
+    for _ in range(3):
+        ops.stft(xs, out_c=Xs, out_mag=Ms)
+    h0, h1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    h0.record()
+    for _ in range(10):
+        ops.stft(xs, out_c=Xs, out_mag=Ms)
+    h1.record()
+    torch.cuda.synchronize()
+    sa_ms = h0.elapsed_time(h1) / 10
+    sa_bytes = n_sa * (4 * N + 12 * T * 129)
+    sa_gbs = sa_bytes / (sa_ms * 1e-3) / 1e9
+    sa = {"bound": "hbm", "kernel": f"stft_fwd (one launch: {n_sa} signals x N={N}, complex + magnitude; "
+                                    "the north-star STFT roofline measurement)",
+          "achieved": sa_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sa_gbs / HBM_PEAK_GBS,
+          "traffic": pmc_traffic("stft_fwd_kernel", [stft_grid_threads(n_sa, T)]),
+          "traffic_source": PMC_FILE, "launch_ms": sa_ms, "algorithmic_bytes": sa_bytes}
+    ceil = stream_ceiling("r1w3")
+    if ceil:  # the STFT moves 1 B in : 3 B out; plain streams of that mix peak here
+        sa.update({"stream_ceiling": ceil, "frac_of_stream_ceiling": sa_gbs / ceil,
+                   "stream_ceiling_source": BW_FILE + " (r1w3: one read : three write streams)"})
+    del xs, Xs, Ms
+    return sa
+
+
+def barrier(world):
+    if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
-        pg = dist.group.WORLD
+        dist.barrier()
+    torch.cuda.synchronize()
 
+
+def base_line(args, cfg, world, elapsed, B, T):
+    return {
+        "metric": "mixtures/sec (8 kHz, 4 s, 2-spk WSJ0-shape) at 1/2/4/8 MI355X",
+        "value": B * world * args.steps / elapsed,
+        "unit": "mixtures/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.precision == "fp32" else "bf16",
+        "data": "synthetic speech-shaped sources (harmonic stack + AM + noise), seed 1+1000*rank, HBM-resident",
+        "config": {"workload": cfg["what"].format(mode=args.mode) + f", B={B}/GPU, N={cfg['N']} (T={T},F=129)",
+                   "name": args.config, "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                   "precision": args.precision},
+    }
+
+
+def train_main(args, cfg, dev, world, rank, pg):
     from dl4ss_amd import engine, ops, synth
 
-    B, K, N = args.batch, 2, 32000
-    net = engine.SepNet(cell="lstm", num_layers=4, hidden=300, emb=50, num_labels=101, device=dev, seed=1)
+    B, K, N = args.batch or cfg["B"], cfg["K"], cfg["N"]
+    net = engine.SepNet(cell=cfg["cell"], num_layers=cfg["L"], hidden=300, emb=50, num_labels=101,
+                        adjust=cfg["adjust"], device=dev, seed=1)
     if world > 1:  # identical initial weights on every rank
         from dl4ss_amd import dp
 
@@ -213,55 +462,25 @@ def main():
                      torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
                      torch.from_numpy(spk.astype(np.int32)).to(dev)))
 
-    # per-phase HIP events on the stream the kernels run on (torch's current stream)
-    ev = {"stft": []}
-
-    def timed_step(i, record):
+    def timed_step(i):
         raw, gains, spk = pool[i % len(pool)]
-        if use_graph:
-            return tr.step_graph(raw, gains, spk)
-        if not record:
-            return tr.step(raw, gains, spk)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        tr.spk.copy_(spk)
-        ops.mix_sources(raw, gains, out_src=tr.src, out_mix=tr.mix, stats_ws=tr.stats)
-        e0.record()  # the two STFT launches (mixtures, then sources) of engine.SepTrainer.features
-        ops.stft(tr.mix, complex_out=False, mag_out=True, out_mag=tr.mag_mix)
-        ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
-        e1.record()
-        ev["stft"].append((e0, e1))
-        tr.forward()
-        loss = tr.loss_and_grad()
-        tr.backward()
-        tr.allreduce()
-        tr.optimizer_step()
-        return loss
+        return tr.step_graph(raw, gains, spk) if use_graph else tr.step(raw, gains, spk)
 
     # HIP graph (default): the step's launches from STFT to the end of backward replay as
-    # one graph after an eager warm-up step (GEMM plans, workspaces); mixing, the all-reduce
-    # and Adam stay eager (engine.SepTrainer.capture)
+    # one graph after an eager warm-up step (workspaces); mixing, the all-reduce and Adam stay
+    # eager (engine.SepTrainer.capture)
     use_graph = False
-    timed_step(0, False)
+    timed_step(0)
     use_graph = not args.eager
     for i in range(1, max(args.warmup, 1)):
-        timed_step(i, False)
+        timed_step(i)
     tr.check()
 
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
-    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
     t0 = time.perf_counter()
-    s0.record()
     for i in range(args.steps):
-        loss = timed_step(i, True)
-    s1.record()
-    barrier()
+        loss = timed_step(i)
+    barrier(world)
     elapsed = time.perf_counter() - t0
     tr.check()
     if world > 1:
@@ -272,36 +491,24 @@ def main():
     if not np.isfinite(loss_v):
         raise RuntimeError("non-finite loss")
 
-    if use_graph:  # the in-step STFT launches, timed eagerly on the step's buffers (one untimed pair first)
-        ops.stft(tr.mix, complex_out=False, mag_out=True, out_mag=tr.mag_mix)
-        ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
-        for _ in range(args.steps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            ops.stft(tr.mix, complex_out=False, mag_out=True, out_mag=tr.mag_mix)
-            ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
-            e1.record()
-            ev["stft"].append((e0, e1))
-        torch.cuda.synchronize()
-
-    # ---- roofline of the two north-star kernels (STFT in-step events; input GEMM isolated), same stream
-    T, F = tr.T, tr.F
-    stft_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["stft"]]))
-    stft_bytes = B * (K + 1) * (4 * N + 4 * T * F)  # mag-only STFT of mixture + K sources
-    # input-projection GEMM of BiLSTM layer 2 (M = B*T, N = 2400, K = 600, bias fused), timed in
-    # isolation with the step's own kernel and operands: in bf16 mode gemm_gl.hip on the bf16 h
+    T = tr.T
+    stft_ms = stft_instep_graph(tr, B, K, N)
+    stft_bytes = B * (K + 1) * (4 * N + 4 * T * 129)  # mag-only STFT of mixture + K sources
+    # input-projection GEMM of RNN layer 2 (M = B*T, N = 2 x gates x H, K = 600, bias fused), timed
+    # in isolation with the step's own kernel and operands: in bf16 mode gemm_gl.hip on the bf16 h
     # the layer-1 recurrence wrote and the bf16 W_ih copy (the in-step launch), else gemm.hip fp32
     bih = net.cat_view("bias_ih", 1)
+    ncol = bih.numel()
     if tr.fast:
         xb, wb = tr.outb[0][:, :2 * net.H], tr.wb_ih[1][:, :2 * net.H]
         run_gemm = lambda: tr._gemm_fwd(xb, wb, bih, tr.G)  # noqa: E731
-        gemm_kernel = GEMM_GL_INPROJ if tr.gemm_path == "gl" else "gemm_bb_kernel"
-        gemm_name = f"{gemm_kernel} (bf16 operands, in-step BiLSTM layer-2 input projection 8032x2400x600 + bias)"
+        gemm_kernel = GEMM_GL_INPROJ
+        gemm_name = f"{gemm_kernel} (bf16 operands, in-step layer-2 input projection {B * T}x{ncol}x600 + bias)"
     else:
         x, wih = tr.out[0].view(B * T, -1), net.cat_view("weight_ih", 1)
         run_gemm = lambda: ops.gemm(x, wih, transB=True, bias=bih, out=tr.G, precision=args.precision)  # noqa: E731
         gemm_kernel = "gemm_kernel"
-        gemm_name = "gemm_kernel (fp32 operands, BiLSTM layer-2 input projection 8032x2400x600 + bias)"
+        gemm_name = f"gemm_kernel (fp32 operands, layer-2 input projection {B * T}x{ncol}x600 + bias)"
     for _ in range(3):
         run_gemm()
     g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -311,64 +518,19 @@ def main():
     g1.record()
     torch.cuda.synchronize()
     gemm_ms = g0.elapsed_time(g1) / 20
-    gemm_flops = 2.0 * B * T * 600 * 2400
-    # standalone STFT at the north-star measurement size (>= 2048 signals, ~1 GB of
-    # traffic per launch, complex + magnitude outputs): the >= 50 % HBM target.  4096
-    # signals (2.1 GB per launch) amortise the launch's ramp-up and drain better
-    sa = None
-    if not args.no_stft_standalone:
-        n_sa = 4096
-        xs = torch.randn(n_sa, N, device=dev)
-        Xs = torch.empty(n_sa, T, F, 2, device=dev)
-        Ms = torch.empty(n_sa, T, F, device=dev)
-        for _ in range(3):
-            ops.stft(xs, out_c=Xs, out_mag=Ms)
-        h0, h1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        h0.record()
-        for _ in range(10):
-            ops.stft(xs, out_c=Xs, out_mag=Ms)
-        h1.record()
-        torch.cuda.synchronize()
-        sa_ms = h0.elapsed_time(h1) / 10
-        sa_bytes = n_sa * (4 * N + 12 * T * F)
-        sa_gbs = sa_bytes / (sa_ms * 1e-3) / 1e9
-        sa = {"bound": "hbm", "kernel": f"stft_fwd (one launch: {n_sa} signals x N=32000, complex + magnitude; "
-                                        "the north-star STFT roofline measurement)",
-              "achieved": sa_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sa_gbs / HBM_PEAK_GBS,
-              "traffic": pmc_traffic("stft_fwd_kernel", [stft_grid_threads(n_sa, T)]),
-              "traffic_source": PMC_FILE, "launch_ms": sa_ms, "algorithmic_bytes": sa_bytes}
-        ceil = stream_ceiling("r1w3")
-        if ceil:  # the STFT moves 1 B in : 3 B out; plain streams of that mix peak here
-            sa.update({"stream_ceiling": ceil, "frac_of_stream_ceiling": sa_gbs / ceil,
-                       "stream_ceiling_source": BW_FILE + " (r1w3: one 16-B read : three 16-B write streams)"})
-        del xs, Xs, Ms
+    gemm_tf = 2.0 * B * T * 600 * ncol / (gemm_ms * 1e-3) / 1e12
+    sa = None if args.no_stft_standalone else stft_standalone(dev, N, T)
 
     if rank == 0:
-        value = B * world * args.steps / elapsed
+        out = base_line(args, cfg, world, elapsed, B, T)
+        out["config"].update({"loss": args.mode, "launch": "hip-graph" if use_graph else "eager",
+                              "step": "mix+STFT+fwd+loss+bwd+allreduce+Adam"})
         stft_gbs = stft_bytes / (stft_ms * 1e-3) / 1e9
-        gemm_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12
-        out = {
-            "metric": "mixtures/sec (8 kHz, 4 s, 2-spk WSJ0-shape) at 1/2/4/8 MI355X",
-            "value": value,
-            "unit": "mixtures/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32" if args.precision == "fp32" else "bf16",
-            "data": "synthetic speech-shaped sources (harmonic stack + AM + noise), seed 1+1000*rank, HBM-resident",
-            "config": {"workload": f"C2: 2-spk {args.mode} BiLSTM-4L magnitude mask, B=32/GPU, N=32000 (T=251,F=129),"
-                                   " full step: mix+STFT+fwd+loss+bwd+allreduce+Adam",
-                       "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
-                       "precision": args.precision, "loss": args.mode,
-                       "launch": "hip-graph" if use_graph else "eager"},
+        out.update({
             "loss": loss_v,
             "roofline": sa,
-            "roofline_instep": {"bound": "hbm", "kernel": "stft_fwd in-step (2 launches/step: 32 mixtures + 64 "
-                                                         "sources, magnitude)",
+            "roofline_instep": {"bound": "hbm", "kernel": f"stft_fwd in-step (2 launches/step: {B} mixtures + "
+                                                         f"{B * K} sources, magnitude; timed as a replayed graph)",
                                 "achieved": stft_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": stft_gbs / HBM_PEAK_GBS,
                                 "traffic": pmc_traffic("stft_fwd_kernel", stft_grids(B, K, T)),
@@ -376,12 +538,112 @@ def main():
             "roofline_mfma": {"bound": "mfma", "kernel": gemm_name,
                               "achieved": gemm_tf, "peak": MFMA_PEAK[args.precision], "unit": "TFLOP/s",
                               "frac": gemm_tf / MFMA_PEAK[args.precision], "launch_ms": gemm_ms,
-                              "mfma_busy": pmc_mfma_busy(gemm_kernel), "mfma_busy_source": MFMA_FILE},
-        }
+                              "mfma_busy": pmc_mfma_busy(gemm_kernel) if args.config == "C2" else None,
+                              "mfma_busy_source": MFMA_FILE},
+        })
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, N, K)
-            out["cpu_baseline_with_classifier"] = cpu_baseline(args, N, K, with_classifier=True)
+            out["cpu_baseline"] = cpu_baseline(args, cfg)
+            if args.config == "C2":
+                out["cpu_baseline_with_classifier"] = cpu_baseline(args, cfg, with_classifier=True)
         print(json.dumps(out), flush=True)
+
+
+def recursive_main(args, cfg, dev, world, rank, pg):
+    """C5: each rank is an independent replica running the recursive extraction on its own
+    synthetic mixtures (B per step, default 1); after the timed region one all-gather brings
+    every rank's extracted speaker ids to all ranks (the final metric gather)."""
+    from dl4ss_amd import _lib, engine, infer, ops, synth
+
+    B, N = args.batch or cfg["B"], cfg["N"]
+    T = ops.n_frames(N)
+    net = engine.SepNet(cell="gru", num_layers=2, adjust=False, device=dev, seed=1)
+    cnet = infer.ClassifierNet(129, 600, 3, 101, device=dev, seed=2)
+    ex = infer.RecursiveExtractor(net, cnet, B, T, precision=args.precision)
+    gen = synth.SyntheticMixtures(n_samples=N, k=2, seed=5, rank=rank)
+    pool = []
+    for _ in range(4):
+        src, spk, u = gen.batch(B)
+        pool.append((torch.from_numpy(src.astype(np.float32)).to(dev),
+                     torch.from_numpy(synth.gains_for(u, 2).astype(np.float32)).to(dev)))
+    y = torch.empty(B * 2, 128 * (T - 1), device=dev)
+    src_b = torch.empty(B, 2, N, device=dev)
+    mix_b = torch.empty(B, N, device=dev)
+    stats = torch.empty(32 * B * 2, device=dev)
+    Xc = torch.empty(B, T, 129, 2, device=dev)
+    Xm = torch.empty(B, T, 129, device=dev)
+    pred = torch.empty(B, 2, T, 129, device=dev)
+    spk_all = []
+
+    def extract(i):
+        raw, gains = pool[i % len(pool)]
+        ops.mix_sources(raw, gains, out_src=src_b, out_mix=mix_b, stats_ws=stats)
+        ops.stft(mix_b, out_c=Xc, out_mag=Xm)
+        out = ex.run(Xm)
+        _lib.call("dl4ss_mask_split", _lib.ptr(out["masks"]), _lib.ptr(Xm.unsqueeze(1).expand(B, 2, T, 129)
+                                                                         .contiguous()), pred.numel(),
+                  _lib.ptr(pred), None, _lib.stream_ptr())
+        _lib.call("dl4ss_istft_apply", _lib.ptr(Xc), _lib.ptr(pred), B * 2, 2, T, 0, 0, _lib.ptr(y),
+                  _lib.stream_ptr())
+        return out
+
+    for i in range(max(args.warmup, 1)):
+        extract(i)
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = extract(i)
+        spk_all.append(out["spk"].clone())
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    mine = torch.cat(spk_all)  # (steps * B, S) int32 on the device
+    if world > 1:
+        import torch.distributed as dist
+
+        from dl4ss_amd import dp
+
+        elapsed = dp.max_over_ranks(elapsed, dev, pg)
+        gathered = torch.empty(world * mine.shape[0], mine.shape[1], dtype=mine.dtype, device=dev)
+        dist.all_gather_into_tensor(gathered, mine, group=pg)
+    else:
+        gathered = mine
+    sa = None if args.no_stft_standalone else stft_standalone(dev, N, T)
+    if rank == 0:
+        g = gathered.cpu()
+        line = base_line(args, cfg, world, elapsed, B, T)
+        line["scaling"] = "weak"
+        line["config"].update({"replicas": world, "collective": "all_gather of speaker ids after the timed region",
+                               "step": "mix+STFT+classifier+2 extraction steps+final masks+iSTFT"})
+        line.update({"roofline": sa, "roofline_mfma": None,
+                     "gathered_extractions": int(g.shape[0]),
+                     "gathered_speakers_found": int((g >= 0).sum()),
+                     "speakers_row0": g[0].tolist()})
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline_recursive(args, cfg)
+        print(json.dumps(line), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # start the ranks before anything touches the GPU; never re-exec this process
+        sys.exit(launch_ranks(args.gpus, argv))
+    world, rank, local = world_from_env(args.gpus)
+    if args.standin:
+        return standin_main(args, world, rank)
+    cfg = CONFIGS[args.config]
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1 or args.dist:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+    if cfg["kind"] == "train":
+        train_main(args, cfg, dev, world, rank, pg)
+    else:
+        recursive_main(args, cfg, dev, world, rank, pg)
     if pg is not None:
         import torch.distributed as dist
 

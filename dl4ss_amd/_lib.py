@@ -68,6 +68,8 @@ SIGNATURES = {
     "dl4ss_gemm_bf16_lt": [I, I, I, I, I, P, LL, P, LL, P, LL, F, I, LL, LL, LL, P, LL, P],
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
     "dl4ss_adam_guarded": [P, P, P, P, LL, F, F, F, F, I, P, P, P],
+    "dl4ss_adam_guarded_dp": [P, P, P, P, LL, F, F, F, F, I, P, P, P, P],
+    "dl4ss_status_flag": [P, P, P],
     "dl4ss_birnn_plan_info": [I, I, I, I, I, P],
     "dl4ss_debug_set_spin_limit": [ctypes.c_uint],
     "dl4ss_debug_set_place_force": [ctypes.c_int],

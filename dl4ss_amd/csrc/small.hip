@@ -203,9 +203,15 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ A
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2s,
-                                                   const int* __restrict__ status, float* __restrict__ loss) {
-  if (status && *status) {  // a recurrence hand-off of this step timed out: refuse the update
-    if (loss && blockIdx.x == 0 && threadIdx.x == 0) loss[0] = __builtin_nanf("");
+                                                   int* __restrict__ status, const float* __restrict__ dp_flag,
+                                                   float* __restrict__ loss) {
+  // refuse the update when a recurrence hand-off of this step timed out on this rank
+  // (status[0]) or on any data-parallel peer (dp_flag: the all-reduced status flag)
+  if ((status && status[0]) || (dp_flag && dp_flag[0] != 0.f)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (loss) loss[0] = __builtin_nanf("");
+      if (status) status[1] += 1;  // refused-update count: the host rolls its step count back by it
+    }
     return;
   }
   const float step = lr / bc1;
@@ -293,16 +299,23 @@ DL4SS_API int dl4ss_colsum(const float* A, long long lda, int M, int N, float* o
   return 0;
 }
 
-DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-                                 float beta2, float eps, int step, const int* status, float* loss, void* stream);
+DL4SS_API int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                                    float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
+                                    void* stream);
 
 DL4SS_API int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                          float beta2, float eps, int step, void* stream) {
-  return dl4ss_adam_guarded(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, nullptr, stream);
+  return dl4ss_adam_guarded_dp(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, nullptr, nullptr, stream);
 }
 
 DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-                                 float beta2, float eps, int step, const int* status, float* loss, void* stream) {
+                                 float beta2, float eps, int step, int* status, float* loss, void* stream) {
+  return dl4ss_adam_guarded_dp(p, g, m, v, n, lr, beta1, beta2, eps, step, status, nullptr, loss, stream);
+}
+
+DL4SS_API int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                                    float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
+                                    void* stream) {
   DL4SS_REQUIRE(p && g && m && v && n >= 0 && step >= 1);
   if (n == 0) return 0;
   // bias corrections in double on the host, as torch computes them in Python floats
@@ -310,7 +323,18 @@ DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, l
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   const unsigned grid = (unsigned)min(8192LL, (n / 4 + 255) / 256 + 1);
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr, beta1, beta2, eps,
-                     bc1, bc2s, status, loss);
+                     bc1, bc2s, status, dp_flag, loss);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void status_flag_kernel(const int* __restrict__ status, float* __restrict__ flag) {
+  if (threadIdx.x == 0) flag[0] = status[0] ? 1.f : 0.f;
+}
+
+DL4SS_API int dl4ss_status_flag(const int* status, float* flag, void* stream) {
+  DL4SS_REQUIRE(status && flag);
+  hipLaunchKernelGGL(status_flag_kernel, dim3(1), dim3(64), 0, as_stream(stream), status, flag);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }

@@ -61,7 +61,12 @@ class SepNet:
         self.numel = off
         self.device = torch.device(device)
         self.flat = torch.zeros(off, device=self.device, dtype=torch.float32)
-        self.grad = torch.zeros_like(self.flat)
+        # the flat gradient plus one 16-B slot behind it: slot 0 carries each rank's hand-off
+        # status flag through the gradient all-reduce (SepTrainer.allreduce), so every rank's
+        # guarded Adam refuses the same steps
+        self.grad_ext = torch.zeros(off + 4, device=self.device, dtype=torch.float32)
+        self.grad = self.grad_ext[:off]
+        self.dp_flag = self.grad_ext[off:off + 1]
         self.reset_parameters(seed)
 
     def view(self, name, buf=None):
@@ -165,7 +170,9 @@ class SepTrainer:
         w8 = (ws + 255) // 256 * 32
         self.rnn_ws_all = torch.empty(2, net.L * w8, device=dev, dtype=torch.int64)  # [fwd | bwd][layer]
         self._ws_slot = lambda l, bwd: self.rnn_ws_all[int(bwd), l * w8:(l + 1) * w8]
-        self.status = torch.zeros(1, device=dev, dtype=torch.int32)
+        # {hand-off timed out, refused-update count} (the recurrence kernels set [0]; the guarded
+        # Adam counts its refusals in [1])
+        self.status = torch.zeros(2, device=dev, dtype=torch.int32)
         self.m = torch.zeros_like(net.flat)
         self.v = torch.zeros_like(net.flat)
         self.step_count = 0
@@ -490,6 +497,7 @@ class SepTrainer:
                   _lib.ptr(self.dh_bcast) if net.adjust else None, st)
         if self.fast:
             self._backward_fast()
+            self._status_flag()
             return
         dPre = self.V
         hL = self.out[-1].view(BT, 2 * H)
@@ -522,21 +530,36 @@ class SepTrainer:
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
                 ops.gemm(dG, net.cat_view("weight_ih", l), out=dH_next, splitk="auto", precision=self.precision)
                 dH = dH_next
+        self._status_flag()
+
+    def _status_flag(self):
+        """Data parallel: this rank's hand-off status as the float behind the flat gradient
+        (rewritten every step), combined by the all-reduce (allreduce()).  Without a process
+        group the slot stays zero."""
+        if self.pg is not None:
+            _lib.call("dl4ss_status_flag", _lib.ptr(self.status), _lib.ptr(self.net.dp_flag), _lib.stream_ptr())
 
     def allreduce(self):
-        """One RCCL all-reduce of the flat gradient buffer (mean over ranks)."""
+        """One RCCL all-reduce of the flat gradient buffer (mean over ranks).  The slot behind
+        the gradient carries this rank's hand-off status flag (dl4ss_status_flag, written at the
+        end of backward()): after the mean it is non-zero on every rank iff a hand-off timed out
+        on any rank, and the guarded Adam reads it (a timed-out rank's incomplete
+        gradient must not reach the healthy ranks' weights either)."""
         if self.pg is None:
             return
         from . import dp
 
-        dp.allreduce_mean_(self.net.grad, self.pg)
+        dp.allreduce_mean_(self.net.grad_ext, self.pg)
 
     def optimizer_step(self):
         """Adam on device; refused (parameters untouched, loss[0] = NaN) when a recurrence
-        hand-off of this step timed out -- a timed-out step never reaches the weights."""
+        hand-off of this step timed out on this rank or (data parallel) on any rank -- a
+        timed-out step never reaches the weights.  A refused step is counted on device
+        (status[1]); check() takes the refused steps back out of step_count, so the bias
+        corrections follow the updates actually applied, as torch.optim.Adam's do."""
         self.step_count += 1
         ops.adam_(self.net.flat, self.net.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps,
-                  status=self.status, loss=self.loss)
+                  status=self.status, loss=self.loss, dp_flag=self.net.dp_flag)
 
     def step(self, raw, gains, spk_idx):
         """One full training step on device-resident inputs; returns the loss tensor (not synced)."""
@@ -596,11 +619,14 @@ class SepTrainer:
         return self._graph_loss
 
     def check(self):
-        """Raise if a recurrence hand-off timed out since the last check (the status word is
-        reset, so the trainer can continue after the caller has handled it; the guarded Adam
-        already refused every update computed from the timed-out step)."""
+        """Raise if a recurrence hand-off timed out, here or (data parallel) on a peer rank, since
+        the last check: the guarded Adam already refused every update computed from then on.
+        The refused steps are taken back out of step_count and the status word is reset, so the
+        trainer can continue after the caller has handled it."""
         torch.cuda.synchronize()
-        s = int(self.status.item())
-        if s:
+        s, refused = (int(x) for x in self.status.tolist())
+        if s or refused:
             self.status.zero_()
-            raise RuntimeError(f"BiRNN hand-off timed out (status {s}): the step's update was refused")
+            self.step_count -= refused
+            where = "on this rank" if s else "on a data-parallel peer"
+            raise RuntimeError(f"BiRNN hand-off timed out {where} (status {s}): {refused} update(s) refused")

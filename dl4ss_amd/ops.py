@@ -310,15 +310,19 @@ def colsum(A, out):
     return out
 
 
-def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, loss=None):
-    """torch Adam step on flat buffers; with ``status`` (the recurrence hand-off status word)
-    the update is refused on device when a hand-off of this step timed out, and loss[0] is
-    set to NaN (dl4ss_adam_guarded)."""
+def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, loss=None, dp_flag=None):
+    """torch Adam step on flat buffers; with ``status`` (the recurrence hand-off status word,
+    2 ints: {timed out, refused-update count}) the update is refused on device when a hand-off
+    of this step timed out, loss[0] is set to NaN and status[1] counts the refusal
+    (dl4ss_adam_guarded); with ``dp_flag`` (the all-reduced status flag behind the flat
+    gradient) also when a data-parallel peer's hand-off timed out (dl4ss_adam_guarded_dp)."""
     for t in (p, g, m, v):
         _f32c(t, "adam")
-    _lib.call("dl4ss_adam_guarded", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(), float(lr),
-              float(betas[0]), float(betas[1]), float(eps), int(step), _lib.ptr(status), _lib.ptr(loss),
-              _lib.stream_ptr())
+    if status is not None and status.numel() < 2:
+        raise ValueError("adam_: the status word needs 2 ints (timed out, refused-update count)")
+    _lib.call("dl4ss_adam_guarded_dp", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(), float(lr),
+              float(betas[0]), float(betas[1]), float(eps), int(step), _lib.ptr(status), _lib.ptr(dp_flag),
+              _lib.ptr(loss), _lib.stream_ptr())
 
 
 def birnn_plan(cell, B, H, precision="bf16", max_wg=0):

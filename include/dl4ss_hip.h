@@ -256,11 +256,20 @@ int dl4ss_colsum(const float* A, long long lda, int M, int N, float* out, void* 
 /* torch.optim.Adam step on flat fp32 buffers (EvalVer.py:538-544). */
 int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
                float eps, int step, void* stream);
-/* dl4ss_adam that refuses a step computed from a timed-out recurrence: when *status != 0
- * (a BiRNN hand-off of this step timed out) no parameter or moment changes and loss[0]
- * (if not NULL) is set to NaN, so the step's loss read by the caller reports it. */
+/* dl4ss_adam that refuses a step computed from a timed-out recurrence: when status[0] != 0
+ * (a BiRNN hand-off of this step timed out) no parameter or moment changes, loss[0] (if not
+ * NULL) is set to NaN, so the step's loss read by the caller reports it, and status[1] (the
+ * refused-update count; status points at 2 ints) is incremented. */
 int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-                       float beta2, float eps, int step, const int* status, float* loss, void* stream);
+                       float beta2, float eps, int step, int* status, float* loss, void* stream);
+/* dl4ss_adam_guarded that also refuses when *dp_flag != 0: the data-parallel form, where
+ * dp_flag is the slot behind the flat gradient that dl4ss_status_flag filled from each rank's
+ * status and the gradient all-reduce combined, so every rank refuses the same steps. */
+int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                          float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
+                          void* stream);
+/* flag[0] = status[0] != 0 ? 1 : 0 (one float, written behind the flat gradient before its all-reduce). */
+int dl4ss_status_flag(const int* status, float* flag, void* stream);
 
 /* ---- kernels behind the reference-API nn.Modules (dl4ss_amd/compat/myNet.py) ---- */
 /* dpre = dv * (1 - v^2): backward of MIX_SPEECH's tanh(Linear) (EvalVer.py:298-299). */

@@ -43,13 +43,9 @@ def test_c3_full_size_step(dev):
     _compare_step(dev, "gru", 2, 16, 2, 32000, "crm", tol_grad=5e-3)
 
 
-def test_c3_first_non_finite_step_matches_oracle(dev):
-    """The cRM inverse compression -1/C log((K - M)/(K + M)) is infinite once a compressed
-    mask reaches K (fp32 tanh(e) rounds to 1 for |e| >= 9.02).  Training the C3
-    configuration on one repeated batch, the HIP step and the oracle step must first produce a
-    non-finite loss at the same step (or both stay finite), and agree until then."""
-    B, K, N, S = 16, 2, 32000, 40
-    net, tr, src, spk, gains, ref = _setup(dev, "gru", 2, B, K, N, "crm", seed=3)
+def _c3_run(dev, seed, S, stop_at_non_finite=True):
+    B, K, N = 16, 2, 32000
+    net, tr, src, spk, gains, ref = _setup(dev, "gru", 2, B, K, N, "crm", seed=seed)
     feats, X, Y = _oracle_features(src, gains, True)
     idx = torch.from_numpy(spk)
     opt = om.make_adam(ref)
@@ -69,7 +65,27 @@ def test_c3_first_non_finite_step_matches_oracle(dev):
         if first_ours is not None or first_ref is not None:
             break
         assert abs(lo - lr) <= 1e-3 * abs(lr), (s, lo, lr)
+    return first_ours, first_ref
+
+
+def test_c3_first_non_finite_step_matches_oracle(dev):
+    """The cRM inverse compression -1/C log((K - M)/(K + M)) is infinite once a compressed
+    mask reaches K (fp32 tanh(e) rounds to 1 for |e| >= 9.02).  With the
+    reference's own seed (1, main_run.py:21-23) and default init (N(0,1) query embedding) the
+    C3 configuration hits it at once: the HIP step and the oracle step must both report a
+    non-finite loss, at the same step.  The hazard must actually occur (a run where neither side
+    goes non-finite fails instead of passing vacuously: seeds 2-4, 6 and 8 stay finite for 25
+    steps, 1, 5 and 7 are non-finite from the first step, measured on the oracle)."""
+    first_ours, first_ref = _c3_run(dev, 1, 10)
+    assert first_ref is not None, "the cRM_EvalVer.py:688 hazard did not occur"
     assert first_ours == first_ref, (first_ours, first_ref)
+
+
+def test_c3_finite_window_matches_oracle(dev):
+    """The same repeated-batch C3 training on a seed whose logits stay below the saturation:
+    the HIP and oracle losses agree within 1e-3 at every one of 20 steps, none non-finite."""
+    first_ours, first_ref = _c3_run(dev, 3, 20)
+    assert first_ours is None and first_ref is None, (first_ours, first_ref)
 
 
 def test_c5_full_length_recursive(dev):

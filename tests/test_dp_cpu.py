@@ -113,3 +113,31 @@ def test_dp_two_ranks_equals_global_batch():
         assert tmax == 2.0
     # the two ranks' synthetic shards are different utterances
     assert not torch.equal(shards[0][0], shards[1][0])
+
+
+def _flag_worker(rank, world, port, out):
+    """The hand-off status flag rides behind the flat gradient through the mean all-reduce
+    (engine.SepNet.grad_ext / SepTrainer.allreduce): one rank's timeout reaches every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = []
+    for bad in (None, 1, 0):  # no rank timed out / rank 1 / rank 0
+        grad_ext = torch.zeros(8 + 4)
+        grad_ext[:8] = float(rank + 1)
+        grad_ext[8] = 1.0 if rank == bad else 0.0  # dl4ss_status_flag
+        dp.allreduce_mean_(grad_ext)
+        res.append((float(grad_ext[0]), float(grad_ext[8])))
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_dp_status_flag_reaches_every_rank():
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_flag_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        (g0, f0), (g1, f1), (g2, f2) = out[r]
+        assert g0 == g1 == g2 == 2.0  # the gradient mean is unaffected by the flag slot
+        assert f0 == 0.0  # clean step: every rank's guarded Adam applies it
+        assert f1 > 0.0 and f2 > 0.0  # a timeout on any one rank: every rank refuses the step

@@ -36,16 +36,62 @@ def test_timed_out_step_never_updates_the_weights(dev, precision):
         torch.cuda.synchronize()
     finally:
         lib.dl4ss_debug_set_spin_limit(0)
-    assert int(tr.status.item()) != 0
+    assert int(tr.status[0].item()) != 0 and int(tr.status[1].item()) == 1
     assert torch.isnan(loss[0]).item()
     assert torch.equal(net.flat, before[0]) and torch.equal(tr.m, before[1]) and torch.equal(tr.v, before[2])
+    n_before = tr.step_count
     with pytest.raises(RuntimeError, match="timed out"):
         tr.check()
-    assert int(tr.status.item()) == 0  # reset after reporting
+    assert tr.status.tolist() == [0, 0]  # reset after reporting
+    assert tr.step_count == n_before - 1  # the refused update is not counted (torch Adam's step)
     loss = tr.step(*batch)
     tr.check()
     assert np.isfinite(float(loss[0].item()))
     assert not torch.equal(net.flat, before[0])
+
+
+def test_peer_timeout_flag_refuses_the_update(dev):
+    """Data parallel: a peer rank's timed-out hand-off reaches this rank as a non-zero
+    flag behind the flat gradient after the all-reduce (dl4ss_status_flag -> mean).  This
+    rank's own status is clean, yet its guarded Adam must refuse the same step (so the replicas
+    never drift apart), count the refusal, and check() must raise and roll the step back."""
+    B, K, N = 2, 2, 2000
+    net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=5)
+    tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+    batch = _batch(dev, B, K, N, 5)
+    tr.step(*batch)
+    tr.check()
+    before = (net.flat.clone(), tr.m.clone(), tr.v.clone())
+    n0 = tr.step_count
+    tr.spk.copy_(batch[2])
+    tr.features(batch[0], batch[1])
+    tr.forward()
+    loss = tr.loss_and_grad()
+    tr.backward()
+    # what the all-reduce mean leaves behind when one of two ranks set its flag
+    net.dp_flag.fill_(0.5)
+    tr.optimizer_step()
+    torch.cuda.synchronize()
+    assert int(tr.status[0].item()) == 0 and int(tr.status[1].item()) == 1
+    assert torch.isnan(loss[0]).item()
+    assert torch.equal(net.flat, before[0]) and torch.equal(tr.m, before[1]) and torch.equal(tr.v, before[2])
+    with pytest.raises(RuntimeError, match="peer"):
+        tr.check()
+    assert tr.step_count == n0
+    net.dp_flag.zero_()
+    loss = tr.step(*batch)
+    tr.check()
+    assert np.isfinite(float(loss[0].item())) and tr.step_count == n0 + 1
+
+
+def test_status_flag_kernel(dev):
+    st = torch.tensor([0, 0], dtype=torch.int32, device=dev)
+    fl = torch.full((1,), 7.0, device=dev)
+    _lib.call("dl4ss_status_flag", _lib.ptr(st), _lib.ptr(fl), _lib.stream_ptr())
+    assert float(fl.item()) == 0.0
+    st[0] = 3
+    _lib.call("dl4ss_status_flag", _lib.ptr(st), _lib.ptr(fl), _lib.stream_ptr())
+    assert float(fl.item()) == 1.0
 
 
 def test_device_plan_within_residency_budget(dev):
