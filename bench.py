@@ -638,7 +638,11 @@ def main(argv=None):
     if world > 1 or args.dist:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if "RANK" in os.environ:
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # --dist at world size 1 without a launcher: a private single-rank rendezvous
+            dist.init_process_group("nccl", device_id=dev, init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                                    world_size=1)
         pg = dist.group.WORLD
     if cfg["kind"] == "train":
         train_main(args, cfg, dev, world, rank, pg)

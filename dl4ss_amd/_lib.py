@@ -24,8 +24,6 @@ SIGNATURES = {
     "dl4ss_istft": [P, LL, I, I, I, I, P, P],
     "dl4ss_mix_sources": [P, P, I, I, I, P, P, P, P],
     "dl4ss_gemm": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, P],
-    "dl4ss_gemm_bf16": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, P],
-    "dl4ss_gemm_bf16_batched": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P],
     "dl4ss_f32_to_bf16": [P, P, LL, P],
     "dl4ss_f32_to_bf16_2d": [P, LL, I, I, P, LL, P],
     "dl4ss_colsum_bf16": [P, LL, I, I, P, P],
@@ -62,10 +60,8 @@ SIGNATURES = {
     "dl4ss_time_mean": [P, I, I, I, P, P],
     "dl4ss_bss_corr": [P, I, I, I, I, P, P],
     "dl4ss_mix_sources_ex": [P, P, P, I, I, I, P, P, P, P],
-    "dl4ss_gemm_bf16_set_tile": [I],
     "dl4ss_f32_to_bf16_2d_multi": [I, P, P, P, P, P, P, P],
     "dl4ss_mask_attn_loss_bf16v": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
-    "dl4ss_gemm_bf16_lt": [I, I, I, I, I, P, LL, P, LL, P, LL, F, I, LL, LL, LL, P, LL, P],
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
     "dl4ss_adam_guarded": [P, P, P, P, LL, F, F, F, F, I, P, P, P],
     "dl4ss_adam_guarded_dp": [P, P, P, P, LL, F, F, F, F, I, P, P, P, P],

@@ -22,8 +22,8 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-at
 # per-file extras: the STFT's radix-4x4 butterflies run 1.2-1.5x faster as scalar fp32
 # than SLP-packed into v_pk_add_f32 (the packing needs a v_mov per pair of operands)
 FILE_FLAGS = {"stft.hip": ["-fno-slp-vectorize"]}
-# hipBLASLt for the plain (epilogue-free) backward GEMMs (gemm_lt.hip)
-LINK = ["-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+# no vendor BLAS: every GEMM is a hand-written kernel (gemm.hip, gemm_gl.hip)
+LINK = []
 
 
 def _newer(src, dst, deps):

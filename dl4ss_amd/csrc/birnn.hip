@@ -52,6 +52,7 @@ constexpr int HMAX = 320;    // largest hidden size of the training kernels (siz
 constexpr int HMAX_L = 640;  // largest hidden size of the forward-only (inference) instantiations: the
                              // H = 600 speaker classifier of EvalVer.py:305-326 / GRID.py:178-199
 constexpr int DL4SS_RNN_WS_ZEROED = 0x100;  // precision flag: workspace already zero (no memset)
+constexpr int DL4SS_RNN_DGH_PAD8 = 0x200;  // precision flag (bwd): dGh_bf16 direction stride padded to 8
 constexpr unsigned SPIN_LIMIT = 1u << 20;  // ~1 s of polling: a stuck hand-off exits, never hangs
 
 typedef unsigned long long u64;
@@ -176,6 +177,8 @@ struct RnnArgs {
   unsigned short* hprevb;  // fwd (B,T,2H) bf16(h_{t-1})    -- dW_hh GEMM operand
   unsigned short* dGb;     // bwd (B,T,2,NGATE*H) bf16(dG)  -- dW_ih / dX GEMM operand
   unsigned short* dGhb;    // bwd GRU: bf16(dGh)            -- dW_hh GEMM operand
+  int ghb;                 // bwd GRU: dGhb's per-direction column stride (NGATE*H, or padded to a
+                           //      multiple of 8 by DL4SS_RNN_DGH_PAD8: 16-B aligned GEMM operand rows)
   float* dbi;              // bwd: += sum_{b,t} dG   (bias_ih gradient, (2, NGATE*H))
   float* dbh;              // bwd: += sum_{b,t} dGh  (bias_hh gradient)
   float* dbpart;           // bwd: per-row bias sums [b][d][ih | hh][NGATE*H] (fixed-order reduce), or
@@ -1709,8 +1712,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         for (int q = 0; q < NGATE; ++q) a.dGh[go + q * H] = pgh[q];
       }
       if (a.dGhb) {
+        const long long goh = (long long)((bg * T + pt) * 2 + d) * a.ghb + cj;
 #pragma unroll
-        for (int q = 0; q < NGATE; ++q) a.dGhb[go + q * H] = bf16_rne(pgh[q]);
+        for (int q = 0; q < NGATE; ++q) a.dGhb[goh + q * H] = bf16_rne(pgh[q]);
       }
     }
   };
@@ -2307,7 +2311,8 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
                                  void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
   const bool prezeroed = precision & DL4SS_RNN_WS_ZEROED;
-  precision &= ~DL4SS_RNN_WS_ZEROED;
+  const bool dgh_pad8 = precision & DL4SS_RNN_DGH_PAD8;
+  precision &= ~(DL4SS_RNN_WS_ZEROED | DL4SS_RNN_DGH_PAD8);
   DL4SS_REQUIRE(precision == 0 || precision == 1);
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && workspace && status);
   DL4SS_REQUIRE(dG || dG_bf16);
@@ -2333,6 +2338,8 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   a.Whh = W_hh; a.act = const_cast<float*>(act); a.cs = const_cast<float*>(cs);
   a.hprev = const_cast<float*>(hprev); a.dOut = dOut; a.dOutB = dOut_bcast; a.dG = dG; a.dGh = dGh;
   a.dGb = reinterpret_cast<unsigned short*>(dG_bf16); a.dGhb = reinterpret_cast<unsigned short*>(dGh_bf16);
+  const int GHc = (cell == CELL_LSTM ? 4 : 3) * H;
+  a.ghb = dgh_pad8 ? (GHc + 7) / 8 * 8 : GHc;
   a.dbi = db_ih; a.dbh = db_hh;
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
   const bool bias = pk && (db_ih || db_hh);

@@ -1,0 +1,227 @@
+// fp32 -> bf16 operand copies and bf16 column sums of the bf16 training step.
+//
+// The bf16 step's GEMM operands are produced as bf16 in HBM (gemm_gl.hip reads them by LDS-DMA):
+// the BiRNN kernels and the attention GRAD pass write theirs directly; the weights (W_ih of every
+// layer and the Linear, one launch: dl4ss_f32_to_bf16_2d_multi) and the layer-0 features
+// (dl4ss_f32_to_bf16_2d) are converted here once per step, rows zero-padded to a multiple of 8
+// elements (16-B rows).  Rounding: nearest even, as every MFMA operand of the step.
+// The Linear bias gradient is the column sum of bf16 dPre (dl4ss_colsum_bf16_det: per-256-row-block
+// partials + a fixed-order reduce, bitwise reproducible; EvalVer.py:298 Linear.bias).
+#include "common.h"
+#include <hip/hip_bf16.h>
+
+namespace {
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, unsigned short* __restrict__ y, long long n) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    const float4 v = *reinterpret_cast<const float4*>(x + i);
+    __hip_bfloat162 lo2 = __float22bfloat162_rn(make_float2(v.x, v.y));
+    __hip_bfloat162 hi2 = __float22bfloat162_rn(make_float2(v.z, v.w));
+    const unsigned lo = *reinterpret_cast<unsigned*>(&lo2), hi = *reinterpret_cast<unsigned*>(&hi2);
+    *reinterpret_cast<uint2*>(y + i) = make_uint2(lo, hi);
+  } else {
+    for (long long j = i; j < n; ++j) {
+      const unsigned u = __float_as_uint(x[j]);
+      y[j] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    }
+  }
+}
+
+__global__ void f32_to_bf16_2d_kernel(const float* __restrict__ x, long long ldx, int rows, int cols,
+                                      unsigned short* __restrict__ y, long long ldy) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)rows * ldy) return;
+  const long long r = i / ldy, c = i - r * ldy;
+  unsigned short o = 0;
+  if (c < cols) {
+    const unsigned u = __float_as_uint(x[r * ldx + c]);
+    o = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  }
+  y[i] = o;
+}
+
+// Several row-padded fp32 -> bf16 conversions in one launch (the step's bf16 weight copies):
+// segment i converts rows x cols of x[i] (row stride ldx) into y[i] (row stride ldy, zero
+// padding beyond cols).
+constexpr int CVT_MAX = 8;
+struct CvtSegs {
+  const float* x[CVT_MAX];
+  unsigned short* y[CVT_MAX];
+  long long ldx[CVT_MAX], ldy[CVT_MAX];
+  int row0[CVT_MAX + 1];  // row prefix over the segments
+  int cols[CVT_MAX];
+  int n;
+};
+// one workgroup per row (rows of every segment in sequence); each thread converts pairs of
+// columns and stores them as one 4-B word (ldy even)
+__global__ __launch_bounds__(256) void f32_to_bf16_multi_kernel(CvtSegs sg) {
+  const int row = blockIdx.x;
+  int g = 0;
+#pragma unroll
+  for (int j = 1; j < CVT_MAX; ++j) g += (j < sg.n && row >= sg.row0[j]) ? 1 : 0;
+  const long long r = row - sg.row0[g];
+  const float* xr = sg.x[g] + r * sg.ldx[g];
+  unsigned* yr = reinterpret_cast<unsigned*>(sg.y[g] + r * sg.ldy[g]);
+  const int cols = sg.cols[g];
+  const int np = (int)(sg.ldy[g] >> 1);
+  for (int p = threadIdx.x; p < np; p += 256) {
+    const int c = 2 * p;
+    unsigned lo = 0, hi = 0;
+    if (c < cols) {
+      const unsigned u = __float_as_uint(xr[c]);
+      lo = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    }
+    if (c + 1 < cols) {
+      const unsigned u = __float_as_uint(xr[c + 1]);
+      hi = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    }
+    yr[p] = lo | (hi << 16);
+  }
+}
+
+// out[n] += sum_m A[m*lda + n] for bf16 A (bias gradients from bf16 dPre); VEC: 8 columns per
+// lane with 16-B loads (lda % 8 == 0, aligned base), a 64-lane row segment covers 512 columns.
+// part == nullptr: float atomics into out (order-dependent); else every row block stores its
+// sums to part[blockIdx.y][N] and colsum_reduce_kernel adds the blocks in fixed order.
+template <bool VEC>
+__global__ __launch_bounds__(256) void colsum_bf16_v_kernel(const unsigned short* __restrict__ A, long long lda, int M,
+                                                            int N, int rows_per_block, float* __restrict__ out,
+                                                            float* __restrict__ part) {
+  constexpr int CPL = VEC ? 8 : 1;
+  __shared__ float s[4][64 * CPL];
+  const int c0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * CPL;
+  const int rl = threadIdx.x >> 6;
+  const int m0 = blockIdx.y * rows_per_block;
+  const int m1 = min(M, m0 + rows_per_block);
+  float acc[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) acc[j] = 0.f;
+  if (c0 < N) {
+    if constexpr (VEC) {
+      for (int m = m0 + rl; m < m1; m += 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(A + (long long)m * lda + c0);
+        const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[2 * j] += __uint_as_float(w[j] << 16);
+          acc[2 * j + 1] += __uint_as_float(w[j] & 0xFFFF0000u);
+        }
+      }
+    } else {
+      for (int m = m0 + rl; m < m1; m += 4) acc[0] += __uint_as_float((unsigned)A[(long long)m * lda + c0] << 16);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) s[rl][(threadIdx.x & 63) * CPL + j] = acc[j];
+  __syncthreads();
+  if (rl == 0)
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int l = (threadIdx.x & 63) * CPL + j;
+      if (c0 + j >= N) continue;
+      const float v = (s[0][l] + s[1][l]) + (s[2][l] + s[3][l]);
+      if (part)
+        part[(long long)blockIdx.y * N + c0 + j] = v;
+      else
+        atomicAdd(out + c0 + j, v);
+    }
+}
+
+// out[n] += sum_{y < nby} part[y][n], y in order (the deterministic colsum's second pass)
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int nby, int N,
+                                                            float* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f;
+  for (int y = 0; y < nby; ++y) a += part[(long long)y * N + n];
+  out[n] += a;
+}
+
+}  // namespace
+
+// y[r*ldy + c] = bf16(x[r*ldx + c]) for c < cols, 0 for cols <= c < ldy (row padding for 16-B rows)
+DL4SS_API int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy,
+                                   void* stream) {
+  DL4SS_REQUIRE(x && y && rows >= 0 && cols >= 0 && ldx >= cols && ldy >= cols);
+  if (rows == 0) return 0;
+  const long long n = (long long)rows * ldy;
+  hipLaunchKernelGGL(f32_to_bf16_2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), x,
+                     ldx, rows, cols, reinterpret_cast<unsigned short*>(y), ldy);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+static int colsum_bf16_launch(const void* A, long long lda, int M, int N, float* out, float* part, void* stream) {
+  const int rpb = 256;
+  const auto* a = reinterpret_cast<const unsigned short*>(A);
+  if (lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && lda >= ((N + 7) & ~7))  // 16-B rows, padding readable
+    hipLaunchKernelGGL(colsum_bf16_v_kernel<true>, dim3(cdiv(N, 512), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
+                       a, lda, M, N, rpb, out, part);
+  else
+    hipLaunchKernelGGL(colsum_bf16_v_kernel<false>, dim3(cdiv(N, 64), cdiv(M, rpb)), dim3(256), 0, as_stream(stream),
+                       a, lda, M, N, rpb, out, part);
+  DL4SS_CHECK_LAUNCH();
+  if (part) {
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cdiv(N, 256)), dim3(256), 0, as_stream(stream), part, cdiv(M, rpb), N,
+                       out);
+    DL4SS_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+DL4SS_API int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, void* stream) {
+  DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
+  if (M == 0 || N == 0) return 0;
+  return colsum_bf16_launch(A, lda, M, N, out, nullptr, stream);
+}
+
+// Bytes of the partial-sum workspace dl4ss_colsum_bf16_det needs for an M x N operand.
+DL4SS_API long long dl4ss_colsum_bf16_part_bytes(int M, int N) {
+  return M > 0 && N > 0 ? (long long)cdiv(M, 256) * N * 4 : 0;
+}
+
+// Deterministic dl4ss_colsum_bf16: per-256-row-block partial sums, then a fixed-order reduce
+// (the bf16 step's Linear bias gradient: bitwise reproducible run to run).
+DL4SS_API int dl4ss_colsum_bf16_det(const void* A, long long lda, int M, int N, float* out, float* part,
+                                    long long part_bytes, void* stream) {
+  DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
+  if (M == 0 || N == 0) return 0;
+  DL4SS_REQUIRE(part && part_bytes >= dl4ss_colsum_bf16_part_bytes(M, N));
+  return colsum_bf16_launch(A, lda, M, N, out, part, stream);
+}
+
+DL4SS_API int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ldx, const int* rows,
+                                         const int* cols, void* const* y, const long long* ldy, void* stream) {
+  DL4SS_REQUIRE(n >= 1 && n <= CVT_MAX && x && ldx && rows && cols && y && ldy);
+  CvtSegs sg{};
+  sg.n = n;
+  sg.row0[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    DL4SS_REQUIRE(x[i] && y[i] && rows[i] >= 0 && cols[i] >= 0 && ldx[i] >= cols[i] && ldy[i] >= cols[i] && ldy[i] > 0);
+    DL4SS_REQUIRE(ldy[i] % 2 == 0 && ((uintptr_t)y[i] & 3) == 0);  // 4-B pair stores
+    sg.x[i] = x[i];
+    sg.y[i] = reinterpret_cast<unsigned short*>(y[i]);
+    sg.ldx[i] = ldx[i];
+    sg.ldy[i] = ldy[i];
+    sg.cols[i] = cols[i];
+    sg.row0[i + 1] = sg.row0[i] + rows[i];
+  }
+  for (int i = n + 1; i <= CVT_MAX; ++i) sg.row0[i] = sg.row0[n];
+  if (sg.row0[n] == 0) return 0;
+  hipLaunchKernelGGL(f32_to_bf16_multi_kernel, dim3(sg.row0[n]), dim3(256), 0, as_stream(stream), sg);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
+
+// y = bf16(x), round to nearest even (the rounding gemm.hip applies at its LDS store).
+DL4SS_API int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream) {
+  DL4SS_REQUIRE(n >= 0 && (n == 0 || (x && y)));
+  if (n == 0) return 0;
+  DL4SS_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0);
+  const long long threads = (n + 3) / 4;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, as_stream(stream), x,
+                     reinterpret_cast<unsigned short*>(y), n);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}

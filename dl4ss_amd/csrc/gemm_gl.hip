@@ -1,8 +1,9 @@
 // bf16-operand MFMA GEMM with LDS-DMA staging (gfx950): C[M,N] (fp32) (+)= op(A) . op(B)
-// (+ bias) (tanh / tanh -> bf16), both operands already bf16 in HBM -- the second
-// generation of gemm_bb.hip for the separation step's GEMMs.
+// (+ bias) (tanh / tanh -> bf16), both operands already bf16 in HBM -- every GEMM of the
+// bf16 separation step.
 //
-// Why a new kernel: gemm_bb stages operands global -> VGPR -> ds_write_b128.  On gfx950 a
+// Why LDS-DMA: the round-1 kernel (register-staged, since removed) moved operands
+// global -> VGPR -> ds_write_b128.  On gfx950 a
 // ds_write_b128 moves ~79 B/clk/CU (MI355X_MICROARCH.md, LDS table), so refilling two
 // 128 x 64 bf16 tiles per k-tile for two workgroups costs ~810 LDS cycles against 1024
 // MFMA cycles, on top of the fragment reads: the 128 x 128 tile was LDS-bound at ~350
@@ -26,7 +27,7 @@
 // k beyond K reads a zero line (g_zero_line) instead of the operand, so partial k-tiles
 // need no masking pass; rows beyond M / N read clamped addresses (their outputs are not
 // stored).  Split-K (grid.z) stores fp32 partial slabs that gemm_gl_reduce_kernel adds in
-// fixed order (deterministic, unlike the atomics of gemm_bb's split-K).
+// fixed order (deterministic: no float atomics).
 #include "common.h"
 
 namespace {
@@ -740,7 +741,7 @@ DL4SS_API long long dl4ss_gemm_bf16_gl_ws_bytes(int M, int N, int K, int splitk,
   return s > 1 ? (long long)batch * s * M * N * 4 : 0;
 }
 
-// C = op(A) op(B) (+ bias) (epilogue), bf16 operands, the conventions of dl4ss_gemm_bf16_batched
+// C = op(A) op(B) (+ bias) (epilogue), bf16 operands, the layout conventions of dl4ss_gemm (strided batch)
 // (transA: A stored K x M; transB: B stored N x K).  Requires 16-B aligned operand rows (ld %
 // 8 == 0, aligned bases, strides % 8 == 0); returns hipErrorInvalidValue otherwise.  k-major
 // operands are bounded per k-row (exact for any K); a k-contiguous operand is read in 8-element

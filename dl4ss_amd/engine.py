@@ -25,6 +25,7 @@ from . import _lib, ops
 
 CELLS = {"lstm": 0, "gru": 1}
 WS_ZEROED = 0x100  # DL4SS_RNN_WS_ZEROED (include/dl4ss_hip.h)
+DGH_PAD8 = 0x200  # DL4SS_RNN_DGH_PAD8
 
 
 def _ngate(cell):
@@ -180,23 +181,12 @@ class SepTrainer:
         self.s1 = 1.0 / (B * nch * T * F)
         self.s2 = 0.0 if (mode == "crm" or loss_channels) else sum_weight / (B * T * F)
         self.spk = torch.empty(B, K, device=dev, dtype=torch.int32)
-        # bf16 mode: every GEMM operand is produced directly as bf16 (gemm_bb.hip): the BiRNN
-        # kernels write bf16 h / h_{t-1} / dG (and fuse the bias gradients), the attention
-        # kernel writes bf16 dPre, the weights and the layer-0 features are converted once per
-        # step.  Rows are padded to multiples of 8 (16-B aligned operand rows).
+        # bf16 mode: every GEMM of the step runs on the hand-written LDS-DMA MFMA kernel
+        # (gemm_gl.hip; deterministic split-K) and every operand is produced directly as bf16:
+        # the BiRNN kernels write bf16 h / h_{t-1} / dG / dGh (and fuse the bias gradients), the
+        # attention kernel writes bf16 dPre, the weights and the layer-0 features are converted
+        # once per step.  Rows are padded to multiples of 8 (16-B aligned operand rows).
         self.fast = precision == "bf16" and self.rnn_precision == "bf16"
-        # bf16 mode GEMM path (DL4SS_GEMM): "gl" (default) every GEMM of the step on the
-        # hand-written LDS-DMA kernel (gemm_gl.hip; deterministic split-K); "lt" the round-1
-        # form: forward on gemm_bb.hip, plain backward GEMMs through hipBLASLt; "bb" all on gemm_bb
-        self.gemm_path = os.environ.get("DL4SS_GEMM", "gl") if self.fast else "bb"
-        if self.gemm_path not in ("gl", "lt", "bb"):
-            raise ValueError(f"DL4SS_GEMM={self.gemm_path}: expected gl, lt or bb")
-        self.use_lt = self.gemm_path == "lt"
-        # DL4SS_OVERLAP=1: weight-gradient GEMMs of layer l on a side stream, concurrent with the
-        # BPTT of layer l-1.  Off by default: measured 6.89 vs 6.41 ms per step -- the GEMM
-        # workgroups share CUs with the persistent recurrence and slow every hand-off more
-        # than the hidden GEMM time saves.
-        self.overlap = self.gemm_path != "bb" and os.environ.get("DL4SS_OVERLAP", "0") == "1"
         # Forward input projections x W_ih^T + b_ih formed inside the packed recurrence kernel
         # (dl4ss_birnn_fwd_xw) instead of a gemm_gl launch + a G buffer round trip; bitwise the same
         # G (tests/test_rnn_xw_gpu.py).  DL4SS_RNN_XW: "l0" (default) the first layer only (129
@@ -206,9 +196,8 @@ class SepTrainer:
         xw = os.environ.get("DL4SS_RNN_XW", "l0")
         if xw not in ("0", "1", "l0"):
             raise ValueError(f"DL4SS_RNN_XW={xw}: expected 0, 1 or l0")
-        self.xw = self.fast and self.gemm_path == "gl" and xw != "0"
+        self.xw = self.fast and xw != "0"
         self.xw_kmax = 160 if xw == "l0" else 640
-        self.side = torch.cuda.Stream(device=dev) if self.overlap else None
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
             p8 = lambda n: (n + 7) // 8 * 8
@@ -217,23 +206,20 @@ class SepTrainer:
             self.xb0 = torch.empty(BT, p8(D0), **bf)
             self.outb = [torch.empty(BT, p8(2 * H), **bf) for _ in range(net.L)]
             self.hprevb = [torch.empty(BT, 2 * p8(H), **bf) for _ in range(net.L)]
-            # two of each: with the weight-gradient GEMMs of layer l on the side stream, BPTT of
-            # layer l-1 writes the other buffer
-            self.dGb2 = [torch.empty(BT, 2 * NGH, **bf) for _ in range(2)]
-            self.dGhb2 = [torch.empty(BT, 2 * NGH, **bf) for _ in range(2)] if net.cell == "gru" else None
-            self.dGb = self.dGb2[0]
-            self.dGhb = self.dGhb2[0] if self.dGhb2 else None
+            self.dGb = torch.empty(BT, 2 * NGH, **bf)
+            # GRU dGh: each direction's gate columns start 16-B aligned (900 -> 904,
+            # DL4SS_RNN_DGH_PAD8) so both directions' dW_hh are one batched LDS-DMA GEMM
+            self.ngh_p8 = p8(NGH)
+            self.dGhb = torch.empty(BT, 2 * self.ngh_p8, **bf) if net.cell == "gru" else None
             # zero row padding (never written): gemm_gl reads k-contiguous rows in 8-element chunks
             self.dPreb = torch.zeros(BT, p8(F * net.E), **bf)
-            # gemm_gl split-K slabs (the largest split of _backward_fast: dH at 3; the side stream
-            # of DL4SS_OVERLAP gets its own)
+            # gemm_gl split-K slabs (the largest split of _backward_fast)
             FE_ = F * net.E
             gl_need = max(_lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, FE_, 3, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", FE_, 2 * H, BT, 2, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", 2 * NGH, 2 * H, BT, 4, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", NGH, H, BT, 8, 2))
             self.gl_ws = torch.empty(max(gl_need, 1), device=dev, dtype=torch.uint8)
-            self.gl_ws_side = torch.empty_like(self.gl_ws) if self.overlap else self.gl_ws
             # partial sums of the deterministic Linear-bias colsum (dl4ss_colsum_bf16_det)
             pb = _lib.query("dl4ss_colsum_bf16_part_bytes", BT, F * net.E)
             self.colsum_part = torch.empty(max(1, pb // 4), device=dev, dtype=torch.float32)
@@ -312,8 +298,7 @@ class SepTrainer:
 
     def _gemm_fwd(self, x, w, bias, out, epilogue=ops.EPI_NONE):
         """out = x w^T + bias (epilogue): the input projections and the Linear (+ tanh -> bf16 V)"""
-        f = ops.gemm_bf16_gl if self.gemm_path == "gl" else ops.gemm_bf16
-        f(x, w, transB=True, bias=bias, epilogue=epilogue, out=out)
+        ops.gemm_bf16_gl(x, w, transB=True, bias=bias, epilogue=epilogue, out=out)
 
     def forward(self, feats=None):
         net, B, T, H = self.net, self.B, self.T, self.net.H
@@ -387,99 +372,41 @@ class SepTrainer:
         cell = CELLS[net.cell]
         dPreb = self.dPreb[:, :FE]
         hLb = self.outb[-1][:, :2 * H]
-        lt = self.use_lt  # plain (epilogue-free) GEMMs through hipBLASLt, else the hand-written kernel
-        main = torch.cuda.current_stream()
-        ov = self.overlap
-        st = _lib.stream_ptr(main)
+        st = _lib.stream_ptr()
+        gru = self.dGhb is not None
         self.rnn_ws_all[1].zero_()  # every layer's BPTT hand-off workspace, one fill
-
-        def on_side(fn):
-            """run fn on the side stream once everything queued on the main stream so far is done"""
-            if not ov:
-                fn()
-                return
-            self.side.wait_stream(main)
-            with torch.cuda.stream(self.side):
-                fn()
-
-        gl = self.gemm_path == "gl"
         # gemm_gl split-K factors, measured per shape at C2 (tools/gemm_gl_bench.py --sweep): dH
         # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
         # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
         dH = self.dH[0]
-        if gl:
-            ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk=3, ws=self.gl_ws)  # input gradient first
-        elif lt:
-            ops.gemm_bf16_lt(dPreb, self.wb_lin[:, :2 * H], dH)  # the input gradient first: BPTT waits on it
-        else:
-            ops.gemm_bf16(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk="auto")
-
-        def linear_grads():
-            if gl:
-                ops.gemm_bf16_gl(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk=2,
-                                 ws=self.gl_ws_side)
-            elif lt:
-                ops.gemm_bf16_lt(dPreb, hLb, net.view("mix.Linear.weight", g), transA=True, beta=1.0)
-            else:
-                ops.gemm_bf16(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto")
-            _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
-                      _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part), self.colsum_part.numel() * 4,
-                      _lib.stream_ptr())
-
-        on_side(linear_grads)
+        ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk=3, ws=self.gl_ws)  # input gradient first
+        ops.gemm_bf16_gl(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk=2,
+                         ws=self.gl_ws)
+        _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+                  _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part), self.colsum_part.numel() * 4, st)
         hp8 = self.p8(H)
-        done = {}  # layer -> event after its weight-gradient GEMMs on the side stream
+        dGb, dGhb = self.dGb, self.dGhb if gru else self.dGb
+        ldgh = self.ngh_p8 if gru else NGH  # dW_hh operand: direction d at column d * ldgh
         for l in range(net.L - 1, -1, -1):
-            dGb = self.dGb2[l % 2]
-            dGhb = self.dGhb2[l % 2] if self.dGhb2 else dGb
-            if l + 2 in done:  # dGb2[l % 2] was layer l+2's: its weight gradients must have read it
-                main.wait_event(done[l + 2])
-            _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(dH),
+            _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED | (DGH_PAD8 if gru else 0), B, T, H, _lib.ptr(dH),
                       _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), None, None,
-                      _lib.ptr(dGb), _lib.ptr(dGhb) if self.dGhb2 else None, _lib.ptr(net.cat_view("bias_ih", l, g)),
+                      _lib.ptr(dGb), _lib.ptr(self.dGhb) if gru else None, _lib.ptr(net.cat_view("bias_ih", l, g)),
                       _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self._ws_slot(l, True)), self.ws_bytes,
                       _lib.ptr(self.status), st)
             if l > 0:  # the input gradient first: it is all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
-                if gl:
-                    ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next)
-                elif lt:
-                    ops.gemm_bf16_lt(dGb, self.wb_ih[l][:, :2 * H], dH_next)
-                else:
-                    ops.gemm_bf16(dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk="auto")
+                ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next)
             xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
-
-            def weight_grads(l=l, dGb=dGb, dGhb=dGhb, xb=xb):
-                whh_g = net.cat_view("weight_hh", l, g)
-                # both directions' dW_hh in one launch: member d = columns d*NGH of dGh, d*pad8(H) of h_{t-1}
-                if gl:
-                    ops.gemm_bf16_gl(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), beta=1.0, splitk=4,
-                                     ws=self.gl_ws_side)
-                    if NGH % 8 == 0:
-                        ops.gemm_bf16_gl(dGhb[:, :NGH], self.hprevb[l][:, :H], transA=True, out=whh_g[:NGH],
-                                         beta=1.0, splitk=8, batch=2, strideA=NGH, strideB=hp8, strideC=NGH * H,
-                                         M=NGH, N=H, K=BT, ws=self.gl_ws_side)
-                    else:  # GRU (NGH = 900): the reverse direction's columns are not 16-B aligned for LDS-DMA
-                        ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
-                                              NGH, H, BT, transA=True, beta=1.0, splitk="auto")
-                elif lt:
-                    ops.gemm_bf16_lt(dGb, xb, net.cat_view("weight_ih", l, g), transA=True, beta=1.0)
-                    ops.gemm_bf16_lt(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], transA=True, beta=1.0,
-                                     batch=2, strideA=NGH, strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT)
-                else:
-                    ops.gemm_bf16(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), splitk="auto", beta=1.0)
-                    ops.gemm_bf16_batched(dGhb[:, :NGH], self.hprevb[l][:, :H], whh_g[:NGH], 2, NGH, hp8, NGH * H,
-                                          NGH, H, BT, transA=True, beta=1.0, splitk="auto")
-
-            on_side(weight_grads)
-            if ov:
-                done[l] = self.side.record_event()
+            ops.gemm_bf16_gl(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), beta=1.0, splitk=4,
+                             ws=self.gl_ws)
+            # both directions' dW_hh in one launch: member d = columns d*ldgh of dGh, d*pad8(H) of h_{t-1}
+            ops.gemm_bf16_gl(dGhb[:, :NGH], self.hprevb[l][:, :H], transA=True,
+                             out=net.cat_view("weight_hh", l, g)[:NGH], beta=1.0, splitk=8, batch=2, strideA=ldgh,
+                             strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT, ws=self.gl_ws)
             if l > 0:
                 dH = dH_next
-        if ov:
-            main.wait_stream(self.side)  # every gradient is in place before the all-reduce / Adam
 
     def backward(self):
         net, B, T, H = self.net, self.B, self.T, self.net.H
@@ -591,13 +518,11 @@ class SepTrainer:
 
     def capture(self):
         """Record STFT -> forward -> loss -> backward (~70 launches: persistent BiRNN
-        kernels, MFMA / hipBLASLt GEMMs, attention, small kernels) as one HIP graph,
-        replayed by step_graph().  The mixing kernel (its input pointer changes per batch),
-        the RCCL all-reduce and Adam (its bias correction is a per-step host scalar) stay
-        eager launches around the replay.  Call after at least one eager step(), so every
-        GEMM plan (hipBLASLt heuristic timing) and workspace exists before the capture."""
-        if self.overlap:
-            raise RuntimeError("capture(): the DL4SS_OVERLAP side stream is not captured")
+        kernels, gemm_gl GEMMs, attention, small kernels) as one HIP graph, replayed by
+        step_graph().  The mixing kernel (its input pointer changes per batch), the RCCL
+        all-reduce and Adam (its bias correction is a per-step host scalar) stay eager launches
+        around the replay.  Call after at least one eager step(), so every workspace exists
+        before the capture."""
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):

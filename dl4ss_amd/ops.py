@@ -87,7 +87,7 @@ def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=N
 # dense contractions
 # ---------------------------------------------------------------------------
 PREC = {"fp32": 0, "bf16": 1}
-EPI_NONE, EPI_TANH, EPI_TANH_BF16 = 0, 1, 2  # 2: tanh written as bf16 (gemm_bf16 only)
+EPI_NONE, EPI_TANH, EPI_TANH_BF16 = 0, 1, 2  # 2: tanh written as bf16 (gemm_bf16_gl only)
 
 
 def _mat(t, name):
@@ -140,59 +140,13 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.
     return out
 
 
-GEMM_BF16_TARGET_WGS = 256  # measured best on MI355X (tools/gemm_bench_bf16.py sweep: 256/512/768)
 GEMM_GL_TARGET_WGS = 512  # gemm_gl (2 workgroups per CU): split-K to about two per CU
-
-
-def gemm_bf16_set_tile(tile):
-    """Force the bf16 GEMM tile configuration (0 automatic, 1 128x128, 2 256x128, 3 256x256)."""
-    _lib.call("dl4ss_gemm_bf16_set_tile", int(tile))
 
 
 def _mat_bf16(t, name):
     if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
         raise RuntimeError(f"{name}: expected a 2-D row-major bfloat16 CUDA matrix (unit inner stride)")
     return t
-
-
-def gemm_bf16(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE, beta=0.0, out=None, splitk=1):
-    """out (fp32) = op(A) @ op(B) (+ bias) (tanh) (+ beta*out) with bf16 A and B
-    (dl4ss_gemm_bf16: the bf16-operand MFMA GEMM, gemm_bb.hip).  Layout and split-K
-    conventions as gemm()."""
-    _mat_bf16(A, "gemm_bf16(A)")
-    _mat_bf16(B, "gemm_bf16(B)")
-    M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
-    Kb, N = (B.shape[1], B.shape[0]) if transB else (B.shape[0], B.shape[1])
-    if K != Kb:
-        raise RuntimeError(f"gemm_bf16: inner dims differ ({K} vs {Kb})")
-    if out is None:
-        if beta != 0.0 or splitk not in (1, "auto"):
-            raise RuntimeError("gemm_bf16: accumulation needs an output tensor")
-        out = torch.empty(M, N, device=A.device,
-                          dtype=torch.bfloat16 if epilogue == EPI_TANH_BF16 else torch.float32)
-    if epilogue == EPI_TANH_BF16:
-        _mat_bf16(out, "gemm_bf16(out, bf16 epilogue)")
-        if beta != 0.0:
-            raise RuntimeError("gemm_bf16: the bf16-output epilogue does not accumulate")
-    else:
-        _mat(out, "gemm_bf16(out)")
-    if tuple(out.shape) != (M, N):
-        raise RuntimeError(f"gemm_bf16: out shape {tuple(out.shape)} != {(M, N)}")
-    if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
-        raise RuntimeError("gemm_bf16: bias must be contiguous with N elements")
-    if splitk == "auto":
-        # split-K adds fp32 atomic traffic (1.3 TB/s) on the output: split only as far as ~256
-        # workgroups (the sweep in tools/gemm_bench_bf16.py)
-        splitk = auto_splitk(M, N, K, target_wgs=GEMM_BF16_TARGET_WGS) if epilogue == EPI_NONE else 1
-        if splitk > 1 and beta == 0.0:
-            out.zero_()
-            beta = 1.0
-        elif splitk > 1 and beta != 1.0:
-            splitk = 1
-    _lib.call("dl4ss_gemm_bf16", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
-              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue,
-              float(beta), int(splitk), _lib.stream_ptr())
-    return out
 
 
 _gl_ws = {}
@@ -214,7 +168,7 @@ def gemm_bf16_gl(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE,
                  batch=1, strideA=0, strideB=0, strideC=0, M=None, N=None, K=None, ws=None):
     """out (fp32, or bf16 with EPI_TANH_BF16) = op(A) @ op(B) (+ bias) (epilogue) (+ beta*out)
     with bf16 A and B through the LDS-DMA MFMA kernel (dl4ss_gemm_bf16_gl, gemm_gl.hip).
-    Layout conventions as gemm_bf16; split-K is deterministic (fp32 slabs + fixed-order
+    Layout conventions as gemm(); split-K is deterministic (fp32 slabs + fixed-order
     reduce); batch > 1 takes raw element strides from the first-member views.  ws: the
     caller's split-K workspace (a uint8 tensor), else a per-device/stream one grown on demand."""
     _mat_bf16(A, "gemm_bf16_gl(A)")
@@ -247,48 +201,6 @@ def gemm_bf16_gl(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE,
               _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), _lib.ptr(bias), epilogue,
               float(beta), int(splitk), int(batch), int(strideA), int(strideB), int(strideC), _lib.ptr(ws),
               ws.numel() if ws is not None else 0, _lib.stream_ptr())
-    return out
-
-
-LT_WS_BYTES = 32 << 20  # hipBLASLt workspace cap (allocated once per device)
-_lt_ws = {}
-
-
-def gemm_bf16_lt(A, B, out, transA=False, transB=False, beta=0.0, batch=1, strideA=0, strideB=0, strideC=0,
-                 M=None, N=None, K=None):
-    """out (fp32) = op(A) @ op(B) + beta*out with bf16 A, B through hipBLASLt
-    (dl4ss_gemm_bf16_lt): the plain backward GEMMs.  Layout conventions as gemm_bf16; with
-    batch > 1 the member offsets are raw element strides from the given first-member views."""
-    _mat_bf16(A, "gemm_bf16_lt(A)")
-    _mat_bf16(B, "gemm_bf16_lt(B)")
-    _mat(out, "gemm_bf16_lt(out)")
-    if M is None:
-        M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
-        N = B.shape[0] if transB else B.shape[1]
-    key = (A.device, torch.cuda.current_stream().cuda_stream)  # one workspace per stream (concurrent GEMMs)
-    ws = _lt_ws.get(key)
-    if ws is None:
-        ws = _lt_ws[key] = torch.empty(LT_WS_BYTES, dtype=torch.uint8, device=A.device)
-    _lib.call("dl4ss_gemm_bf16_lt", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
-              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), float(beta), int(batch),
-              int(strideA), int(strideB), int(strideC), _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
-    return out
-
-
-def gemm_bf16_batched(A, B, out, batch, strideA, strideB, strideC, M, N, K, transA=False, transB=False,
-                      beta=0.0, splitk=1):
-    """Strided batch of gemm_bf16 over raw views: member i reads A/B at element offsets
-    i*strideA / i*strideB from the given (first-member) views and writes out + i*strideC."""
-    _mat_bf16(A, "gemm_bf16_batched(A)")
-    _mat_bf16(B, "gemm_bf16_batched(B)")
-    _mat(out, "gemm_bf16_batched(out)")
-    if splitk == "auto":
-        splitk = auto_splitk(M, N, K, target_wgs=max(1, GEMM_BF16_TARGET_WGS // batch))
-        if splitk > 1 and beta == 0.0:
-            raise RuntimeError("gemm_bf16_batched: split-K accumulates (beta 1) into a zeroed output")
-    _lib.call("dl4ss_gemm_bf16_batched", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
-              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), None, EPI_NONE, float(beta),
-              int(splitk), int(batch), int(strideA), int(strideB), int(strideC), _lib.stream_ptr())
     return out
 
 

@@ -77,21 +77,12 @@ int dl4ss_gemm(int transA, int transB, int M, int N, int K, const float* A, long
                long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta, int precision,
                int splitk, void* stream);
 
-/* bf16-operand form of dl4ss_gemm (precision bf16): A and B are raw bf16 words already
- * rounded by their producers; C fp32.  Same layout, epilogue and split-K conventions;
- * the products equal dl4ss_gemm(precision = BF16) on the fp32 originals. */
-int dl4ss_gemm_bf16(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
-                    long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta, int splitk,
-                    void* stream);
-/* Strided batch (grid.y): member i uses A + i*strideA, B + i*strideB, C + i*strideC (elements). */
-int dl4ss_gemm_bf16_batched(int transA, int transB, int M, int N, int K, const void* A, long long lda,
-                            const void* B, long long ldb, float* C, long long ldc, const float* bias, int epilogue,
-                            float beta, int splitk, int batch, long long strideA, long long strideB,
-                            long long strideC, void* stream);
 /* y[i] = bf16(x[i]) (round to nearest even), n elements; x 16-B aligned, y 8-B aligned. */
 int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream);
-/* bf16-operand GEMM with LDS-DMA staging (gemm_gl.hip; replaces hipBLASLt and gemm_bb on the
- * step's GEMMs): semantics of dl4ss_gemm_bf16_batched plus a deterministic split-K (fp32
+/* bf16-operand GEMM with LDS-DMA staging (gemm_gl.hip): every GEMM of the bf16 step.  A and B
+ * are raw bf16 words already rounded by their producers, C fp32 (or bf16 with the tanh-bf16
+ * epilogue); layout, bias and epilogue as dl4ss_gemm.  Strided batch: member i uses
+ * A + i*strideA, B + i*strideB, C + i*strideC (elements).  Deterministic split-K (fp32
  * slabs in ws, dl4ss_gemm_bf16_gl_ws_bytes bytes, then a fixed-order reduce; EPI_NONE only).
  * Needs lda / ldb / strides % 8 == 0, 16-B aligned A / B, for a k-major operand a row stride
  * >= its row count rounded up to 8, and for a k-contiguous one a row stride >= K rounded up
@@ -104,17 +95,6 @@ int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, const void* 
                        long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta,
                        int splitk, int batch, long long strideA, long long strideB, long long strideC, void* ws,
                        long long ws_bytes, void* stream);
-/* Plain bf16-operand GEMM (no epilogue) through hipBLASLt: the backward pass's weight /
- * input gradients (dW_lin, dH, dW_ih, dW_hh, dX of EvalVer.py:673's autograd).  Semantics
- * of dl4ss_gemm_bf16_batched with epilogue NONE and no split-K; workspace (may be NULL when
- * ws_bytes is 0) is the caller's. */
-int dl4ss_gemm_bf16_lt(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
-                       long long ldb, float* C, long long ldc, float beta, int batch, long long strideA,
-                       long long strideB, long long strideC, void* workspace, long long ws_bytes, void* stream);
-/* Tuning knob of dl4ss_gemm_bf16[_batched]: force a tile configuration for later calls
- * (0 automatic, 1 = 128x128 / 4 waves, 2 = 256x128 / 8 waves, 3 = 256x256 / 8 waves). */
-int dl4ss_gemm_bf16_set_tile(int tile);
-
 /* 2-D form with row padding: y[r*ldy + c] = bf16(x[r*ldx + c]) (c < cols), 0 up to ldy. */
 int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, void* stream);
 /* out[n] += sum_m A[m*lda + n] for a bf16 matrix A (bias gradient from bf16 dPre). */
@@ -138,6 +118,10 @@ enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
  * DL4SS_RNN_WS_ZEROED: the caller then guarantees it is zero (e.g. one fill per training
  * step over separate workspaces for every layer and pass). */
 #define DL4SS_RNN_WS_ZEROED 0x100
+/* precision flag of dl4ss_birnn_bwd_ex: dGh_bf16 is laid out (B, T, 2, pad8(NGATE*H)) -- each
+ * direction's columns start 16-B aligned (the GRU's 900 gate rows -> 904), so both directions'
+ * dW_hh run as one LDS-DMA batched GEMM (gemm_gl).  The unpadded default is (B, T, 2, NGATE*H). */
+#define DL4SS_RNN_DGH_PAD8 0x200
 long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
 /* The persistent recurrence's plan under a co-residency budget: every workgroup of a launch
  * (2 directions x nchunk batch chunks x NG units groups) must be resident at once, so the

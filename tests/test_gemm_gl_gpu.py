@@ -94,20 +94,22 @@ def test_gemm_gl_splitk_deterministic(dev, ta, tb):
         _check(o, ref + C0.double().cpu(), mag + C0.double().cpu().abs())
 
 
-def test_gemm_gl_strided_batch(dev):
-    """both directions' dW_hh in one launch: member d reads columns d*NGH of dGh and d*pad8(H)
-    of h_{t-1} (the engine's batched form), with and without split-K"""
+@pytest.mark.parametrize("NGH,ldg", [(1200, 1200), (900, 904)], ids=["lstm", "gru_pad8"])
+def test_gemm_gl_strided_batch(dev, NGH, ldg):
+    """both directions' dW_hh in one launch: member d reads columns d*ldg of dGh and d*pad8(H)
+    of h_{t-1} (the engine's batched form), with and without split-K.  GRU: 900 gate rows per
+    direction, stored at a 904-column stride (DL4SS_RNN_DGH_PAD8) so member 1 starts 16-B aligned."""
     g = torch.Generator(device="cpu").manual_seed(3)
-    BT, NGH, H, hp8 = 1004, 1200, 300, 304
-    dG = ops.to_bf16(torch.randn(BT, 2 * NGH, generator=g).to(dev))
+    BT, H, hp8 = 1004, 300, 304
+    dG = ops.to_bf16(torch.randn(BT, 2 * ldg, generator=g).to(dev))
     hp = ops.to_bf16(torch.randn(BT, 2 * hp8, generator=g).to(dev))
-    for s in (1, 3):
+    for s in (1, 3, 8):
         out = torch.zeros(2 * NGH, H, device=dev)
         ops.gemm_bf16_gl(dG[:, :NGH], hp[:, :H], transA=True, out=out[:NGH], beta=1.0, splitk=s, batch=2,
-                         strideA=NGH, strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT)
+                         strideA=ldg, strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT)
         torch.cuda.synchronize()
         for d in range(2):
-            ref, mag = _ref(dG[:, d * NGH:(d + 1) * NGH], hp[:, d * hp8:d * hp8 + H], True, False)
+            ref, mag = _ref(dG[:, d * ldg:d * ldg + NGH], hp[:, d * hp8:d * hp8 + H], True, False)
             _check(out[d * NGH:(d + 1) * NGH], ref, mag)
 
 

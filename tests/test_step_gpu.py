@@ -230,20 +230,23 @@ def test_graph_step_matches_eager(dev, precision, mode):
         assert float(dp.max()) <= 2 * 2e-4 and int((dp > 1e-6).sum()) <= max(1, dp.numel() // 10000)
 
 
-@pytest.mark.parametrize("precision,mode,B", [("bf16", "pit", 4), ("bf16", "label", 4), ("bf16", "pit", 32)])
-def test_step_bitwise_reproducible(dev, precision, mode, B):
+@pytest.mark.parametrize("precision,mode,B,cell,K", [("bf16", "pit", 4, "lstm", 2), ("bf16", "label", 4, "lstm", 2),
+                                                     ("bf16", "pit", 32, "lstm", 2), ("bf16", "pit", 4, "gru", 2),
+                                                     ("bf16", "pit", 32, "gru", 3)])
+def test_step_bitwise_reproducible(dev, precision, mode, B, cell, K):
     """The bf16 throughput step: two steps from the same saved state on the same batch give
     bit-identical losses, gradients and parameters (every reduction has a fixed order; the
     BiRNN bias gradients go through per-row partials and bias_reduce_kernel, not float
-    atomics).  The fp32 parity mode is not covered: its split-K GEMMs (gemm.hip) and
-    fp32 BPTT accumulate with atomics."""
-    K, N = 2, 8000
+    atomics; every GEMM, the BiGRU's dW_hh included (its dGh direction columns padded to 904,
+    DL4SS_RNN_DGH_PAD8), is gemm_gl's fixed-order split-K).  The fp32 parity mode is not
+    covered: its split-K GEMMs (gemm.hip) and fp32 BPTT accumulate with atomics."""
+    N = 8000
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=9)
     src, spk, u = gen.batch(B)
     batch = (torch.from_numpy(src.astype(np.float32)).to(dev),
              torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
              torch.from_numpy(spk.astype(np.int32)).to(dev))
-    net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=11)
+    net = engine.SepNet(cell=cell, num_layers=2, adjust=cell == "lstm", device=dev, seed=11)
     tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision)
     tr.step(*batch)
     state = (net.flat.detach().clone(), tr.m.clone(), tr.v.clone(), tr.step_count)

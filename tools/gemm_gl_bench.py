@@ -1,6 +1,6 @@
-"""Time the C2 step's GEMM shapes (B = 32: BT = 8032) on the three bf16 GEMM paths:
-gemm_bb (register-staged, gemm_bb.hip), hipBLASLt (gemm_lt.hip; epilogue-free shapes only) and
-gemm_gl (LDS-DMA, gemm_gl.hip).  HIP events around 20 back-to-back launches on random data;
+"""Time the C2 step's GEMM shapes (B = 32: BT = 8032) on gemm_gl (LDS-DMA, gemm_gl.hip) in each
+tile configuration, beside torch's bf16 matmul (the vendor library: a timing reference only,
+bf16 output, epilogue-free shapes).  HIP events around 20 back-to-back launches on random data;
 prints one JSON line per shape and path (us per launch, TFLOP/s)."""
 import json
 import sys
@@ -80,15 +80,14 @@ for name, (flop, kw) in shapes.items():
             _lib.call("dl4ss_gemm_gl_set_config", cfg)
             ops.gemm_bf16_gl(A, B, out=out, splitk=SPLIT if split is None else split, **kw)
         return f
-    paths = {"gemm_bb": lambda: ops.gemm_bf16(A, B, out=out, splitk="auto" if beta == 1.0 else 1, **kw),
-             "gemm_gl": gl(1), "gemm_gl_256x128": gl(2), "gemm_gl_pp256": gl(4), "gemm_gl_pp256_10": gl(5)}
+    paths = {"gemm_gl": gl(1), "gemm_gl_256x128": gl(2), "gemm_gl_pp256": gl(4), "gemm_gl_pp256_10": gl(5)}
     if SPLIT > 1:
         paths["gemm_gl_256x128_halfsplit"] = gl(2, max(1, SPLIT // 2))
     for s in (2, 3, 4, 6, 8, 12):
         paths[f"gemm_gl_pp256 splitk={s}"] = gl(4, s)
         paths[f"gemm_gl_pp256_10 splitk={s}"] = gl(5, s)
     if epi == ops.EPI_NONE and kw.get("bias") is None:
-        paths["hipblaslt"] = lambda: ops.gemm_bf16_lt(A, B, out, transA=ta, transB=tb, beta=beta)
+        paths["torch_bf16_matmul"] = lambda: torch.matmul(A.t() if ta else A, B.t() if tb else B)
     for pname, fn in paths.items():
         try:
             us = timeit(fn)
@@ -98,9 +97,7 @@ for name, (flop, kw) in shapes.items():
             print(json.dumps({"shape": name, "path": pname, "error": str(e)[:200]}), flush=True)
 # dW_hh: both directions batched
 flop = 2 * BT * 1200 * H * 2
-fns = {"gemm_bb": lambda: ops.gemm_bf16_batched(dG[:, :1200], hp[:, :H], dWhh[:1200], 2, 1200, p8(H), 1200 * H, 1200,
-                                                H, BT, transA=True, beta=1.0, splitk="auto"),
-       "gemm_gl": lambda: ops.gemm_bf16_gl(dG[:, :1200], hp[:, :H], transA=True, out=dWhh[:1200], beta=1.0,
+fns = {"gemm_gl": lambda: ops.gemm_bf16_gl(dG[:, :1200], hp[:, :H], transA=True, out=dWhh[:1200], beta=1.0,
                                            splitk=8, batch=2, strideA=1200, strideB=p8(H), strideC=1200 * H,
                                            M=1200, N=H, K=BT),
        "gemm_gl_pp256 splitk=8": lambda: (_lib.call("dl4ss_gemm_gl_set_config", 4), ops.gemm_bf16_gl(
@@ -108,9 +105,7 @@ fns = {"gemm_bb": lambda: ops.gemm_bf16_batched(dG[:, :1200], hp[:, :H], dWhh[:1
            strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT), _lib.call("dl4ss_gemm_gl_set_config", 0)),
        "gemm_gl_pp256 splitk=12": lambda: (_lib.call("dl4ss_gemm_gl_set_config", 4), ops.gemm_bf16_gl(
            dG[:, :1200], hp[:, :H], transA=True, out=dWhh[:1200], beta=1.0, splitk=12, batch=2, strideA=1200,
-           strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT), _lib.call("dl4ss_gemm_gl_set_config", 0)),
-       "hipblaslt": lambda: ops.gemm_bf16_lt(dG[:, :1200], hp[:, :H], dWhh[:1200], transA=True, beta=1.0, batch=2,
-                                             strideA=1200, strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT)}
+           strideB=p8(H), strideC=1200 * H, M=1200, N=H, K=BT), _lib.call("dl4ss_gemm_gl_set_config", 0))}
 _lib.call("dl4ss_gemm_gl_set_config", 0)
 for pname, fn in fns.items():
     us = timeit(fn)
