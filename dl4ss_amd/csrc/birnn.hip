@@ -529,7 +529,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int PKU = 24;     // staged h slots per (row, producer): 8 granules x 3
 constexpr int XKMAX = 2 * HMAX / 32;  // fused input projection: k-steps of 32 (Kin <= 2 HMAX)
-constexpr int SXB = XKMAX * 32;       // bf16 row stride of its B images (80 16-B chunks)
+// bf16 row stride of its B images: 80 16-B chunks of data + 2 pad chunks (656 bf16 = 328 dwords:
+// the BC rows and the zero row land on distinct bank quads for every 16-lane ds_read_b128
+// group; at 80 chunks every row started on bank 0, a 4-way conflict, tools/lds_banks.py)
+constexpr int SXC = XKMAX * 4 + 2;    // 16-B chunks per row
+constexpr int SXB = SXC * 8;
+// the one zero row of the fused projection's B reads sits after the ring at the bank offset
+// row BC of a ring buffer would have (so it, too, is conflict-free against rows 0..BC-1)
+constexpr int SXZ_SLACK = 128;        // bf16
 constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
@@ -621,19 +628,24 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const int GH = NGATE * H;
   const int tile = wv < WPOLL ? wv : wv - 1;
   const bool mv = wv != WPOLL && tile < MT;
+  const int SGS = MT * 16 + 4;  // sgate row stride (floats): 4 batch rows on 4 distinct bank quads
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  unsigned short* shb = reinterpret_cast<unsigned short*>(smem);                       // [16][SHB]
-  float* sgate = smem + 8 * SHB;                                                        // [BC][MT*16]
-  float* sin = sgate + BC * MT * 16;                                                    // [2][BC*32][4]
+  // h B image [16][SHB]: rows 0..BC-1 are the gathered h, row BC stays zero and every MFMA lane
+  // of a row >= BC reads it (one broadcast address instead of 15 - BC zero rows: the matvec's B
+  // reads are conflict-free, tools/lds_banks.py)
+  unsigned short* shb = reinterpret_cast<unsigned short*>(smem);
+  float* sgate = smem + 8 * SHB;                                                        // [BC][SGS]
+  float* sin = sgate + BC * SGS;                                                        // [2][BC*32][4]
   unsigned short* spub = reinterpret_cast<unsigned short*>(sin + 2 * BC * 32 * 4);      // [BC][PKU]
   // XW: XRING step buffers of the layer-input rows ([BC][SXB] bf16 + the pad items of the last
   // DMA piece) and one zero row (the B-image rows >= BC), 16-B aligned
-  constexpr int NXQ = XW ? (BC * 80 + 127) / 128 : 1;  // DMA pieces per prefetch wave and step
-  constexpr int XBUF = NXQ * 128 * 8;                   // bf16 per step buffer
+  static_assert(!XW || FWD_NPW == 2, "the fused projection's DMA pieces assume two prefetch waves of 64 lanes");
+  constexpr int NXQ = XW ? (BC * SXC + 127) / 128 : 1;  // DMA pieces per prefetch wave and step
+  constexpr int XBUF = NXQ * 128 * 8;                    // bf16 per step buffer (a multiple of 256 B)
   unsigned short* sxb = reinterpret_cast<unsigned short*>(
-      (reinterpret_cast<uintptr_t>(spub + BC * PKU) + 15) & ~static_cast<uintptr_t>(15));
-  unsigned short* sxz = sxb + XRING * XBUF;  // [SXB] zeros
+      (reinterpret_cast<uintptr_t>(spub + BC * PKU) + 255) & ~static_cast<uintptr_t>(255));
+  unsigned short* sxz = sxb + XRING * XBUF + (BC * SXB) % SXZ_SLACK;  // [SXB] zeros
 
   // ---- W_hh tile of this wave as bf16 A fragments: lane holds A[row tile*16 + (lane&15)][k]
   bf16x8 afrag[KSMAX];
@@ -717,10 +729,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   StepLoader<NQ> ld;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int i = tid - (WPOLL + 1) * 64 + q * NPF;  // item = gate * (BC*J) + cell
-    const int gate = i / (BC * J), cell = i % (BC * J);
+    // item = cell * 4 + gate: consecutive lanes commit consecutive LDS words (conflict-free
+    // ds_write_b32; gate-major items were 16 B apart, a 4-way conflict)
+    const int i = tid - (WPOLL + 1) * 64 + q * NPF;
+    const int gate = i & 3, cell = i >> 2;
     const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
-    const bool on = pfw && gate < NGATE;
+    const bool on = pfw && gate < NGATE && cell < BC * J;
     ld.p[q] = (on && ib < a.B && ij < H) ? a.G + ((long long)ib * T * 2 + d) * GH + gate * H + ij : nullptr;
     ld.stride[q] = 2 * GH;
     ld.shift[q] = 0;
@@ -732,8 +746,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #pragma unroll
     for (int q = 0; q < NXQ; ++q) {
       const int i = q * 128 + (wv - WPOLL - 1) * 64 + lane;
-      const int b = i / 80, c = i % 80;
-      const bool on = pfw && b < BC && 8 * c < a.Kin && b0 + b < a.B;
+      const int b = i / SXC, c = i % SXC;  // chunks c >= 80 of a row are its pad
+      const bool on = pfw && b < BC && c < XKMAX * 4 && 8 * c < a.Kin && b0 + b < a.B;
       xsrc[q] = on ? a.Xb + (long long)(b0 + b) * T * a.ldx + 8 * c : nullptr;
     }
   }
@@ -809,7 +823,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 
   auto matvec = [&]() {  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
     if (!mv) return;
-    const unsigned short* bp = shb + (lane & 15) * SHB + 8 * (lane >> 4);
+    const unsigned short* bp = shb + min(lane & 15, BC) * SHB + 8 * (lane >> 4);
     bf16x8 bv[KSMAX];
 #pragma unroll
     for (int ks = 0; ks < KSMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
@@ -829,7 +843,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     const int col = lane & 15;
     if (col < BC) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sgate[col * MT * 16 + tile * 16 + (lane >> 4) * 4 + i] = acc[0][i];
+      for (int i = 0; i < 4; ++i) sgate[col * SGS + tile * 16 + (lane >> 4) * 4 + i] = acc[0][i];
     }
   };
 
@@ -1012,7 +1026,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         const float gxa[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
-          hg[q] = bh[q] + sgate[cb * MT * 16 + q * J + cu];
+          hg[q] = bh[q] + sgate[cb * SGS + q * J + cu];
           gx[q] = gxa[q];
         }
         if constexpr (CELL == CELL_LSTM) {
@@ -1440,6 +1454,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   constexpr int KSRMAX = (4 * 20 + 31) / 32;   // MFMA K-steps over gate rows (3)
   constexpr int SDG = KSRMAX * 32 + 8;         // bf16 row stride of the dgh B image
   constexpr int WSPAN = MTWMAX * 16;           // output units per MFMA wave (80)
+  constexpr int WSP = WSPAN + 4;               // transpose row stride (floats): rows on distinct bank quads
   const int H = a.H, T = a.T, J = a.J, NG = a.NG;
   const int R = NGATE * J;
   const int ngroups = 2 * a.nchunk;
@@ -1460,8 +1475,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   unsigned short* sdgb = reinterpret_cast<unsigned short*>(smem);  // [16][SDG] bf16 dgh B image
   float* sdh = smem + 8 * SDG;                                      // [16][BC][J] gathered partials (rows >= NG stay 0)
-  float* wsc = sdh + ((16 * BC * J + 3) & ~3);                      // [4 waves][BC][WSPAN]
-  float* sop = wsc + 4 * BC * WSPAN;                                // [2][BC*32][8] per-step operands
+  float* wsc = sdh + ((16 * BC * J + 3) & ~3);                      // [4 waves][BC][WSP]
+  // per-step operands, [2 steps][2 planes][BC*32][4] with the planes 16 words apart in bank
+  // order: the prefetch commit (a cell's 8 operands on 8 consecutive lanes) and the cell's two
+  // 16-B reads are both conflict-free (a [cell][8] record was an 8-way commit conflict)
+  constexpr int SOPP = BC * 32 * 4 + 16;
+  float* sop = wsc + 4 * BC * WSP;
   for (int i = tid; i < 8 * SDG + 16 * BC * J; i += NT) smem[i] = 0.0f;
 
   // ---- W_hh^T tiles (waves 0-3): tile m = wv*MTWMAX + t, lane holds
@@ -1511,10 +1530,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   StepLoader<NQ> ld;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int i = tid - WPF * 64 + q * NPF;  // item = slot * (BC*J) + cell
-    const int slot = i / (BC * J), cell = i % (BC * J);
+    const int i = tid - WPF * 64 + q * NPF;  // item = cell * 8 + slot
+    const int slot = i & 7, cell = i >> 3;
     const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
-    const bool on = wv >= WPF && slot < 8;
+    const bool on = wv >= WPF && cell < BC * J;
     const bool valid = on && ib < a.B && ij < H;
     const float* p = nullptr;
     int stride = 2 * H, shift = 0;
@@ -1534,7 +1553,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.p[q] = p;
     ld.stride[q] = stride;
     ld.shift[q] = shift;
-    ld.dst[q] = on ? ((cell / J) * 32 + iu) * 8 + slot : -1;
+    ld.dst[q] = on ? (slot >> 2) * SOPP + ((cell / J) * 32 + iu) * 4 + (slot & 3) : -1;
   }
   if (wv >= WPF) ld.issue(d == 0 ? T - 1 : 0, T);
   __syncthreads();
@@ -1680,7 +1699,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   }
   if (wv >= WPF) {
     for (int s = 0; s < T; ++s) {
-      ld.commit(sop + (s & 1) * BC * 32 * 8);
+      ld.commit(sop + (s & 1) * 2 * SOPP);
       if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
       __syncthreads();  // B1
       __syncthreads();  // B2
@@ -1732,8 +1751,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         // two 16-B reads per lane: the 8-float operand record read as scalars is an 8-way
         // bank conflict (lanes 32 B apart); issued first, with the 16 partial reads behind
         // them in the same LDS round trip (sdh is zero before the first gather)
-        const float4 o0 = *reinterpret_cast<const float4*>(sop + (s & 1) * BC * 32 * 8 + tid * 8);
-        const float4 o1 = *reinterpret_cast<const float4*>(sop + (s & 1) * BC * 32 * 8 + tid * 8 + 4);
+        const float4 o0 = *reinterpret_cast<const float4*>(sop + (s & 1) * 2 * SOPP + tid * 4);
+        const float4 o1 = *reinterpret_cast<const float4*>(sop + (s & 1) * 2 * SOPP + SOPP + tid * 4);
         const float dh_rec = sum_partials16(sdh + cb * J + cu, BC * J);
         const float dout = o0.x + doutb;
         const float act[4] = {o0.y, o0.z, o0.w, o1.x};
@@ -1789,11 +1808,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     //      wave-private LDS to [b][unit], packed four units per 16-B store
     {
 #ifndef BWD_REG_PUBLISH  // transpose each tile through wave-private LDS: 2 store rounds (measured faster)
-      const unsigned short* bp = sdgb + (lane & 15) * SDG + 8 * (lane >> 4);
+      // rows >= BC of the dgh B image are zero: read row BC (broadcast, conflict-free B reads)
+      const unsigned short* bp = sdgb + min(lane & 15, BC) * SDG + 8 * (lane >> 4);
       bf16x8 bv[KSRMAX];
 #pragma unroll
       for (int ks = 0; ks < KSRMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
-      float* wsw = wsc + wv * BC * WSPAN;
+      float* wsw = wsc + wv * BC * WSP;
       const int col = lane & 15;
       // k-step-major over the wave's tiles: MTWMAX independent chains in flight
       f32x4 acc[MTWMAX];
@@ -1807,7 +1827,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       if (col < BC) {
 #pragma unroll
         for (int t2 = 0; t2 < MTWMAX; ++t2)
-          *reinterpret_cast<f32x4*>(wsw + col * WSPAN + t2 * 16 + 4 * (lane >> 4)) = acc[t2];
+          *reinterpret_cast<f32x4*>(wsw + col * WSP + t2 * 16 + 4 * (lane >> 4)) = acc[t2];
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
@@ -1819,7 +1839,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         const int e = e0 + lane;
         const int bb = e / (WSPAN / 4), k = wv * WSPAN + 4 * (e % (WSPAN / 4));
         if ((NQW % 64 == 0 || e < NQW) && k < H) {
-          const float4 v = *reinterpret_cast<const float4*>(wsw + bb * WSPAN + (k - wv * WSPAN));
+          const float4 v = *reinterpret_cast<const float4*>(wsw + bb * WSP + (k - wv * WSPAN));
           const unsigned r0 = pack24(v.x), r1 = pack24(v.y), r2 = pack24(v.z), r3 = pack24(v.w);
           const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
           const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules
@@ -2008,8 +2028,9 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) 
     p.smem_bwd_mf = 2 * 16 * SDG + sizeof(float) * (NG * BC * J + 3 + BC * HMAX + 2 * BC * J * 8);
     p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= (FWD_NPW == 3 ? 5 : FWD_NPW == 2 ? 6 : 7);
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
-    p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((16 * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16) + 2 * BC * 32 * 8);
-    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * MT * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
+    p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((16 * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16 + 4) +
+                                                    2 * 2 * (BC * 32 * 4 + 16));
+    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + 2 * BC * 32 * 4) + 2 * BC * PKU;
     return true;
   }
   return false;
@@ -2284,8 +2305,9 @@ DL4SS_API int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf
   a.bih = b_ih;
   a.Kin = Kin; a.ldx = ldx; a.ldw = ldw;
   const int grid = (int)(groups * p.NG);
-  const int nxq = (p.BC * 80 + 127) / 128;
-  const size_t smem = (p.smem_fwd_pk + 15) / 16 * 16 + (XRING * nxq * 128 * 8 + SXB) * sizeof(unsigned short);
+  const int nxq = (p.BC * SXC + 127) / 128;
+  // + 256: the ring starts at the next 256-B boundary of the LDS address (bank order of its rows)
+  const size_t smem = p.smem_fwd_pk + 256 + (XRING * nxq * 128 * 8 + SXZ_SLACK + SXB) * sizeof(unsigned short);
   return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, true, true, p.BC, a, grid, smem, st)
                            : dispatch<CELL_GRU>(true, true, true, p.BC, a, grid, smem, st);
 }
