@@ -330,17 +330,25 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
   }
 }
 
-// PIT selection: per utterance, lowest-index permutation minimising sum_k C[k][perm k]
+// PIT selection: per utterance, lowest-index permutation minimising sum_k C[k][perm k].  One
+// wave per utterance: lane l sums the block partials l, l + 64, ... in order, then a fixed
+// butterfly tree over the lanes (deterministic; one thread walking all nblk partials serially
+// took ~12 us at C2)
 template <int K>
-__global__ void pit_select_kernel(const float* __restrict__ part, int B, int nblk, int* __restrict__ perm) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+__global__ __launch_bounds__(64) void pit_select_kernel(const float* __restrict__ part, int B, int nblk,
+                                                        int* __restrict__ perm) {
+  const int b = blockIdx.x, lane = threadIdx.x;
   float C[K * K];
 #pragma unroll
   for (int i = 0; i < K * K; ++i) C[i] = 0.f;
-  for (int blk = 0; blk < nblk; ++blk)
+  for (int blk = lane; blk < nblk; blk += 64)
 #pragma unroll
     for (int i = 0; i < K * K; ++i) C[i] += part[((long long)b * nblk + blk) * (K * K + 1) + i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) C[i] += __shfl_xor(C[i], off);
+  if (lane != 0) return;
   int best = 0;
   float bc = 0.f;
   for (int p = 0; p < Perms<K>::N; ++p) {
@@ -510,7 +518,7 @@ int attn_common(int pass, int crm, int B, int K, int T, int F, int E, const floa
 DL4SS_API int dl4ss_pit_select(const float* part_loss, int B, int K, int nblk, int* perm, void* stream) {
   DL4SS_REQUIRE(part_loss && perm && B > 0 && K >= 1 && K <= 3);
   hipStream_t st = as_stream(stream);
-  dim3 grid(cdiv(B, 64)), blk(64);
+  dim3 grid(B), blk(64);
   if (K == 1) hipLaunchKernelGGL(pit_select_kernel<1>, grid, blk, 0, st, part_loss, B, nblk, perm);
   if (K == 2) hipLaunchKernelGGL(pit_select_kernel<2>, grid, blk, 0, st, part_loss, B, nblk, perm);
   if (K == 3) hipLaunchKernelGGL(pit_select_kernel<3>, grid, blk, 0, st, part_loss, B, nblk, perm);

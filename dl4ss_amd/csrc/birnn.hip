@@ -38,6 +38,7 @@
 // re-checks it against CUs x occupancy (launch_resident).
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include "common.h"
 
 namespace {
@@ -233,7 +234,6 @@ struct StepLoader {
 // rounded up, rows past B, the pad items of the last piece) read a global zero line.
 typedef __attribute__((address_space(3))) void lds_void_t;
 __device__ __attribute__((aligned(64))) const unsigned g_xzero_line[16] = {0};
-constexpr int XRING = 4;  // step buffers: x(s+1) consumed while x(s+2), x(s+3) are in flight
 
 // Poll the granules src[off[g]] (off < 0: nothing to read) until every tag == tag;
 // returns false on timeout.  Offsets are computed once per launch by the caller;
@@ -534,9 +534,16 @@ constexpr int XKMAX = 2 * HMAX / 32;  // fused input projection: k-steps of 32 (
 // group; at 80 chunks every row started on bank 0, a 4-way conflict, tools/lds_banks.py)
 constexpr int SXC = XKMAX * 4 + 2;    // 16-B chunks per row
 constexpr int SXB = SXC * 8;
-// the one zero row of the fused projection's B reads sits after the ring at the bank offset
-// row BC of a ring buffer would have (so it, too, is conflict-free against rows 0..BC-1)
-constexpr int SXZ_SLACK = 128;        // bf16
+// Fused projection in blocks: one MFMA's 16 B-columns are SPB = 16 / BC consecutive steps x BC
+// batch rows, so a tile's projection of a whole block of SPB steps is ONE XK-long MFMA chain
+// (a quarter of a per-step form's MFMAs at BC = 4); the chain of block k+1 is split into SPB
+// parts, one per step of block k.  The layer-input rows sit in a ring of 3 blocks of step slots
+// (slot stride XBUF + 16 BC bf16: the 16 columns' rows on distinct bank quads,
+// tools/lds_banks.py), DMA'd two blocks ahead of use.
+__host__ __device__ constexpr int xw_spb(int bc) { return 16 / bc; }
+__host__ __device__ constexpr int xw_nxq(int bc) { return (bc * SXC + 127) / 128; }
+__host__ __device__ constexpr int xw_slot(int bc) { return xw_nxq(bc) * 128 * 8 + 16 * bc; }  // bf16
+__host__ __device__ constexpr int xw_ring_bf16(int bc) { return 3 * xw_spb(bc) * xw_slot(bc); }
 constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
@@ -553,6 +560,9 @@ static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
 // s_sleep units (64 clocks) a polling wave waits before its first sweep of a step: the own
 // workgroup's granules (every consumer gathers its own publish too) cannot land before the
 // cell / matvec phase that follows the barrier, so earlier sweeps only load the L2
+#ifndef XW_MAP
+#define XW_MAP 0  // fused projection tile -> wave map (see rnn_fwd_pk_kernel)
+#endif
 #ifndef FWD_POLL_DELAY
 #define FWD_POLL_DELAY 0
 #endif
@@ -636,16 +646,20 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   // reads are conflict-free, tools/lds_banks.py)
   unsigned short* shb = reinterpret_cast<unsigned short*>(smem);
   float* sgate = smem + 8 * SHB;                                                        // [BC][SGS]
-  float* sin = sgate + BC * SGS;                                                        // [2][BC*32][4]
-  unsigned short* spub = reinterpret_cast<unsigned short*>(sin + 2 * BC * 32 * 4);      // [BC][PKU]
-  // XW: XRING step buffers of the layer-input rows ([BC][SXB] bf16 + the pad items of the last
-  // DMA piece) and one zero row (the B-image rows >= BC), 16-B aligned
+  // per-step input projections [NSIN][BC*32][4]: double buffered, or with XW two blocks of SPB steps
+  constexpr int SPB = xw_spb(BC);
+  constexpr int NSIN = XW ? 2 * SPB : 2;
+  float* sin = sgate + BC * SGS;
+  unsigned short* spub = reinterpret_cast<unsigned short*>(sin + NSIN * BC * 32 * 4);   // [BC][PKU]
+  // XW: the ring of 3 * SPB step slots of the layer-input rows ([BC][SXB] bf16 + the pad items of
+  // the last DMA piece), 256-B aligned (the bank order of its rows)
   static_assert(!XW || FWD_NPW == 2, "the fused projection's DMA pieces assume two prefetch waves of 64 lanes");
-  constexpr int NXQ = XW ? (BC * SXC + 127) / 128 : 1;  // DMA pieces per prefetch wave and step
-  constexpr int XBUF = NXQ * 128 * 8;                    // bf16 per step buffer (a multiple of 256 B)
+  static_assert(16 % BC == 0, "a block fills the MFMA's 16 B-columns");
+  constexpr int NXQ = xw_nxq(BC);       // DMA pieces per prefetch wave and step
+  constexpr int XSL = xw_slot(BC);      // bf16 per step slot
+  constexpr int NSLOT = 3 * SPB;
   unsigned short* sxb = reinterpret_cast<unsigned short*>(
       (reinterpret_cast<uintptr_t>(spub + BC * PKU) + 255) & ~static_cast<uintptr_t>(255));
-  unsigned short* sxz = sxb + XRING * XBUF + (BC * SXB) % SXZ_SLACK;  // [SXB] zeros
 
   // ---- W_hh tile of this wave as bf16 A fragments: lane holds A[row tile*16 + (lane&15)][k]
   bf16x8 afrag[KSMAX];
@@ -664,38 +678,58 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   }
   for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;
   for (int i = tid; i < BC * PKU; i += NT) spub[i] = 0;
-  if (XW)
-    for (int i = tid; i < SXB / 2; i += NT) reinterpret_cast<unsigned*>(sxz)[i] = 0u;
 
-  // ---- XW: W_ih tile of this wave (the same gate rows as its W_hh tile) as bf16 A fragments,
-  //      A[row tile*16 + (lane&15)][k = ks*32 + 8(lane>>4) + j], k >= Kin zero; and the b_ih of
-  //      the lane's four output rows 4(lane>>4) + i
-  bf16x8 wfrag[XW ? XK : 1];
-  float bir[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (XW) {
-    const int rl = tile * 16 + (lane & 15);
-    const int q = rl / J, u = rl % J;
-    const bool rv = mv && rl < R && j0 + u < H;
-    const unsigned short* wrow = a.Wihb + ((long long)d * GH + q * H + j0 + u) * a.ldw;
-    // one 16-B load per fragment (rows 16-B aligned: ldw % 8 == 0); the chunk holding k = Kin
-    // element by element, chunks past it zero
+  // ---- XW: the fused projection runs off the cell waves, on waves 4-7 (their slack: the free
+  //      prefetch wave 6, the DMA / tile-4 wave 5, and the polling waves between B2 and the first
+  //      granule that can land): tile 0 on wave 6, tile 1 on wave 5 (one each: their branch also
+  //      holds wave 5's matvec fragments), tiles 2 + 2i on wave 4 and 3 + 2i on wave 7 (two each).
+  //      Per tile, bf16 A fragments of its W_ih rows, A[row t*16 + (lane&15)][k = ks*32 +
+  //      8(lane>>4) + j] (k >= Kin zero), and the b_ih of the lane's four output rows 4(lane>>4) + i;
+  //      loaded inside the roles that use them (dead elsewhere: no register pressure on the cell
+  //      waves).  Tile counts per role are compile-time (IC<1> / IC<2>) so unused slots stay dead.
+  constexpr int XWT = 2;
+  int xt[XWT];
+#if XW_MAP == 0  // second tiles on the polling waves
+  xt[0] = !XW ? -1 : wv == 6 ? 0 : wv == 5 ? 1 : wv == WPOLL ? 2 : wv == 7 ? 3 : -1;
+  xt[1] = (XW && (wv == WPOLL || wv == 7) && xt[0] + 2 < MT) ? xt[0] + 2 : -1;
+#else  // second tiles on the prefetch waves (6 first)
+  xt[0] = !XW ? -1 : wv == 6 ? 0 : wv == 5 ? 1 : wv == WPOLL ? 2 : wv == 7 ? 3 : -1;
+  xt[1] = (XW && (wv == 6 || wv == 5) && xt[0] + 4 < MT) ? xt[0] + 4 : -1;
+#endif
+  if (xt[0] >= MT) xt[0] = -1;
+  bf16x8 wfr[XWT][XW ? XK : 1];
+  float bir[XWT][4];
+  f32x4 xacc[XWT];
+  auto load_w = [&](auto ntl) {
+    constexpr int NTL = decltype(ntl)::value;
 #pragma unroll
-    for (int ks = 0; ks < XK; ++ks) {
-      const int k0 = ks * 32 + 8 * (lane >> 4);
-      if (rv && k0 + 8 <= a.Kin) {
-        wfrag[ks] = *reinterpret_cast<const bf16x8*>(wrow + k0);
-      } else {
+    for (int i = 0; i < NTL; ++i) {
+      const int t = xt[i];
+      const int rl = t * 16 + (lane & 15);
+      const int q = rl / J, u = rl % J;
+      const bool rv = t >= 0 && rl < R && j0 + u < H;
+      const unsigned short* wrow = a.Wihb + ((long long)d * GH + q * H + j0 + u) * a.ldw;
+      // one 16-B load per fragment (rows 16-B aligned: ldw % 8 == 0); the chunk holding k = Kin
+      // element by element, chunks past it zero
 #pragma unroll
-        for (int j = 0; j < 8; ++j) wfrag[ks][j] = (short)((rv && k0 + j < a.Kin) ? wrow[k0 + j] : 0);
+      for (int ks = 0; ks < XK; ++ks) {
+        const int k0 = ks * 32 + 8 * (lane >> 4);
+        if (rv && k0 + 8 <= a.Kin) {
+          wfr[i][ks] = *reinterpret_cast<const bf16x8*>(wrow + k0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wfr[i][ks][j] = (short)((rv && k0 + j < a.Kin) ? wrow[k0 + j] : 0);
+        }
       }
-    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rr = tile * 16 + 4 * (lane >> 4) + i;
-      const int qq = rr / J, uu = rr % J;
-      bir[i] = (mv && rr < R && j0 + uu < H) ? a.bih[(long long)d * GH + qq * H + j0 + uu] : 0.0f;
+      for (int e = 0; e < 4; ++e) {
+        const int rr = t * 16 + 4 * (lane >> 4) + e;
+        const int qq = rr / J, uu = rr % J;
+        bir[i][e] = (t >= 0 && rr < R && j0 + uu < H) ? a.bih[(long long)d * GH + qq * H + j0 + uu] : 0.0f;
+      }
+      xacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  }
+  };
 
   // ---- cell lanes (waves 0-3): row cb = tid / 32, unit cu = tid % 32 (< J)
   const int cb = tid >> 5, cu = tid & 31;
@@ -751,30 +785,34 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       xsrc[q] = on ? a.Xb + (long long)(b0 + b) * T * a.ldx + 8 * c : nullptr;
     }
   }
-  // DMA of step u's rows into ring buffer u % XRING (prefetch waves only)
+  // DMA of step u's rows into ring slot u % NSLOT (prefetch waves only)
   auto xdma = [&](int u) {
     const long long toff = (long long)(d == 0 ? u : T - 1 - u) * a.ldx;
-    unsigned short* dst = sxb + (u % XRING) * XBUF + (wv - WPOLL - 1) * 64 * 8;
+    unsigned short* dst = sxb + (u % NSLOT) * XSL + (wv - WPOLL - 1) * 64 * 8;
 #pragma unroll
     for (int q = 0; q < NXQ; ++q) {
       const void* src = xsrc[q] ? (const void*)(xsrc[q] + toff) : (const void*)g_xzero_line;
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(dst + q * 128 * 8), 16, 0, 0);
     }
   };
-  // wait until step u's pieces landed; those of the `ahead` later steps issued after them (when
-  // < T) may stay in flight
-  auto xwait = [&](int u, int ahead) {
-    const int later = min(T - 1 - u, ahead);
-    if (later >= 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NXQ) : "memory");
-    else if (later == 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NXQ) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // wait until at most `n` steps' pieces (the latest issued) are still in flight (n <= SPB)
+  auto xwait = [&](int n) {
+    static_assert(!XW || SPB * NXQ <= 63, "vmcnt range");
+#define XW_WAIT(k) \
+  case k:          \
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((k) * NXQ <= 63 ? (k) * NXQ : 63) : "memory"); break;
+    switch (n) {
+      XW_WAIT(0) XW_WAIT(1) XW_WAIT(2) XW_WAIT(3) XW_WAIT(4) XW_WAIT(5) XW_WAIT(6) XW_WAIT(7) XW_WAIT(8)
+      XW_WAIT(9) XW_WAIT(10) XW_WAIT(11) XW_WAIT(12) XW_WAIT(13) XW_WAIT(14) XW_WAIT(15)
+      default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(16 * NXQ <= 63 ? 16 * NXQ : 63) : "memory");
+    }
+#undef XW_WAIT
   };
   if (XW && pfw) {
-    for (int u = 0; u < min(T, XRING - 1); ++u) xdma(u);
-    xwait(0, XRING - 2);
+    // blocks 0-2 in flight; blocks 0 and 1 must land before the first barrier (block 0's chain
+    // runs before the loop, block 1's first part at step 0)
+    for (int u = 0; u < min(T, NSLOT); ++u) xdma(u);
+    xwait(max(0, min(T, NSLOT) - 2 * SPB));
   } else if (!XW && pfw) {
     ld.issue(d == 0 ? 0 : T - 1, T);
   }
@@ -782,44 +820,66 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
   STAMP_DECL
 
-  // XW: G[b][rows of this tile] of the step whose inputs sit in B image `buf` -> sin[sb]:
-  // x W_ih^T as one accumulator chain over the k-steps in order, then + b_ih (the separate
-  // GEMM's arithmetic: gemm_gl's k-loop and bias epilogue)
-  auto xproj = [&](int buf, int sb) {
-    if (!mv) return;
-    const unsigned short* bp = ((lane & 15) < BC ? sxb + buf * XBUF + (lane & 15) * SXB : sxz) + 8 * (lane >> 4);
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    // k-steps past Kin multiply zero fragments (exact); the B reads of batch i+1 are issued
-    // before the MFMAs of batch i, so the chain waits on MFMA latency, not on LDS round trips
-    constexpr int XB = 5, NB = (XK + XB - 1) / XB;
-    bf16x8 cur[XB], nxt[XB];
+  // XW: G of block kb (steps kb*SPB .. +SPB-1) for this wave's tiles' rows: x W_ih^T as one
+  // accumulator chain over the k-steps in order, then + b_ih (the separate GEMM's arithmetic:
+  // gemm_gl's k-loop and bias epilogue, bitwise).  xpart runs part j of it, the k-steps
+  // [j PK, (j+1) PK) (the B fragments, shared by the wave's tiles, read once; every index
+  // compile-time through the unrolled part switch); xfinal adds b_ih and writes the block's G to
+  // sin.  B column n = o * BC + b: step kb*SPB + o, batch row b.
+  constexpr int PK = XW ? (XK + SPB - 1) / SPB : 1;
+  auto xpart = [&](auto ntl, int kb, int j) {
+    constexpr int NTL = decltype(ntl)::value;
+    if (xt[0] < 0) return;
+    const int n = lane & 15;
+    const unsigned short* bp = sxb + ((kb % 3) * SPB + n / BC) * XSL + (n % BC) * SXB + 8 * (lane >> 4);
 #pragma unroll
-    for (int i = 0; i < XB; ++i) cur[i] = i < XK ? *reinterpret_cast<const bf16x8*>(bp + i * 32) : bf16x8{};
+    for (int jj = 0; jj < SPB; ++jj) {
+      if (jj != j || jj * PK >= XK) continue;
+      bf16x8 bv[PK];
 #pragma unroll
-    for (int bb = 0; bb < NB; ++bb) {
-      if (bb + 1 < NB) {
+      for (int i = 0; i < PK; ++i)
+        if (jj * PK + i < XK) bv[i] = *reinterpret_cast<const bf16x8*>(bp + (jj * PK + i) * 32);
 #pragma unroll
-        for (int i = 0; i < XB; ++i) {
-          const int ks = (bb + 1) * XB + i;
-          nxt[i] = ks < XK ? *reinterpret_cast<const bf16x8*>(bp + ks * 32) : bf16x8{};
+      for (int i = 0; i < PK; ++i)
+        if (jj * PK + i < XK) {
+#pragma unroll
+          for (int t = 0; t < NTL; ++t)
+            if (xt[t] >= 0)
+              xacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[t][jj * PK + i], bv[i], xacc[t], 0, 0, 0);
         }
-      }
-#pragma unroll
-      for (int i = 0; i < XB; ++i)
-        if (bb * XB + i < XK) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfrag[bb * XB + i], cur[i], acc, 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < XB; ++i) cur[i] = nxt[i];
-    }
-    const int col = lane & 15;
-    if (col < BC) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rr = tile * 16 + 4 * (lane >> 4) + i;
-        if (rr < R) sin[sb * BC * 32 * 4 + (col * 32 + rr % J) * 4 + rr / J] = acc[i] + bir[i];
-      }
     }
   };
-  if (XW) xproj(0, 0);  // G of step 0 (its rows landed before the barrier above; the zero row too)
+  auto xfinal = [&](auto ntl, int kb) {
+    constexpr int NTL = decltype(ntl)::value;
+    const int n = lane & 15, o = n / BC, b = n % BC;
+    float* dst = sin + ((kb & 1) * SPB + o) * BC * 32 * 4;
+#pragma unroll
+    for (int i = 0; i < NTL; ++i) {
+      if (xt[i] < 0) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = xt[i] * 16 + 4 * (lane >> 4) + e;
+        if (rr < R) dst[(b * 32 + rr % J) * 4 + rr / J] = xacc[i][e] + bir[i][e];
+      }
+      xacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // this step's part of block kb + 1's chain (steps of block kb = s / SPB); the last part finishes it
+  auto xstep = [&](auto ntl, int s) {
+    const int kb = s / SPB + 1, j = s % SPB;
+    if (kb * SPB >= T) return;
+    xpart(ntl, kb, j);
+    if (j == SPB - 1 || s == T - 1) xfinal(ntl, kb);
+  };
+  // a role's start: its W_ih fragments, then block 0 whole (its rows landed before the barrier)
+  auto xstart = [&](auto ntl) {
+    load_w(ntl);
+    for (int j = 0; j < SPB; ++j) xpart(ntl, 0, j);
+    xfinal(ntl, 0);
+  };
+  // compile-time tile slots of the prefetch-wave and polling-wave roles
+  using XPF = std::integral_constant<int, XW_MAP == 0 ? 1 : 2>;
+  using XPL = std::integral_constant<int, XW_MAP == 0 ? 2 : 1>;
 
   auto matvec = [&]() {  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
     if (!mv) return;
@@ -851,6 +911,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifdef RNN_POLLPRIO  // experiment: the polling waves win SIMD arbitration
     __builtin_amdgcn_s_setprio(RNN_POLLPRIO);
 #endif
+    if (XW) xstart(XPL{});
     // ---- polling wave(s): 16-B unit idx = (b * NG + producer) * 4 + pair; lane holds
     //      units lane + 64 (g FWD_NPW + pwv) (idle lanes re-read unit 0: every load is
     //      unconditional, so the compiler can keep a sweep in flight behind a counted vmcnt)
@@ -981,11 +1042,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       STAMP(2)
       __syncthreads();  // B2
       STAMP(3)
+      // XW: this step's part of the next block's projection, before the next gather: no granule of
+      // step s+1 can land before the cell phase and publish that follow B2
+      if (XW) xstep(XPL{}, s);
     }
     STAMP_FLUSH
     return;
   }
   if (pfw) {
+    if (XW) xstart(XPF{});
     for (int s = 0; s < T; ++s) {
       if (!XW) {
         ld.commit(sin + (s & 1) * BC * 32 * 4);
@@ -995,15 +1060,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       __syncthreads();  // B1
       STAMP(1)
       matvec();
-      // XW: step s+1's rows landed before B2 (xproj(s+1) follows it); step s+2's may be in flight
-      if (XW && s + 1 < T) xwait(s + 1, 1);
+      // XW: at a block start the rows of the next block (consumed from this step on) landed
+      // before B2; the block after it may stay in flight
+      if (XW && s % SPB == 0) xwait(max(0, min(SPB, T - (s / SPB + 2) * SPB)));
       STAMP(2)
       __syncthreads();  // B2
       STAMP(3)
-      if (XW && s + 1 < T) xproj((s + 1) % XRING, (s + 1) & 1);
-      // step s+3's rows into buffer (s+3) % XRING, issued after B2 (off the matvec -> B2 path); that
-      // buffer was last read by xproj of step s-1, before B1(s-1)
-      if (XW && s + XRING - 1 < T) xdma(s + XRING - 1);
+      if (XW) xstep(XPF{}, s);
+      // step s + 3 SPB's rows into slot s % NSLOT, issued after B2 (off the matvec -> B2 path); that
+      // slot held step s's rows, last read by the chain of block s / SPB, which ended before B1(s)
+      if (XW && s + NSLOT < T) xdma(s + NSLOT);
       STAMP(4)
     }
     STAMP_FLUSH
@@ -1022,7 +1088,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       float hn = 0.0f, st[4] = {0.f, 0.f, 0.f, 0.f};
       if (cval) {
         float hg[NGATE], gx[NGATE];
-        const float4 g4 = *reinterpret_cast<const float4*>(sin + (s & 1) * BC * 32 * 4 + tid * 4);  // one 16-B read
+        const int sb = XW ? ((s / SPB) & 1) * SPB + s % SPB : (s & 1);
+        const float4 g4 = *reinterpret_cast<const float4*>(sin + sb * BC * 32 * 4 + tid * 4);  // one 16-B read
         const float gxa[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
@@ -1081,9 +1148,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       hst = hn;
     }
     STAMP(4)
-    // XW: step s+1's input projection while the hand-off of step s travels (its B image was
-    // committed before B2; sin[(s+1)&1] was last read by the cell phase of step s-1)
-    if (XW && s + 1 < T) xproj((s + 1) % XRING, (s + 1) & 1);
   }
   STAMP_FLUSH
 }
@@ -2305,9 +2369,10 @@ DL4SS_API int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf
   a.bih = b_ih;
   a.Kin = Kin; a.ldx = ldx; a.ldw = ldw;
   const int grid = (int)(groups * p.NG);
-  const int nxq = (p.BC * SXC + 127) / 128;
-  // + 256: the ring starts at the next 256-B boundary of the LDS address (bank order of its rows)
-  const size_t smem = p.smem_fwd_pk + 256 + (XRING * nxq * 128 * 8 + SXZ_SLACK + SXB) * sizeof(unsigned short);
+  // + the per-step projections of two blocks instead of two steps, + 256: the ring starts at the
+  // next 256-B boundary of the LDS address (bank order of its rows)
+  const size_t smem = p.smem_fwd_pk + sizeof(float) * (2 * xw_spb(p.BC) - 2) * p.BC * 32 * 4 + 256 +
+                      (size_t)xw_ring_bf16(p.BC) * sizeof(unsigned short);
   return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, true, true, p.BC, a, grid, smem, st)
                            : dispatch<CELL_GRU>(true, true, true, p.BC, a, grid, smem, st);
 }

@@ -35,6 +35,9 @@ from typing import Tuple
 import torch
 from torch import Tensor
 
+# every op computes and returns fp32 (the real ops reject other dtypes): the fake kernels say so
+F32 = dict(dtype=torch.float32)
+
 from . import _lib, autograd as ag, ops
 
 NS = "dl4ss"
@@ -54,7 +57,7 @@ def stft_mag(x: Tensor, log: bool = False) -> Tensor:
 @stft_mag.register_fake
 def _(x, log=False):
     N = x.shape[-1]
-    return x.new_empty(*x.shape[:-1], ops.n_frames(N), ops.F_BINS)
+    return x.new_empty(*x.shape[:-1], ops.n_frames(N), ops.F_BINS, **F32)
 
 
 @_op("stft_complex")
@@ -65,7 +68,7 @@ def stft_complex(x: Tensor, conj: bool = False) -> Tensor:
 @stft_complex.register_fake
 def _(x, conj=False):
     N = x.shape[-1]
-    return x.new_empty(*x.shape[:-1], ops.n_frames(N), ops.F_BINS, 2)
+    return x.new_empty(*x.shape[:-1], ops.n_frames(N), ops.F_BINS, 2, **F32)
 
 
 @_op("istft")
@@ -75,7 +78,7 @@ def istft(S: Tensor, conj: bool = False) -> Tensor:
 
 @istft.register_fake
 def _(S, conj=False):
-    return S.new_empty(*S.shape[:-3], ops.HOP * (S.shape[-3] - 1))
+    return S.new_empty(*S.shape[:-3], ops.HOP * (S.shape[-3] - 1), **F32)
 
 
 @_op("istft_apply")
@@ -95,7 +98,7 @@ def istft_apply(X: Tensor, aux: Tensor, k_per_mix: int, crm: bool, conj: bool = 
 
 @istft_apply.register_fake
 def _(X, aux, k_per_mix, crm, conj=False):
-    return X.new_empty(aux.shape[0], ops.HOP * (X.shape[-3] - 1))
+    return X.new_empty(aux.shape[0], ops.HOP * (X.shape[-3] - 1), **F32)
 
 
 @_op("mix_sources")
@@ -106,7 +109,7 @@ def mix_sources(raw: Tensor, gains: Tensor) -> Tuple[Tensor, Tensor]:
 @mix_sources.register_fake
 def _(raw, gains):
     B, K, N = raw.shape
-    return raw.new_empty(B, K, N), raw.new_empty(B, N)
+    return raw.new_empty(B, K, N, **F32), raw.new_empty(B, N, **F32)
 
 
 # --------------------------------------------------------------------------- BiRNN layer
@@ -120,8 +123,9 @@ def birnn_layer(x: Tensor, w_ih: Tensor, b_ih: Tensor, w_hh: Tensor, b_hh: Tenso
 @birnn_layer.register_fake
 def _(x, w_ih, b_ih, w_hh, b_hh, cell, H, precision):
     B, T, _ = x.shape
-    cs = x.new_empty(B, T, 2, H) if cell == "lstm" else x.new_empty(0)
-    return x.new_empty(B, T, 2 * H), x.new_empty(B, T, 2 * H), x.new_empty(B, T, 2, 4 * H), cs
+    cs = x.new_empty(B, T, 2, H, **F32) if cell == "lstm" else x.new_empty(0, **F32)
+    return (x.new_empty(B, T, 2 * H, **F32), x.new_empty(B, T, 2 * H, **F32), x.new_empty(B, T, 2, 4 * H, **F32),
+            cs)
 
 
 @_op("birnn_layer_bwd")
@@ -135,13 +139,15 @@ def birnn_layer_bwd(dout: Tensor, x: Tensor, w_ih: Tensor, w_hh: Tensor, hprev: 
 @birnn_layer_bwd.register_fake
 def _(dout, x, w_ih, w_hh, hprev, act, cs, cell, H, precision, need_dx):
     ng = 2 * (4 if cell == "lstm" else 3) * H
-    return (torch.empty_like(x) if need_dx else x.new_empty(0), torch.empty_like(w_ih), x.new_empty(ng),
-            torch.empty_like(w_hh), x.new_empty(ng))
+    return (torch.empty_like(x, **F32) if need_dx else x.new_empty(0, **F32), torch.empty_like(w_ih, **F32),
+            x.new_empty(ng, **F32), torch.empty_like(w_hh, **F32), x.new_empty(ng, **F32))
 
 
 def _birnn_setup(ctx, inputs, output):
     x, w_ih, b_ih, w_hh, b_hh, cell, H, precision = inputs
     _, hprev, act, cs = output
+    # saved state for the backward, not values a loss may depend on (their gradients would be dropped)
+    ctx.mark_non_differentiable(hprev, act, cs)
     ctx.save_for_backward(x, w_ih, w_hh, hprev, act, cs)
     ctx.meta = (cell, H, precision)
 
@@ -170,7 +176,7 @@ def linear_tanh(x2d: Tensor, w: Tensor, b: Tensor, precision: str) -> Tensor:
 
 @linear_tanh.register_fake
 def _(x2d, w, b, precision):
-    return x2d.new_empty(x2d.shape[0], w.shape[0])
+    return x2d.new_empty(x2d.shape[0], w.shape[0], **F32)
 
 
 @_op("linear_tanh_bwd")
@@ -182,7 +188,8 @@ def linear_tanh_bwd(dv: Tensor, x2d: Tensor, w: Tensor, v: Tensor, precision: st
 
 @linear_tanh_bwd.register_fake
 def _(dv, x2d, w, v, precision, need_dx):
-    return (torch.empty_like(x2d) if need_dx else x2d.new_empty(0)), torch.empty_like(w), w.new_empty(w.shape[0])
+    return ((torch.empty_like(x2d, **F32) if need_dx else x2d.new_empty(0, **F32)), torch.empty_like(w, **F32),
+            w.new_empty(w.shape[0], **F32))
 
 
 def _lt_setup(ctx, inputs, output):
@@ -209,7 +216,7 @@ def attention_dot(V: Tensor, q: Tensor, crm: bool) -> Tensor:
 @attention_dot.register_fake
 def _(V, q, crm):
     Bq, R, _ = V.shape
-    return V.new_empty(Bq, R, 2) if crm else V.new_empty(Bq, R)
+    return V.new_empty(Bq, R, 2, **F32) if crm else V.new_empty(Bq, R, **F32)
 
 
 @_op("attention_dot_bwd")
@@ -222,7 +229,7 @@ def attention_dot_bwd(dmask: Tensor, V: Tensor, q: Tensor, mask: Tensor, crm: bo
 
 @attention_dot_bwd.register_fake
 def _(dmask, V, q, mask, crm, need_dV):
-    return (torch.empty_like(V) if need_dV else V.new_empty(0)), torch.empty_like(q)
+    return (torch.empty_like(V, **F32) if need_dV else V.new_empty(0, **F32)), torch.empty_like(q, **F32)
 
 
 def _att_setup(ctx, inputs, output):
