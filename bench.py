@@ -45,12 +45,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_TAG = "r02_prof_e"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
+PMC_TAG = "r03_prof_a"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
 PMC_FILE = f"profiles/{PMC_TAG}_pmc.json"
 MFMA_FILE = f"profiles/{PMC_TAG}_mfma.json"
-# the in-step input-projection kernel as rocprofv3 names it (its MFMA-busy counter is looked up by it)
+# the step's GEMM kernels as rocprofv3 names them (MFMA-busy counters are looked up by name): the
+# Linear + tanh -> bf16 V (the largest in-step dense contraction) and the input projection (a GEMM
+# only on the unfused path: the step forms it inside the recurrence, dl4ss_birnn_fwd_xw)
+GEMM_GL_LINEAR = "gemm_gl_kernel<true, true, 2, false, Cfg<128, 2> >"
 GEMM_GL_INPROJ = "gemm_gl_kernel<true, true, 0, false, Cfg<128, 2> >"
-BW_FILE = "profiles/r02_bw_probe.jsonl"  # tools/bw_probe.hip: plain 16-B streaming ceilings on MI355X
+BW_FILE = "profiles/r03_bw_probe.jsonl"  # tools/bw_probe.hip: plain streaming ceilings on MI355X
 
 
 def stream_ceiling(kind):
@@ -494,31 +497,51 @@ def train_main(args, cfg, dev, world, rank, pg):
     T = tr.T
     stft_ms = stft_instep_graph(tr, B, K, N)
     stft_bytes = B * (K + 1) * (4 * N + 4 * T * 129)  # mag-only STFT of mixture + K sources
-    # input-projection GEMM of RNN layer 2 (M = B*T, N = 2 x gates x H, K = 600, bias fused), timed
-    # in isolation with the step's own kernel and operands: in bf16 mode gemm_gl.hip on the bf16 h
-    # the layer-1 recurrence wrote and the bf16 W_ih copy (the in-step launch), else gemm.hip fp32
+    # the MFMA rooflines, each GEMM timed in isolation with the step's own kernel on the step's
+    # operands (HIP events around 20 launches on the launch stream):
+    #  * Linear + tanh -> bf16 V (M = B*T, N = F*E = 6450, K = 600, bias + tanh fused): the largest
+    #    dense contraction inside the step;
+    #  * the layer-2 input projection (M = B*T, N = 2 x gates x H, K = 600 + bias) as a GEMM: the
+    #    north star's input-projection GEMM, which the step itself forms inside the recurrence kernel
+    #    (dl4ss_birnn_fwd_xw), so this is the unfused path's kernel, not an in-step launch.
     bih = net.cat_view("bias_ih", 1)
     ncol = bih.numel()
+    FE = 129 * 50
+
+    def time_gemm(fn, reps=20):
+        for _ in range(3):
+            fn()
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record()
+        for _ in range(reps):
+            fn()
+        g1.record()
+        torch.cuda.synchronize()
+        return g0.elapsed_time(g1) / reps
+
     if tr.fast:
+        hb = tr.outb[-1][:, :2 * net.H]
+        lin_ms = time_gemm(lambda: tr._gemm_fwd(hb, tr.wb_lin[:, :2 * net.H], net.view("mix.Linear.bias"), tr.Vb,
+                                                ops.EPI_TANH_BF16))
+        lin_kernel = GEMM_GL_LINEAR
+        lin_name = f"{lin_kernel} (bf16 operands, in-step Linear {B * T}x{FE}x600 + bias + tanh -> bf16 V)"
         xb, wb = tr.outb[0][:, :2 * net.H], tr.wb_ih[1][:, :2 * net.H]
-        run_gemm = lambda: tr._gemm_fwd(xb, wb, bih, tr.G)  # noqa: E731
-        gemm_kernel = GEMM_GL_INPROJ
-        gemm_name = f"{gemm_kernel} (bf16 operands, in-step layer-2 input projection {B * T}x{ncol}x600 + bias)"
+        inp_ms = time_gemm(lambda: tr._gemm_fwd(xb, wb, bih, tr.G))
+        inp_kernel = GEMM_GL_INPROJ
+        inp_name = (f"{inp_kernel} (bf16 operands, layer-2 input projection {B * T}x{ncol}x600 + bias as a GEMM; "
+                    "the step fuses it into rnn_fwd_pk_kernel)")
     else:
         x, wih = tr.out[0].view(B * T, -1), net.cat_view("weight_ih", 1)
-        run_gemm = lambda: ops.gemm(x, wih, transB=True, bias=bih, out=tr.G, precision=args.precision)  # noqa: E731
-        gemm_kernel = "gemm_kernel"
-        gemm_name = f"gemm_kernel (fp32 operands, layer-2 input projection {B * T}x{ncol}x600 + bias)"
-    for _ in range(3):
-        run_gemm()
-    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    g0.record()
-    for _ in range(20):
-        run_gemm()
-    g1.record()
-    torch.cuda.synchronize()
-    gemm_ms = g0.elapsed_time(g1) / 20
-    gemm_tf = 2.0 * B * T * 600 * ncol / (gemm_ms * 1e-3) / 1e12
+        hL = tr.out[-1].view(B * T, -1)
+        lin_ms = time_gemm(lambda: ops.gemm(hL, net.view("mix.Linear.weight"), transB=True,
+                                            bias=net.view("mix.Linear.bias"), epilogue=ops.EPI_TANH, out=tr.V,
+                                            precision=args.precision))
+        lin_kernel = inp_kernel = "gemm_kernel"
+        lin_name = f"gemm_kernel (fp32 operands, Linear {B * T}x{FE}x600 + bias + tanh)"
+        inp_ms = time_gemm(lambda: ops.gemm(x, wih, transB=True, bias=bih, out=tr.G, precision=args.precision))
+        inp_name = f"gemm_kernel (fp32 operands, layer-2 input projection {B * T}x{ncol}x600 + bias)"
+    lin_tf = 2.0 * B * T * 600 * FE / (lin_ms * 1e-3) / 1e12
+    gemm_tf = 2.0 * B * T * 600 * ncol / (inp_ms * 1e-3) / 1e12
     sa = None if args.no_stft_standalone else stft_standalone(dev, N, T)
 
     if rank == 0:
@@ -535,11 +558,14 @@ def train_main(args, cfg, dev, world, rank, pg):
                                 "frac": stft_gbs / HBM_PEAK_GBS,
                                 "traffic": pmc_traffic("stft_fwd_kernel", stft_grids(B, K, T)),
                                 "traffic_source": PMC_FILE, "launch_ms": stft_ms, "algorithmic_bytes": stft_bytes},
-            "roofline_mfma": {"bound": "mfma", "kernel": gemm_name,
-                              "achieved": gemm_tf, "peak": MFMA_PEAK[args.precision], "unit": "TFLOP/s",
-                              "frac": gemm_tf / MFMA_PEAK[args.precision], "launch_ms": gemm_ms,
-                              "mfma_busy": pmc_mfma_busy(gemm_kernel) if args.config == "C2" else None,
+            "roofline_mfma": {"bound": "mfma", "kernel": lin_name,
+                              "achieved": lin_tf, "peak": MFMA_PEAK[args.precision], "unit": "TFLOP/s",
+                              "frac": lin_tf / MFMA_PEAK[args.precision], "launch_ms": lin_ms,
+                              "mfma_busy": pmc_mfma_busy(lin_kernel) if args.config == "C2" else None,
                               "mfma_busy_source": MFMA_FILE},
+            "roofline_mfma_inproj": {"bound": "mfma", "kernel": inp_name,
+                                     "achieved": gemm_tf, "peak": MFMA_PEAK[args.precision], "unit": "TFLOP/s",
+                                     "frac": gemm_tf / MFMA_PEAK[args.precision], "launch_ms": inp_ms},
         })
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args, cfg)

@@ -561,7 +561,9 @@ static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
 // workgroup's granules (every consumer gathers its own publish too) cannot land before the
 // cell / matvec phase that follows the barrier, so earlier sweeps only load the L2
 #ifndef XW_MAP
-#define XW_MAP 0  // fused projection tile -> wave map (see rnn_fwd_pk_kernel)
+// fused projection tile -> wave map (rnn_fwd_pk_kernel): 1 = second tiles on the prefetch waves
+// (600-wide layers 351 us per launch, first layer 313 us), 0 = on the polling waves (364 / 327 us)
+#define XW_MAP 1
 #endif
 #ifndef FWD_POLL_DELAY
 #define FWD_POLL_DELAY 0

@@ -189,11 +189,11 @@ class SepTrainer:
         self.fast = precision == "bf16" and self.rnn_precision == "bf16"
         # Forward input projections x W_ih^T + b_ih formed inside the packed recurrence kernel
         # (dl4ss_birnn_fwd_xw) instead of a gemm_gl launch + a G buffer round trip; bitwise the same
-        # G (tests/test_rnn_xw_gpu.py).  DL4SS_RNN_XW: "l0" (default) the first layer only (129
-        # features, 5 MFMA k-steps per step: 341-352 us vs 333-338 + 30 us for recurrence + GEMM),
-        # "1" every layer (600-wide inputs, 20 k-steps: 423-435 vs 333-338 + 52 us -- the per-step
-        # MFMA chain of the cell waves outlasts the hand-off), "0" none.
-        xw = os.environ.get("DL4SS_RNN_XW", "l0")
+        # G (tests/test_rnn_xw_gpu.py).  Each tile's projection of a block of 16 / BC steps is one
+        # MFMA chain, split one part per step over the waves with slack (birnn.hip).  DL4SS_RNN_XW:
+        # "1" (default) every layer (C2, per launch: 600-wide layers 351 us vs 328 + 52 us for
+        # recurrence + GEMM, first layer 313 vs 328 + 30), "l0" the first layer only, "0" none.
+        xw = os.environ.get("DL4SS_RNN_XW", "1")
         if xw not in ("0", "1", "l0"):
             raise ValueError(f"DL4SS_RNN_XW={xw}: expected 0, 1 or l0")
         self.xw = self.fast and xw != "0"

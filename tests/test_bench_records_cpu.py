@@ -1,5 +1,5 @@
 """The bench line's roofline fields read committed profile records (no GPU): the PMC traffic of
-the STFT launch, the MFMA-busy counter of the in-step input-projection GEMM and the measured
+the STFT launch, the MFMA-busy counter of the in-step Linear GEMM and the measured
 streaming ceiling must all resolve, so a renamed kernel (rocprofv3 spells template arguments
 out) or a missing profile shows up here instead of as a silent null in BENCH_*.json."""
 import os
@@ -14,7 +14,7 @@ import bench  # noqa: E402
 def test_pmc_records_resolve():
     traffic = bench.pmc_traffic("stft_fwd_kernel", [bench.stft_grid_threads(4096, 251)])
     assert traffic is not None and 2.0e9 < traffic < 2.4e9  # algorithmic 2.116 GB per launch
-    busy = bench.pmc_mfma_busy(bench.GEMM_GL_INPROJ)
+    busy = bench.pmc_mfma_busy(bench.GEMM_GL_LINEAR)
     assert busy is not None and 0.0 < busy < 1.0
 
 

@@ -8,8 +8,11 @@
 //   r1w3      : 1 read : 3 writes (the STFT's complex + magnitude mix: 128 KB in, ~388 KB out
 //               per 4 s signal)
 //   copy_nt   : copy with non-temporal stores
+//   write_dword / r1w3_dword : the same streams with one dword per lane (256 B per wave-instruction)
+//   write_rows_dword : MI355X_MICROARCH.md's store form -- one dword per lane into random 2,304-B
+//               rows of a 302 MB table, each row swept by 9 consecutive wave-instructions
 // Each kernel moves ~2.1 GB per launch (the STFT probe's size); grid-stride over 16-B elements,
-// 256-thread workgroups, grid = 8 x 256 CUs x 4.  Build: hipcc --offload-arch=gfx950 -O3
+// 256-thread workgroups, grid = {2, 4, 8, 16} workgroups per CU.  Build: hipcc --offload-arch=gfx950 -O3
 // tools/bw_probe.hip -o tools/bw_probe ; run: ./tools/bw_probe  (one JSON line per kernel)
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -40,6 +43,37 @@ __global__ __launch_bounds__(256) void k_write(float4* __restrict__ b, long long
 
 __global__ __launch_bounds__(256) void k_copy(const float4* __restrict__ a, float4* __restrict__ b, long long n) {
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) b[i] = a[i];
+}
+
+// one dword per lane: 256 B per wave-instruction, the wave sweeping consecutive 256-B pieces
+__global__ __launch_bounds__(256) void k_write_dw(float* __restrict__ b, long long n) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) b[i] = (float)i;
+}
+
+// MI355X_MICROARCH.md's store measurement: one dword per lane into random 2,304-B rows of a table,
+// each row swept by consecutive wave-instructions (9 x 256 B), one wave per row at a time
+__global__ __launch_bounds__(256) void k_write_rows(float* __restrict__ b, long long nrows, int rows_per_wave,
+                                                   unsigned seed) {
+  const int lane = threadIdx.x & 63;
+  const long long w = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  for (int r = 0; r < rows_per_wave; ++r) {
+    unsigned h = (unsigned)(w * rows_per_wave + r) * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+    float* row = b + (long long)(h % (unsigned)nrows) * 576;  // 2,304 B
+#pragma unroll
+    for (int c = 0; c < 9; ++c) row[c * 64 + lane] = (float)c;
+  }
+}
+
+// r1w3 with dword-per-lane accesses (the same bytes as k_r1w3)
+__global__ __launch_bounds__(256) void k_r1w3_dw(const float* __restrict__ a, float* __restrict__ b,
+                                                 float* __restrict__ c, float* __restrict__ d, long long n) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float v = a[i];
+    b[i] = v;
+    c[i] = -v;
+    d[i] = v * v;
+  }
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -86,23 +120,32 @@ int main() {
   CK(hipMemset(a, 0, bytes_stream));
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  for (int mult : {4, 8, 16}) {
+  for (int mult : {2, 4, 8, 16}) {
     const dim3 grid(cus * mult), blk(256);
     const int it = 20;
-    struct R { const char* name; int streams; float ms; };
-    R rs[5] = {
-        {"read", 1, time_ms([&] { hipLaunchKernelGGL(k_read, grid, blk, 0, 0, a, n, sink); }, it)},
-        {"write", 1, time_ms([&] { hipLaunchKernelGGL(k_write, grid, blk, 0, 0, b, n); }, it)},
-        {"copy", 2, time_ms([&] { hipLaunchKernelGGL(k_copy, grid, blk, 0, 0, a, b, n); }, it)},
-        {"copy_nt", 2, time_ms([&] { hipLaunchKernelGGL(k_copy_nt, grid, blk, 0, 0, (const f32x4*)a, (f32x4*)b, n); }, it)},
-        {"r1w3", 4, time_ms([&] { hipLaunchKernelGGL(k_r1w3, grid, blk, 0, 0, a, b, c, d, n); }, it)},
+    const long long nrows = (302LL << 20) / 2304;  // a 302 MB table (beyond the 256 MB Infinity Cache)
+    const int rpw = 64;
+    const long long rows_bytes = (long long)cus * mult * 4 * rpw * 2304;
+    struct R { const char* name; double bytes; float ms; };
+    R rs[8] = {
+        {"read", 1.0 * bytes_stream, time_ms([&] { hipLaunchKernelGGL(k_read, grid, blk, 0, 0, a, n, sink); }, it)},
+        {"write", 1.0 * bytes_stream, time_ms([&] { hipLaunchKernelGGL(k_write, grid, blk, 0, 0, b, n); }, it)},
+        {"write_dword", 1.0 * bytes_stream,
+         time_ms([&] { hipLaunchKernelGGL(k_write_dw, grid, blk, 0, 0, (float*)b, 4 * n); }, it)},
+        {"write_rows_dword", 1.0 * rows_bytes,
+         time_ms([&] { hipLaunchKernelGGL(k_write_rows, grid, blk, 0, 0, (float*)c, nrows, rpw, 12345u); }, it)},
+        {"copy", 2.0 * bytes_stream, time_ms([&] { hipLaunchKernelGGL(k_copy, grid, blk, 0, 0, a, b, n); }, it)},
+        {"copy_nt", 2.0 * bytes_stream, time_ms([&] { hipLaunchKernelGGL(k_copy_nt, grid, blk, 0, 0, (const f32x4*)a, (f32x4*)b, n); }, it)},
+        {"r1w3", 4.0 * bytes_stream, time_ms([&] { hipLaunchKernelGGL(k_r1w3, grid, blk, 0, 0, a, b, c, d, n); }, it)},
+        {"r1w3_dword", 4.0 * bytes_stream,
+         time_ms([&] { hipLaunchKernelGGL(k_r1w3_dw, grid, blk, 0, 0, (const float*)a, (float*)b, (float*)c, (float*)d, 4 * n); }, it)},
     };
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());
     for (const R& r : rs) {
-      const double gbs = (double)r.streams * bytes_stream / (r.ms * 1e-3) / 1e9;
-      printf("{\"kernel\": \"%s\", \"wg_per_cu\": %d, \"bytes\": %lld, \"ms\": %.4f, \"GB/s\": %.1f, \"frac_8TBs\": %.3f}\n",
-             r.name, mult, (long long)r.streams * bytes_stream, r.ms, gbs, gbs / 8000.0);
+      const double gbs = r.bytes / (r.ms * 1e-3) / 1e9;
+      printf("{\"kernel\": \"%s\", \"wg_per_cu\": %d, \"bytes\": %.0f, \"ms\": %.4f, \"GB/s\": %.1f, \"frac_8TBs\": %.3f}\n",
+             r.name, mult, r.bytes, r.ms, gbs, gbs / 8000.0);
     }
   }
   return 0;
