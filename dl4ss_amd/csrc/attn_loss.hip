@@ -330,6 +330,174 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
   }
 }
 
+// The bf16-V magnitude path (the throughput step): V stays bf16 in LDS (25.6 KB per 256-row tile
+// instead of 51 KB fp32: ~3 resident blocks per CU instead of 2), each lane's |X| / target loads
+// are issued with the tile's V loads (not after the staging barrier), and dq is accumulated per
+// lane in registers over its own rows (dq[k][e] += dl_k V[e], in the same loop that forms dPre,
+// written as bf16 in place over the lane's V row) and reduced once per block (wave butterflies,
+// then waves in order: deterministic) -- instead of a 256-long serial FMA chain per dq element
+// on 100 threads per tile.  Logits, masks, costs and dPre are the fp32 arithmetic of
+// attn_kernel in the same order; only dq's summation order differs.
+template <int E, int K, bool GRAD>
+__global__ __launch_bounds__(NT) void attn_vb_kernel(AttnArgs a) {
+  static_assert(E % 2 == 0, "bf16 pairs");
+  constexpr int EP = E / 2;
+  __shared__ __attribute__((aligned(16))) unsigned sv[TILE * EP];  // bf16 pairs (e, e+1) of each row
+  __shared__ float sq[K * E];
+  __shared__ float sred[NT / 64][K * K + 1];
+  __shared__ float sdq[GRAD ? NT / 64 * K * E : 1];
+
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < K * E; i += NT) sq[i] = a.q[(long long)b * K * E + i];
+  const int per = (a.rows_per_b + a.nblk - 1) / a.nblk;
+  const int rbeg = blockIdx.x * per;
+  const int rend = min(a.rows_per_b, rbeg + per);
+  int pm[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) pm[k] = a.perm ? a.perm[b * K + k] : k;
+  float cost[K * K + 1];
+#pragma unroll
+  for (int i = 0; i < K * K + 1; ++i) cost[i] = 0.f;
+  float dq[GRAD ? K * E : 1];
+#pragma unroll
+  for (int i = 0; i < (GRAD ? K * E : 1); ++i) dq[i] = 0.f;
+
+  for (int r0 = rbeg; r0 < rend; r0 += TILE) {
+    const int nr = min(TILE, rend - r0);
+    const int r = tid, row = r0 + r;
+    const bool own = r < nr;
+    // this lane's |X| and targets, issued with the tile's V loads
+    float x = 0.f, y[K];
+    if (own) {
+      x = a.X[(long long)b * a.xs + row];
+#pragma unroll
+      for (int k = 0; k < K; ++k) y[k] = a.Y[(long long)b * a.ys + (long long)k * a.yks + row];
+    }
+    __syncthreads();  // previous tile fully consumed (and sq visible on the first pass)
+    {
+      const unsigned* src = reinterpret_cast<const unsigned*>(a.Vb + ((long long)b * a.rows_per_b + r0) * E);
+      const int n2 = nr * EP;
+      constexpr int NW = (TILE * EP + NT - 1) / NT;
+      unsigned w[NW];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int i = tid + q * NT;
+        w[q] = i < n2 ? src[i] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int i = tid + q * NT;
+        if (i < n2) sv[i] = w[q];
+      }
+    }
+    __syncthreads();
+    if (own) {
+      unsigned* v = sv + r * EP;
+      float lg[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) lg[k] = 0.f;
+#pragma unroll
+      for (int e2 = 0; e2 < EP; ++e2) {
+        const unsigned wv = v[e2];
+        const float vx = __uint_as_float(wv << 16), vy = __uint_as_float(wv & 0xFFFF0000u);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          lg[k] = fmaf(vx, sq[k * E + 2 * e2], lg[k]);
+          lg[k] = fmaf(vy, sq[k * E + 2 * e2 + 1], lg[k]);
+        }
+      }
+      float m[K], msum = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        m[k] = sigmoidf_(lg[k]);
+        msum += m[k];
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const float dd = m[k] * x - y[j];
+          cost[k * K + j] = fmaf(dd, dd, cost[k * K + j]);
+        }
+      const float ds = msum - 1.0f;
+      cost[K * K] = fmaf(ds, ds, cost[K * K]);
+      if (a.mask_out || a.pred_out) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const long long o = ((long long)b * K + k) * a.rows_per_b + row;
+          if (a.mask_out) a.mask_out[o] = m[k];
+          if (a.pred_out) a.pred_out[o] = m[k] * x;
+        }
+      }
+      if constexpr (GRAD) {
+        float dl[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          float yp = y[0];
+#pragma unroll
+          for (int j = 1; j < K; ++j) yp = pm[k] == j ? y[j] : yp;
+          const float dm = 2.f * a.s1 * (m[k] * x - yp) * x + 2.f * a.s2 * ds;
+          dl[k] = dm * m[k] * (1.f - m[k]);
+        }
+        // dV[e] = sum_k dl_k q_k[e]; dPre = dV (1 - V^2) as bf16 in place; dq_k[e] += dl_k V[e]
+#pragma unroll
+        for (int e2 = 0; e2 < EP; ++e2) {
+          const unsigned wv = v[e2];
+          const float vx = __uint_as_float(wv << 16), vy = __uint_as_float(wv & 0xFFFF0000u);
+          float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            g0 = fmaf(dl[k], sq[k * E + 2 * e2], g0);
+            g1 = fmaf(dl[k], sq[k * E + 2 * e2 + 1], g1);
+            dq[k * E + 2 * e2] = fmaf(dl[k], vx, dq[k * E + 2 * e2]);
+            dq[k * E + 2 * e2 + 1] = fmaf(dl[k], vy, dq[k * E + 2 * e2 + 1]);
+          }
+          __hip_bfloat162 o2 = __float22bfloat162_rn(make_float2(g0 * (1.f - vx * vx), g1 * (1.f - vy * vy)));
+          v[e2] = *reinterpret_cast<unsigned*>(&o2);
+        }
+      }
+    }
+    if constexpr (GRAD) {
+      // bf16 dPre for the Linear's backward GEMMs: pair i of the tile (row r0 + i / EP) as one 4-B
+      // store into row (b*T + t) of the padded bf16 matrix; the tile spans at most 3 frames
+      // (TILE < 2F + 1), so t, f come from the tile's first row by compares, not divisions
+      __syncthreads();
+      const int t0 = r0 / a.F, f0 = r0 - t0 * a.F;
+      for (int i = tid; i < nr * EP; i += NT) {
+        const int rl = i / EP, e2 = i - rl * EP;
+        int f = f0 + rl, t = t0;
+        if (f >= a.F) { f -= a.F; ++t; }
+        if (f >= a.F) { f -= a.F; ++t; }
+        a.dPreB[(((long long)b * a.T + t) * a.ldpb >> 1) + (long long)f * EP + e2] = sv[i];
+      }
+    }
+  }
+
+  // ---- block reductions (fixed order: wave butterflies, then waves 0..3)
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < K * K + 1; ++i) {
+    const float s = wave_sum(cost[i]);
+    if (lane == 0) sred[wave][i] = s;
+  }
+  if constexpr (GRAD) {
+#pragma unroll
+    for (int i = 0; i < K * E; ++i) {
+      const float s = wave_sum(dq[i]);
+      if (lane == 0) sdq[wave * K * E + i] = s;
+    }
+  }
+  __syncthreads();
+  float* pl = a.part_loss + ((long long)b * a.nblk + blockIdx.x) * (K * K + 1);
+  if (tid < K * K + 1) pl[tid] = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
+  if constexpr (GRAD) {
+    float* pd = a.part_dq + ((long long)b * a.nblk + blockIdx.x) * K * E;
+    for (int j = tid; j < K * E; j += NT)
+      pd[j] = sdq[0 * K * E + j] + sdq[1 * K * E + j] + sdq[2 * K * E + j] + sdq[3 * K * E + j];
+  }
+}
+
 // PIT selection: per utterance, lowest-index permutation minimising sum_k C[k][perm k].  One
 // wave per utterance: lane l sums the block partials l, l + 64, ... in order, then a fixed
 // butterfly tree over the lanes (deterministic; one thread walking all nblk partials serially
@@ -417,6 +585,18 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
 template <int E, int K, bool CRM, bool VB>
 int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
   dim3 grid(a.nblk, a.B);
+#ifndef ATTN_V1
+  if constexpr (VB && !CRM) {  // the throughput step's bf16-V magnitude path
+    if (a.dPreB || !grad) {
+      if (grad)
+        hipLaunchKernelGGL((attn_vb_kernel<E, K, true>), grid, dim3(NT), 0, st, a);
+      else
+        hipLaunchKernelGGL((attn_vb_kernel<E, K, false>), grid, dim3(NT), 0, st, a);
+      DL4SS_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+#endif
   if (grad)
     hipLaunchKernelGGL((attn_kernel<E, K, CRM, true, VB>), grid, dim3(NT), 0, st, a);
   else

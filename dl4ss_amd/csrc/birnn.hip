@@ -557,19 +557,10 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 static_assert(FWD_MV_CHAINS >= 1 && FWD_MV_CHAINS <= 8, "FWD_MV_CHAINS: 1..KSMAX accumulator chains");
 static_assert(FWD_NPW >= 1 && FWD_NPW <= 3, "FWD_NPW: 1..3 polling waves");
 static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
-// s_sleep units (64 clocks) a polling wave waits before its first sweep of a step: the own
-// workgroup's granules (every consumer gathers its own publish too) cannot land before the
-// cell / matvec phase that follows the barrier, so earlier sweeps only load the L2
 #ifndef XW_MAP
 // fused projection tile -> wave map (rnn_fwd_pk_kernel): 1 = second tiles on the prefetch waves
 // (600-wide layers 351 us per launch, first layer 313 us), 0 = on the polling waves (364 / 327 us)
 #define XW_MAP 1
-#endif
-#ifndef FWD_POLL_DELAY
-#define FWD_POLL_DELAY 0
-#endif
-#ifndef BWD_POLL_DELAY
-#define BWD_POLL_DELAY 0
 #endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
@@ -617,9 +608,6 @@ __device__ __forceinline__ bool group_needs_write_through(const u64* place, int 
 template <int CELL, int BC, int XK = 0>  // XK > 0: fused input projection over XK k-steps of 32
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   constexpr bool XW = XK > 0;
-#ifdef RNN_PRIO  // experiment: the recurrence waves win SIMD arbitration over co-resident GEMM waves
-  __builtin_amdgcn_s_setprio(3);
-#endif
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
   constexpr int KSMAX = HMAX / 32;
   constexpr int SHB = KSMAX * 32 + 8;  // bf16 row stride of the B image (k >= H stays zero)
@@ -634,9 +622,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const int j0 = w * J;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
-#ifdef RNN_CELLPRIO  // experiment: the cell / publish waves (0-3) win SIMD arbitration over the polling waves
-  if (wv < 4) __builtin_amdgcn_s_setprio(RNN_CELLPRIO);
-#endif
   const int GH = NGATE * H;
   const int tile = wv < WPOLL ? wv : wv - 1;
   const bool mv = wv != WPOLL && tile < MT;
@@ -910,9 +895,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   };
 
   if (pollw) {
-#ifdef RNN_POLLPRIO  // experiment: the polling waves win SIMD arbitration
-    __builtin_amdgcn_s_setprio(RNN_POLLPRIO);
-#endif
     if (XW) xstart(XPL{});
     // ---- polling wave(s): 16-B unit idx = (b * NG + producer) * 4 + pair; lane holds
     //      units lane + 64 (g FWD_NPW + pwv) (idle lanes re-read unit 0: every load is
@@ -939,11 +921,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         // two sweeps in flight: the older one is merged while the newer one travels;
         // a pair is taken from the first sweep that shows both its tags.  One 16-B `sc1`
         // buffer load per granule pair; the empty asm with a memory clobber before each
-        // sweep keeps the loads inside the spin loop (POLL8: 8-B relaxed agent atomics).
-#ifndef POLL8
+        // sweep keeps the loads inside the spin loop (the round-1 8-B relaxed agent atomics were
+        // 13-16 % slower per step: DESIGN.md section 5).
         u32x4 v[GLK], qa[GLK], qb[GLK];
         unsigned done = 0;
-        if (FWD_POLL_DELAY > 0) __builtin_amdgcn_s_sleep(FWD_POLL_DELAY);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
@@ -977,56 +958,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
             return;
           }
         }
-#else
-        const u64* src = xg + (base >> 3);
-        u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
-        unsigned done = 0;
-#pragma unroll
-        for (int g = 0; g < GLK; ++g) {
-          alo[g] = get_granule(src + (loff[g] >> 3));
-          ahi[g] = get_granule(src + (loff[g] >> 3) + 1);
-        }
-        unsigned spins = 0;
-        while (true) {
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            blo[g] = get_granule(src + (loff[g] >> 3));
-            bhi[g] = get_granule(src + (loff[g] >> 3) + 1);
-          }
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            const bool m = ((unsigned)(alo[g] >> 48) == tag) & ((unsigned)(ahi[g] >> 48) == tag) & !((done >> g) & 1);
-            lo[g] = m ? alo[g] : lo[g];
-            hi[g] = m ? ahi[g] : hi[g];
-            done |= (unsigned)m << g;
-          }
-          if (done == (1u << GLK) - 1) break;
-#ifdef RNN_TRACE
-          if (spins == 0) TRACE(3, s);
-#endif
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            alo[g] = get_granule(src + (loff[g] >> 3));
-            ahi[g] = get_granule(src + (loff[g] >> 3) + 1);
-          }
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            const bool m = ((unsigned)(blo[g] >> 48) == tag) & ((unsigned)(bhi[g] >> 48) == tag) & !((done >> g) & 1);
-            lo[g] = m ? blo[g] : lo[g];
-            hi[g] = m ? bhi[g] : hi[g];
-            done |= (unsigned)m << g;
-          }
-          if (done == (1u << GLK) - 1) break;
-          if (++spins > a.spin_limit) {
-            atomicOr(a.status, 1);
-            return;
-          }
-        }
-        u32x4 v[GLK];
-#pragma unroll
-        for (int g = 0; g < GLK; ++g)
-          v[g] = u32x4{(unsigned)lo[g], (unsigned)(lo[g] >> 32), (unsigned)hi[g], (unsigned)(hi[g] >> 32)};
-#endif
 #pragma unroll
         for (int g = 0; g < GLK; ++g) {
           const u32x4 x = v[g];
@@ -1512,9 +1443,6 @@ __device__ __forceinline__ float unpack24(unsigned r) { return __uint_as_float(r
 
 template <int CELL, int BC>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
-#ifdef RNN_PRIO  // experiment: the recurrence waves win SIMD arbitration over co-resident GEMM waves
-  __builtin_amdgcn_s_setprio(3);
-#endif
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
   constexpr int MTWMAX = (HMAX / 16 + 3) / 4;  // MFMA unit tiles per wave (5)
   constexpr int KSRMAX = (4 * 20 + 31) / 32;   // MFMA K-steps over gate rows (3)
@@ -1531,9 +1459,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   const int j0 = w * J;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
-#ifdef RNN_CELLPRIO  // experiment: the cell / publish waves (0-3) win SIMD arbitration over the polling waves
-  if (wv < 4) __builtin_amdgcn_s_setprio(RNN_CELLPRIO);
-#endif
   const int GH = NGATE * H;
   const int AH = 4 * H;
   const int HG = ((H + 1) / 2 + 1) & ~1;  // granules per (producer, row), even: 16-B aligned rows
@@ -1627,9 +1552,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   STAMP_DECL
 
   if (wv >= WPOLL && wv < WPF) {
-#ifdef RNN_POLLPRIO
-    __builtin_amdgcn_s_setprio(RNN_POLLPRIO);
-#endif
     // ---- polling waves: 16-B unit idx = (producer * BC + b) * (J/4) + quad, wave pw
     //      takes the 64-unit blocks pw, pw + BWD_NPW, ...
     constexpr int GLK = (80 * BC + 64 * BWD_NPW - 1) / (64 * BWD_NPW);  // NG <= 16, J <= 20
@@ -1650,7 +1572,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       if (s > 0) {
         const unsigned tag = (unsigned)s & 0xFFFFu;
         if (wv == WPOLL) TRACE(2, s);
-#ifndef POLL8  // POLL8: the round-1 8-B atomic loads (A/B builds)
         // 16-B `sc1` buffer loads, one per granule pair (half the requests of the 8-B atomic
         // loads: BPTT 4800 -> 4153, forward 3302 -> 3111 cycles per step); the empty asm with a
         // memory clobber keeps every sweep inside the loop (the buffer intrinsic is a plain
@@ -1658,7 +1579,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         const int sb = ((s - 1) & 1) * 2 * copy_g * 8;  // the slot's hand-off copy (bytes)
         u32x4 q[GLK], qa[GLK], qb[GLK];
         unsigned done = 0;
-        if (BWD_POLL_DELAY > 0) __builtin_amdgcn_s_sleep(BWD_POLL_DELAY);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, sb + loff[g] * 8, 0, 16);
@@ -1698,59 +1618,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             *reinterpret_cast<float4*>(sdh + doff[g]) = v;  // 16-B aligned: J % 4 == 0
           }
         }
-#else
-        const u64* src = xg + ((s - 1) & 1) * 2 * copy_g;
-        u64 lo[GLK], hi[GLK], alo[GLK], ahi[GLK], blo[GLK], bhi[GLK];
-        unsigned done = 0;
-#pragma unroll
-        for (int g = 0; g < GLK; ++g) {
-          alo[g] = get_granule(src + loff[g]);
-          ahi[g] = get_granule(src + loff[g] + 1);
-        }
-        unsigned spins = 0;
-        while (true) {
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            blo[g] = get_granule(src + loff[g]);
-            bhi[g] = get_granule(src + loff[g] + 1);
-          }
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            const bool m = ((unsigned)(alo[g] >> 48) == tag) & ((unsigned)(ahi[g] >> 48) == tag) & !((done >> g) & 1);
-            lo[g] = m ? alo[g] : lo[g];
-            hi[g] = m ? ahi[g] : hi[g];
-            done |= (unsigned)m << g;
-          }
-          if (done == (1u << GLK) - 1) break;
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            alo[g] = get_granule(src + loff[g]);
-            ahi[g] = get_granule(src + loff[g] + 1);
-          }
-#pragma unroll
-          for (int g = 0; g < GLK; ++g) {
-            const bool m = ((unsigned)(blo[g] >> 48) == tag) & ((unsigned)(bhi[g] >> 48) == tag) & !((done >> g) & 1);
-            lo[g] = m ? blo[g] : lo[g];
-            hi[g] = m ? bhi[g] : hi[g];
-            done |= (unsigned)m << g;
-          }
-          if (done == (1u << GLK) - 1) break;
-          if (++spins > a.spin_limit) {
-            atomicOr(a.status, 2);
-            return;
-          }
-        }
-#pragma unroll
-        for (int g = 0; g < GLK; ++g) {
-          if (on[g]) {
-            const unsigned l0 = (unsigned)lo[g], l1 = (unsigned)(lo[g] >> 32);
-            const unsigned h0 = (unsigned)hi[g], h1 = (unsigned)(hi[g] >> 32);
-            const float4 v = make_float4(unpack24(l0 & 0xFFFFFFu), unpack24((l0 >> 24) | ((l1 & 0xFFFFu) << 8)),
-                                         unpack24(h0 & 0xFFFFFFu), unpack24((h0 >> 24) | ((h1 & 0xFFFFu) << 8)));
-            *reinterpret_cast<float4*>(sdh + doff[g]) = v;  // 16-B aligned: J % 4 == 0
-          }
-        }
-#endif
         if (wv == WPOLL) TRACE(1, s);
       }
       STAMP(0)
@@ -1873,7 +1740,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     // ---- D[k][b] = sum_r W[r][k] dgh[b][r] per 16-unit tile, transposed through
     //      wave-private LDS to [b][unit], packed four units per 16-B store
     {
-#ifndef BWD_REG_PUBLISH  // transpose each tile through wave-private LDS: 2 store rounds (measured faster)
       // rows >= BC of the dgh B image are zero: read row BC (broadcast, conflict-free B reads)
       const unsigned short* bp = sdgb + min(lane & 15, BC) * SDG + 8 * (lane >> 4);
       bf16x8 bv[KSRMAX];
@@ -1916,40 +1782,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         }
       }
       if (wv == 3) TRACE(0, s);
-#else
-      // the 16 x 16 accumulator lane holds 4 consecutive units 4(lane>>4) + i of batch column
-      // lane & 15: one packed quad, published straight from the registers (every tile's MFMA
-      // chain issued first, then the stores) -- no LDS round trip on the critical path
-      const unsigned short* bp = sdgb + (lane & 15) * SDG + 8 * (lane >> 4);
-      bf16x8 bv[KSRMAX];
-#pragma unroll
-      for (int ks = 0; ks < KSRMAX; ++ks) bv[ks] = *reinterpret_cast<const bf16x8*>(bp + ks * 32);
-      f32x4 acc[MTWMAX];
-#pragma unroll
-      for (int t2 = 0; t2 < MTWMAX; ++t2) acc[t2] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KSRMAX; ++ks)
-#pragma unroll
-        for (int t2 = 0; t2 < MTWMAX; ++t2)
-          acc[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t2][ks], bv[ks], acc[t2], 0, 0, 0);
-      STAMP(4)
-      const int col = lane & 15;
-      const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
-#pragma unroll
-      for (int t2 = 0; t2 < MTWMAX; ++t2) {
-        const int k = (wv * MTWMAX + t2) * 16 + 4 * (lane >> 4);
-        if (col < BC && k < H) {
-          const unsigned r0 = pack24(acc[t2][0]), r1 = pack24(acc[t2][1]), r2 = pack24(acc[t2][2]),
-                         r3 = pack24(acc[t2][3]);
-          const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
-          const int off = (((s & 1) * 2 * NG + w) * BC + col) * HG + (k >> 1);  // granules
-          if (wt)
-            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 16);  // sc1 write-through (group spans XCDs)
-          else
-            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);   // plain: stays in the group's L2
-        }
-      }
-#endif
     }
     store_dg();  // this step's dG / dGh, after the publish (off the critical path)
     STAMP(6)

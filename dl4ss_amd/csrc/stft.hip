@@ -28,13 +28,6 @@ constexpr int NBIN = NFFT / 2 + 1;  // 129
 constexpr int FPW = 16;             // frames per workgroup
 constexpr int SPAN = HOPL * FPW + NFFT;  // 2304 samples
 constexpr int YS = 17;              // padded row stride (complex) of the transpose
-#ifndef STFT_EMIT16
-// 1: the forward emits each tile's output range as 16-B granules (element -> (frame, bin) by
-// division, magnitudes staged in LDS): measured 8 % (complex + magnitude) and 16 %
-// (magnitude only) SLOWER at 4096 signals than the per-frame stores -- the kernel is
-// VALU-issue limited as much as store limited; kept as a knob (same arithmetic per element)
-#define STFT_EMIT16 0
-#endif
 
 enum { F_COMPLEX = 1, F_MAG = 2, F_LOGMAG = 4, F_CONJ = 8, F_APPLY_MAG = 16, F_APPLY_CRM = 32 };
 
@@ -215,78 +208,6 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
     const int sig = tile / tiles_per_sig;
     const int t0 = (tile - sig * tiles_per_sig) * FPT;
     const int nfr = min(FPT, T - t0);
-#if STFT_EMIT16
-    // split the pairs and emit the tile as 16-B stores: the tile's outputs are one
-    // contiguous range of the (signal, frame, bin) layout (nfr * 129 elements from
-    // g0), so thread i writes the i-th 16-B-aligned granule of that range (two complex
-    // bins, or four magnitudes) whatever the frame boundaries; the granules that
-    // straddle the range ends (shared with the neighbouring tiles) take element stores.
-    // With both outputs the complex pass stages the magnitudes in the consumed span
-    // buffer, and a second pass streams them out.
-    {
-      const long long g0 = ((long long)sig * T + t0) * NBIN;
-      const int n = nfr * NBIN;
-      float* sm = sx;
-      auto xval = [&](int e, float& m) -> float2 {
-        const int f = (int)((unsigned)e / (unsigned)NBIN);
-        const int k = e - f * NBIN;
-        const float2 zk = sz[(f >> 1) * NFFT + k];
-        const float2 zm = sz[(f >> 1) * NFFT + ((NFFT - k) & (NFFT - 1))];
-        float2 X = (f & 1) == 0 ? make_float2(zk.x + zm.x, zk.y - zm.y) : make_float2(zk.y + zm.y, zm.x - zk.x);
-        if (CONJ) X.y = -X.y;
-        // bin 128 (Z[128] pairs with itself, imaginary part exactly 0): |X| = |Re X|
-        m = k == NFFT / 2 ? fabsf(X.x) : __builtin_amdgcn_sqrtf(X.x * X.x + X.y * X.y);
-        if (LOG) m = __logf(m + 2.220446049250313e-16f);
-        return X;
-      };
-      if (WC) {
-        const long long h0 = g0 + (long long)((((uintptr_t)Xc) >> 3) & 1);  // element index in 16-B granules
-        const long long p0 = h0 >> 1;
-        const int npair = (int)(((h0 + n - 1) >> 1) - p0 + 1);
-        for (int i = tid; i < npair; i += 256) {
-          const int e0 = (int)(2 * (p0 + i) - h0);  // -1 for a head granule
-          float m0 = 0.f, m1 = 0.f;
-          const bool v0 = e0 >= 0, v1 = e0 + 1 < n;
-          const float2 X0 = xval(v0 ? e0 : 0, m0);
-          const float2 X1 = xval(v1 ? e0 + 1 : 0, m1);
-          if (v0 && v1) {
-            *reinterpret_cast<float4*>(Xc + g0 + e0) = make_float4(X0.x, X0.y, X1.x, X1.y);
-          } else {
-            if (v0) Xc[g0 + e0] = X0;
-            if (v1) Xc[g0 + e0 + 1] = X1;
-          }
-          if (WM) {
-            if (v0) sm[e0] = m0;
-            if (v1) sm[e0 + 1] = m1;
-          }
-        }
-      }
-      if (WM) {
-        if (WC) __syncthreads();
-        const long long h0 = g0 + (long long)((((uintptr_t)mag) >> 2) & 3);
-        const long long q0 = h0 >> 2;
-        const int nq = (int)(((h0 + n - 1) >> 2) - q0 + 1);
-        for (int i = tid; i < nq; i += 256) {
-          const int e0 = (int)(4 * (q0 + i) - h0);
-          float m[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int e = e0 + c;
-            const int ec = (e >= 0 && e < n) ? e : 0;
-            if (WC) m[c] = sm[ec];
-            else xval(ec, m[c]);
-          }
-          if (e0 >= 0 && e0 + 3 < n) {
-            *reinterpret_cast<float4*>(mag + g0 + e0) = make_float4(m[0], m[1], m[2], m[3]);
-          } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-              if (e0 + c >= 0 && e0 + c < n) mag[g0 + e0 + c] = m[c];
-          }
-        }
-      }
-    }
-#else
     // split the pairs and emit the tile: thread (parity, bin) = (tid >> 7, tid & 127)
     // writes bin k of frames 2 it + parity (waves 0-1 even frames, 2-3 odd: no
     // divergence); a wave stores 64 consecutive bins of one frame.  Bin 128 by 32
@@ -333,7 +254,6 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
         mag[row0 + f * NBIN + 128] = m;
       }
     }
-#endif
   }
 }
 
