@@ -32,6 +32,8 @@ SIGNATURES = {
     "dl4ss_gemm_bf16_gl_ws_bytes": [I, I, I, I, I],
     "dl4ss_gemm_gl_set_config": [I],
     "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
+    "dl4ss_gemm_bf16_gl_grouped_ws_bytes": [I, P, P, P, P],
+    "dl4ss_gemm_bf16_gl_grouped": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_fwd_xw": [I, I, I, I, P, I, LL, P, LL, P, P, P, P, P, P, P, P, P, P, LL, P, P, I],
     "dl4ss_birnn_fwd_xw_supported": [I, I, I, I, I],
@@ -72,7 +74,8 @@ SIGNATURES = {
 }
 # entry points that return a value rather than a hipError_t
 RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_colsum_bf16_part_bytes": ctypes.c_longlong,
-            "dl4ss_gemm_bf16_gl_ws_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
+            "dl4ss_gemm_bf16_gl_ws_bytes": ctypes.c_longlong,
+            "dl4ss_gemm_bf16_gl_grouped_ws_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
             "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None,
             "dl4ss_debug_set_place_force": None}
 

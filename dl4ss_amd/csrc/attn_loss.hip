@@ -330,26 +330,55 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
   }
 }
 
-// The bf16-V magnitude path (the throughput step): V stays bf16 in LDS (25.6 KB per 256-row tile
-// instead of 51 KB fp32: ~3 resident blocks per CU instead of 2), each lane's |X| / target loads
-// are issued with the tile's V loads (not after the staging barrier), and dq is accumulated per
-// lane in registers over its own rows (dq[k][e] += dl_k V[e], in the same loop that forms dPre,
-// written as bf16 in place over the lane's V row) and reduced once per block (wave butterflies,
-// then waves in order: deterministic) -- instead of a 256-long serial FMA chain per dq element
-// on 100 threads per tile.  Logits, masks, costs and dPre are the fp32 arithmetic of
-// attn_kernel in the same order; only dq's summation order differs.
+// The bf16-V magnitude path (the throughput step), one QUAD of lanes per (b,t,f) row.
+// attn_kernel gives each lane a whole row (E = 50 values: 100 logit FMAs, 100 dPre FMAs and a
+// 256-long serial dq chain per tile on 100 lanes: latency-bound at ~2.5 TB/s); a lane holding
+// all K*E dq sums in registers (221 VGPRs, 2 waves per SIMD) was slower still.  Here lane j of a
+// quad owns the row's bf16 pairs w = j, j+4, j+8, ... (7 of the 25 at E = 50), so a lane keeps
+// only its 14 q values and 14 dq sums per query in registers (~4 waves per SIMD): partial logits
+// over its pairs, the quad's sum by two DPP quad permutes (bitwise the same value in all four
+// lanes), then dl, the lane's dPre pairs (written back as bf16 over its own V words) and its dq
+// terms.  V reaches LDS by LDS-DMA (`global_load_lds_dwordx4`, no staging registers) from the 16-B
+// aligned word below the tile (the tile's first word sits `off` words into the LDS image); dPre leaves by coalesced 4-B stores whose
+// (t, f) destination changes only at frame boundaries (compares, no division).  Only the
+// logits' summation order differs from attn_kernel (quad partials instead of one serial chain);
+// dq is per-lane partials -> wave xor-shuffle tree -> waves 0..3 in order (deterministic).
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+}
+
+typedef __attribute__((address_space(3))) void attn_lds_void;
+__device__ __attribute__((aligned(16))) const unsigned g_attn_zero[4] = {0u, 0u, 0u, 0u};
+
 template <int E, int K, bool GRAD>
-__global__ __launch_bounds__(NT) void attn_vb_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(AttnArgs a) {
   static_assert(E % 2 == 0, "bf16 pairs");
-  constexpr int EP = E / 2;
-  __shared__ __attribute__((aligned(16))) unsigned sv[TILE * EP];  // bf16 pairs (e, e+1) of each row
-  __shared__ float sq[K * E];
+  constexpr int EP = E / 2;              // bf16 pairs per row
+  constexpr int NWL = (EP + 3) / 4;      // pairs per lane
+  constexpr int NQ = NT / 4;             // quads per block
+  constexpr int RPQ = TILE / NQ;         // rows per quad per tile
+  constexpr int NCH = (TILE * EP + 3) / 4 + 1;  // 16-B chunks of a tile, misaligned start included
+  constexpr int NCHP = (NCH + 63) / 64 * 64;     // whole 1-KB DMA instructions
+  __shared__ __attribute__((aligned(16))) unsigned sv[NCHP * 4];
   __shared__ float sred[NT / 64][K * K + 1];
   __shared__ float sdq[GRAD ? NT / 64 * K * E : 1];
 
   const int b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < K * E; i += NT) sq[i] = a.q[(long long)b * K * E + i];
+  const int j = tid & 3, qd = tid >> 2;
+  // this lane's q values (zero for the pair slots past EP)
+  float qv[K][NWL][2];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int i = 0; i < NWL; ++i) {
+      const int w = j + 4 * i;
+      qv[k][i][0] = w < EP ? a.q[((long long)b * K + k) * E + 2 * w] : 0.f;
+      qv[k][i][1] = w < EP ? a.q[((long long)b * K + k) * E + 2 * w + 1] : 0.f;
+    }
   const int per = (a.rows_per_b + a.nblk - 1) / a.nblk;
   const int rbeg = blockIdx.x * per;
   const int rend = min(a.rows_per_b, rbeg + per);
@@ -359,142 +388,171 @@ __global__ __launch_bounds__(NT) void attn_vb_kernel(AttnArgs a) {
   float cost[K * K + 1];
 #pragma unroll
   for (int i = 0; i < K * K + 1; ++i) cost[i] = 0.f;
-  float dq[GRAD ? K * E : 1];
+  float dq[GRAD ? K : 1][GRAD ? NWL : 1][2];
+  if constexpr (GRAD) {
 #pragma unroll
-  for (int i = 0; i < (GRAD ? K * E : 1); ++i) dq[i] = 0.f;
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int i = 0; i < NWL; ++i) dq[k][i][0] = dq[k][i][1] = 0.f;
+  }
+  const unsigned* Vw = reinterpret_cast<const unsigned*>(a.Vb);
+  const long long totw = (long long)a.B * a.rows_per_b * EP;
 
   for (int r0 = rbeg; r0 < rend; r0 += TILE) {
     const int nr = min(TILE, rend - r0);
-    const int r = tid, row = r0 + r;
-    const bool own = r < nr;
-    // this lane's |X| and targets, issued with the tile's V loads
-    float x = 0.f, y[K];
-    if (own) {
-      x = a.X[(long long)b * a.xs + row];
+    // issue this tile's loads: |X| and targets of the quad's rows, then V by 16-B chunks
+    float xr[RPQ], yr[RPQ][K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) y[k] = a.Y[(long long)b * a.ys + (long long)k * a.yks + row];
+    for (int s = 0; s < RPQ; ++s) {
+      const int r = qd + NQ * s;
+      const int row = r0 + (r < nr ? r : 0);
+      xr[s] = a.X[(long long)b * a.xs + row];
+#pragma unroll
+      for (int k = 0; k < K; ++k) yr[s][k] = a.Y[(long long)b * a.ys + (long long)k * a.yks + row];
     }
-    __syncthreads();  // previous tile fully consumed (and sq visible on the first pass)
-    {
-      const unsigned* src = reinterpret_cast<const unsigned*>(a.Vb + ((long long)b * a.rows_per_b + r0) * E);
-      const int n2 = nr * EP;
-      constexpr int NW = (TILE * EP + NT - 1) / NT;
-      unsigned w[NW];
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const int i = tid + q * NT;
-        w[q] = i < n2 ? src[i] : 0u;
-      }
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const int i = tid + q * NT;
-        if (i < n2) sv[i] = w[q];
-      }
+    const long long w0 = ((long long)b * a.rows_per_b + r0) * EP;
+    const int off = (int)(w0 & 3);
+    const long long wa = w0 - off;
+    const int nch = (off + nr * EP + 3) >> 2;
+    __syncthreads();  // the previous tile's rows and dPre copy-out are done with sv
+    // V by LDS-DMA: wave instruction p moves chunks 64p .. 64p + 63 (1 KB) into sv + 256p words
+    int tail = -1;
+    for (int p = wave; p * 64 < nch; p += NT / 64) {
+      const int c = p * 64 + lane;
+      const long long gw = wa + 4LL * c;
+      const bool whole = c < nch && gw + 4 <= totw;
+      if (c < nch && !whole) tail = c;
+      __builtin_amdgcn_global_load_lds(whole ? (const void*)(Vw + gw) : (const void*)g_attn_zero,
+                                       (attn_lds_void*)(sv + 256 * p), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tail >= 0) {  // the buffer's last chunk, partly past its end: the valid words by plain loads
+      const long long gw = wa + 4LL * tail;
+      for (int q = 0; q < 4 && gw + q < totw; ++q) sv[4 * tail + q] = Vw[gw + q];
     }
     __syncthreads();
-    if (own) {
-      unsigned* v = sv + r * EP;
-      float lg[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) lg[k] = 0.f;
+    for (int s = 0; s < RPQ; ++s) {
+      const int r = qd + NQ * s;
+      if (r < nr) {  // quad-uniform
+        const int row = r0 + r;
+        unsigned* v = sv + off + r * EP + j;
+        unsigned wv[NWL];
 #pragma unroll
-      for (int e2 = 0; e2 < EP; ++e2) {
-        const unsigned wv = v[e2];
-        const float vx = __uint_as_float(wv << 16), vy = __uint_as_float(wv & 0xFFFF0000u);
+        for (int i = 0; i < NWL; ++i) wv[i] = (j + 4 * i < EP) ? v[4 * i] : 0u;
+        float lg[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          lg[k] = fmaf(vx, sq[k * E + 2 * e2], lg[k]);
-          lg[k] = fmaf(vy, sq[k * E + 2 * e2 + 1], lg[k]);
-        }
-      }
-      float m[K], msum = 0.f;
+        for (int k = 0; k < K; ++k) lg[k] = 0.f;
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        m[k] = sigmoidf_(lg[k]);
-        msum += m[k];
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const float dd = m[k] * x - y[j];
-          cost[k * K + j] = fmaf(dd, dd, cost[k * K + j]);
-        }
-      const float ds = msum - 1.0f;
-      cost[K * K] = fmaf(ds, ds, cost[K * K]);
-      if (a.mask_out || a.pred_out) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const long long o = ((long long)b * K + k) * a.rows_per_b + row;
-          if (a.mask_out) a.mask_out[o] = m[k];
-          if (a.pred_out) a.pred_out[o] = m[k] * x;
-        }
-      }
-      if constexpr (GRAD) {
-        float dl[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float yp = y[0];
-#pragma unroll
-          for (int j = 1; j < K; ++j) yp = pm[k] == j ? y[j] : yp;
-          const float dm = 2.f * a.s1 * (m[k] * x - yp) * x + 2.f * a.s2 * ds;
-          dl[k] = dm * m[k] * (1.f - m[k]);
-        }
-        // dV[e] = sum_k dl_k q_k[e]; dPre = dV (1 - V^2) as bf16 in place; dq_k[e] += dl_k V[e]
-#pragma unroll
-        for (int e2 = 0; e2 < EP; ++e2) {
-          const unsigned wv = v[e2];
-          const float vx = __uint_as_float(wv << 16), vy = __uint_as_float(wv & 0xFFFF0000u);
-          float g0 = 0.f, g1 = 0.f;
+        for (int i = 0; i < NWL; ++i) {
+          const float vx = __uint_as_float(wv[i] << 16), vy = __uint_as_float(wv[i] & 0xFFFF0000u);
 #pragma unroll
           for (int k = 0; k < K; ++k) {
-            g0 = fmaf(dl[k], sq[k * E + 2 * e2], g0);
-            g1 = fmaf(dl[k], sq[k * E + 2 * e2 + 1], g1);
-            dq[k * E + 2 * e2] = fmaf(dl[k], vx, dq[k * E + 2 * e2]);
-            dq[k * E + 2 * e2 + 1] = fmaf(dl[k], vy, dq[k * E + 2 * e2 + 1]);
+            lg[k] = fmaf(vx, qv[k][i][0], lg[k]);
+            lg[k] = fmaf(vy, qv[k][i][1], lg[k]);
           }
-          __hip_bfloat162 o2 = __float22bfloat162_rn(make_float2(g0 * (1.f - vx * vx), g1 * (1.f - vy * vy)));
-          v[e2] = *reinterpret_cast<unsigned*>(&o2);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          lg[k] += quad_xor1(lg[k]);
+          lg[k] += quad_xor2(lg[k]);
+        }
+        const float x = xr[s];
+        float m[K], msum = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          m[k] = sigmoidf_(lg[k]);
+          msum += m[k];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int jj = 0; jj < K; ++jj) {
+            const float dd = m[k] * x - yr[s][jj];
+            cost[k * K + jj] = fmaf(dd, dd, cost[k * K + jj]);
+          }
+        const float ds = msum - 1.0f;
+        cost[K * K] = fmaf(ds, ds, cost[K * K]);
+        if ((a.mask_out || a.pred_out) && j == 0) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const long long o = ((long long)b * K + k) * a.rows_per_b + row;
+            if (a.mask_out) a.mask_out[o] = m[k];
+            if (a.pred_out) a.pred_out[o] = m[k] * x;
+          }
+        }
+        if constexpr (GRAD) {
+          float dl[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            float yp = yr[s][0];
+#pragma unroll
+            for (int jj = 1; jj < K; ++jj) yp = pm[k] == jj ? yr[s][jj] : yp;
+            const float dm = 2.f * a.s1 * (m[k] * x - yp) * x + 2.f * a.s2 * ds;
+            dl[k] = dm * m[k] * (1.f - m[k]);
+          }
+          // dV[e] = sum_k dl_k q_k[e]; dPre = dV (1 - V^2) as bf16 over the lane's own words;
+          // dq_k[e] += dl_k V[e]
+#pragma unroll
+          for (int i = 0; i < NWL; ++i) {
+            const float vx = __uint_as_float(wv[i] << 16), vy = __uint_as_float(wv[i] & 0xFFFF0000u);
+            float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              g0 = fmaf(dl[k], qv[k][i][0], g0);
+              g1 = fmaf(dl[k], qv[k][i][1], g1);
+              dq[k][i][0] = fmaf(dl[k], vx, dq[k][i][0]);
+              dq[k][i][1] = fmaf(dl[k], vy, dq[k][i][1]);
+            }
+            __hip_bfloat162 o2 = __float22bfloat162_rn(make_float2(g0 * (1.f - vx * vx), g1 * (1.f - vy * vy)));
+            if (j + 4 * i < EP) v[4 * i] = *reinterpret_cast<unsigned*>(&o2);
+          }
         }
       }
     }
     if constexpr (GRAD) {
-      // bf16 dPre for the Linear's backward GEMMs: pair i of the tile (row r0 + i / EP) as one 4-B
-      // store into row (b*T + t) of the padded bf16 matrix; the tile spans at most 3 frames
-      // (TILE < 2F + 1), so t, f come from the tile's first row by compares, not divisions
+      // bf16 dPre rows (b*T + t) of the padded matrix: word i of the tile belongs to frame
+      // t0 + (i >= ib1) + (i >= ib2) + ..., at word (r0 - t F) EP + i of that row
       __syncthreads();
-      const int t0 = r0 / a.F, f0 = r0 - t0 * a.F;
+      const int t0 = r0 / a.F;
+      const int ib1 = ((t0 + 1) * a.F - r0) * EP, fw = a.F * EP;
+      const long long rowb = (long long)b * a.T;
       for (int i = tid; i < nr * EP; i += NT) {
-        const int rl = i / EP, e2 = i - rl * EP;
-        int f = f0 + rl, t = t0;
-        if (f >= a.F) { f -= a.F; ++t; }
-        if (f >= a.F) { f -= a.F; ++t; }
-        a.dPreB[(((long long)b * a.T + t) * a.ldpb >> 1) + (long long)f * EP + e2] = sv[i];
+        int t = t0, ib = ib1;
+        while (i >= ib) { ++t; ib += fw; }
+        a.dPreB[((rowb + t) * a.ldpb >> 1) + (long long)(r0 - t * a.F) * EP + i] = sv[off + i];
       }
     }
   }
 
-  // ---- block reductions (fixed order: wave butterflies, then waves 0..3)
+  // ---- block reductions (fixed order: lane trees, then waves 0..3); costs from lane 0 of each quad
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < K * K + 1; ++i) {
-    const float s = wave_sum(cost[i]);
+    const float s = wave_sum(j == 0 ? cost[i] : 0.f);
     if (lane == 0) sred[wave][i] = s;
   }
   if constexpr (GRAD) {
 #pragma unroll
-    for (int i = 0; i < K * E; ++i) {
-      const float s = wave_sum(dq[i]);
-      if (lane == 0) sdq[wave * K * E + i] = s;
-    }
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int i = 0; i < NWL; ++i)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          float s = dq[k][i][c];
+#pragma unroll
+          for (int o = 4; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+          const int w = lane + 4 * i;  // lanes 0..3 hold the wave's sums of pairs j + 4i
+          if (lane < 4 && w < EP) sdq[(wave * K + k) * E + 2 * w + c] = s;
+        }
   }
   __syncthreads();
   float* pl = a.part_loss + ((long long)b * a.nblk + blockIdx.x) * (K * K + 1);
   if (tid < K * K + 1) pl[tid] = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
   if constexpr (GRAD) {
     float* pd = a.part_dq + ((long long)b * a.nblk + blockIdx.x) * K * E;
-    for (int j = tid; j < K * E; j += NT)
-      pd[j] = sdq[0 * K * E + j] + sdq[1 * K * E + j] + sdq[2 * K * E + j] + sdq[3 * K * E + j];
+    for (int i = tid; i < K * E; i += NT)
+      pd[i] = sdq[0 * K * E + i] + sdq[1 * K * E + i] + sdq[2 * K * E + i] + sdq[3 * K * E + i];
   }
 }
 
@@ -586,12 +644,12 @@ template <int E, int K, bool CRM, bool VB>
 int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
   dim3 grid(a.nblk, a.B);
 #ifndef ATTN_V1
-  if constexpr (VB && !CRM) {  // the throughput step's bf16-V magnitude path
-    if (a.dPreB || !grad) {
+  if constexpr (VB && !CRM) {  // the throughput step's bf16-V magnitude path (16-B aligned V)
+    if ((a.dPreB || !grad) && ((uintptr_t)a.Vb & 15) == 0) {
       if (grad)
-        hipLaunchKernelGGL((attn_vb_kernel<E, K, true>), grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((attn_q4_kernel<E, K, true>), grid, dim3(NT), 0, st, a);
       else
-        hipLaunchKernelGGL((attn_vb_kernel<E, K, false>), grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((attn_q4_kernel<E, K, false>), grid, dim3(NT), 0, st, a);
       DL4SS_CHECK_LAUNCH();
       return 0;
     }
@@ -628,9 +686,10 @@ int attn_common(int pass, int crm, int B, int K, int T, int F, int E, const floa
 }  // namespace
 
 DL4SS_API int dl4ss_attn_nblk(int T, int F) {
-  // DL4SS_ATTN_TILES tiles per block (default 3: 4 -> 3 measured 137 -> 126 us per step for
-  // COST + GRAD + finalize at C2, tools/ab_attn.sh)
-  static const int tpb = std::getenv("DL4SS_ATTN_TILES") ? std::atoi(std::getenv("DL4SS_ATTN_TILES")) : 3;
+  // DL4SS_ATTN_TILES tiles per block (default 4: with attn_q4_kernel at C2 -- 32 x 32 blocks, one
+  // round at 4 resident per CU -- GRAD 65.8 / 66.7 / 71.1 us at 4 / 2 / 3 tiles, COST + PIT select
+  // 25.2 / 25.8 / 27.1 us, profiles/r03_attn_q4.jsonl; round 2's attn_kernel preferred 3)
+  static const int tpb = std::getenv("DL4SS_ATTN_TILES") ? std::atoi(std::getenv("DL4SS_ATTN_TILES")) : 4;
   const int rows = T * F;
   int nblk = (rows + tpb * TILE - 1) / (tpb * TILE);
   return nblk < 1 ? 1 : nblk;

@@ -125,42 +125,16 @@ __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int k
   }
 }
 
+// One BM x 128 output tile of C (or of split-K slab `slab`, SPLIT) over k in [kbeg, kbeg + kspan):
+// the k-loop and the epilogue of gemm_gl_kernel and gemm_gl_grouped_kernel.  smem: the kernel's
+// one LDS array (CF::STG * CF::STAGE bf16).
 template <bool A_KC, bool B_KC, int EPI, bool SPLIT, class CF>
-__global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) void gemm_gl_kernel(
-    int M, int N, int K, const unsigned short* __restrict__ A, long long lda, const unsigned short* __restrict__ B,
-    long long ldb, float* __restrict__ C, long long ldc, const float* __restrict__ bias, float beta, int k_per_split,
-    int grid_m, int grid_n, long long sa, long long sb, long long sc, float* __restrict__ part) {
-  constexpr int BM = CF::BM, STG = CF::STG, IMG_A = CF::IMG_A, STAGE = CF::STAGE;
-  // one LDS array (a second __shared__ object can make hipcc drain vmcnt before every ds_read)
-  __shared__ __attribute__((aligned(16))) unsigned short smem[STG * STAGE];
-  // XCD-major order over the WHOLE grid (tiles x batch members x k-splits): workgroups are
-  // dealt round-robin over the 8 XCDs in dispatch order (x fastest, then y, then z; speed
-  // only, never correctness), so the dispatch index L is remapped bijectively to R, giving
-  // each XCD a contiguous range of R: mostly one (split, member) and 8 M-tiles x all N-tiles
-  // groups of it, whose operand panels then stay in that XCD's L2
-  const int ntiles = grid_m * grid_n;
-  const int nwg = gridDim.x * gridDim.y * gridDim.z;
-  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  const int xcd = L % 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int R = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
-  const int zsplit = R / (ntiles * (int)gridDim.y);
-  const int ymem = (R / ntiles) % (int)gridDim.y;
-  const int tile = R % ntiles;
-  A += ymem * sa;
-  B += ymem * sb;
-  C += ymem * sc;
-  constexpr int GROUP = 8;
-  const int gsize = GROUP * grid_n;
-  const int first_m = (tile / gsize) * GROUP;
-  const int gm_here = min(grid_m - first_m, GROUP);
-  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = zsplit * k_per_split;
-  const int kend = min(K, kbeg + k_per_split);
-  if (kbeg >= kend) return;
-  const int kspan = kend - kbeg;
+__device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, const unsigned short* __restrict__ A,
+                                        long long lda, const unsigned short* __restrict__ B, long long ldb,
+                                        float* __restrict__ C, long long ldc, const float* __restrict__ bias,
+                                        float beta, int m0, int n0, int kbeg, int kspan, float* __restrict__ slab) {
+  constexpr int STG = CF::STG, IMG_A = CF::IMG_A, STAGE = CF::STAGE;
   const int nk = (kspan + BK - 1) / BK;
-
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
@@ -245,7 +219,7 @@ __global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) vo
     bv.w = col + 3 < N ? bias[col + 3] : 0.f;
   }
   // split-K slab of (batch member y, split z): part[y][z][M][N]
-  float* out = SPLIT ? part + ((long long)ymem * gridDim.z + zsplit) * M * N : C;
+  float* out = SPLIT ? slab : C;
   const long long ldo = SPLIT ? N : ldc;
   const bool vec_c = (ldo % 4 == 0) && ((((uintptr_t)out) & 15) == 0) && col + 4 <= N;
 #pragma unroll
@@ -306,6 +280,43 @@ __global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) vo
       }
     }
   }
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool SPLIT, class CF>
+__global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) void gemm_gl_kernel(
+    int M, int N, int K, const unsigned short* __restrict__ A, long long lda, const unsigned short* __restrict__ B,
+    long long ldb, float* __restrict__ C, long long ldc, const float* __restrict__ bias, float beta, int k_per_split,
+    int grid_m, int grid_n, long long sa, long long sb, long long sc, float* __restrict__ part) {
+  constexpr int BM = CF::BM;
+  // one LDS array (a second __shared__ object can make hipcc drain vmcnt before every ds_read)
+  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
+  // XCD-major order over the WHOLE grid (tiles x batch members x k-splits): workgroups are
+  // dealt round-robin over the 8 XCDs in dispatch order (x fastest, then y, then z; speed
+  // only, never correctness), so the dispatch index L is remapped bijectively to R, giving
+  // each XCD a contiguous range of R: mostly one (split, member) and 8 M-tiles x all N-tiles
+  // groups of it, whose operand panels then stay in that XCD's L2
+  const int ntiles = grid_m * grid_n;
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = L % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int R = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
+  const int zsplit = R / (ntiles * (int)gridDim.y);
+  const int ymem = (R / ntiles) % (int)gridDim.y;
+  const int tile = R % ntiles;
+  A += ymem * sa;
+  B += ymem * sb;
+  C += ymem * sc;
+  constexpr int GROUP = 8;
+  const int gsize = GROUP * grid_n;
+  const int first_m = (tile / gsize) * GROUP;
+  const int gm_here = min(grid_m - first_m, GROUP);
+  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = zsplit * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  if (kbeg >= kend) return;
+  gl_tile<A_KC, B_KC, EPI, SPLIT, CF>(smem, M, N, A, lda, B, ldb, C, ldc, bias, beta, m0, n0, kbeg, kend - kbeg,
+                                      SPLIT ? part + ((long long)ymem * gridDim.z + zsplit) * M * N : nullptr);
 }
 
 // One epilogue store of four consecutive columns col .. col + 3 of output row `row` (row < M
@@ -615,6 +626,124 @@ __global__ __launch_bounds__(256) void gemm_gl_reduce_kernel(int M, int N, int S
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Grouped launch: up to GMAXP independent GEMMs (the step's weight gradients: dW_lin and every
+// layer's dW_ih / dW_hh, each its own M x N x K and split-K factor) as ONE grid.  One by one they
+// under-fill the chip (dW_ih: 95 tiles x 4 splits; dW_hh: 2 x 30 tiles x 8 splits) and each pays its
+// own ramp and tail; together they are ~3,000 workgroups of equal-length k-ranges.  The
+// workgroup -> (problem, split, tile) map, the per-tile arithmetic and the slabs are those of the
+// single launches, so every gradient is bitwise what gemm_gl_kernel + gemm_gl_reduce_kernel
+// produce with the same split factors.  Problem parameters travel in the kernel arguments and are
+// selected by unrolled compile-time indices (wave-uniform scalar code, no dynamic indexing into
+// the argument segment).
+// ---------------------------------------------------------------------------------------------
+constexpr int GMAXP = 16;
+struct GlProb {
+  const unsigned short* A;
+  const unsigned short* B;
+  float* C;
+  float* part;  // split-K slabs [nsplit][M][N] (null when nsplit == 1)
+  long long lda, ldb, ldc;
+  float beta;
+  int M, N, K, gm, gn, nsplit, kps;
+  int wg0;  // first workgroup (in the XCD-remapped order) of this problem
+  int u0;   // first reduce unit (gemm_gl_grouped_reduce_kernel)
+  int vec;  // reduce with 16-B accesses (N % 4 == 0, ldc % 4 == 0, C 16-B aligned)
+};
+struct GlGroup {
+  int n, total_wg, total_units;
+  GlProb p[GMAXP];
+};
+
+template <bool A_KC, bool B_KC, class CF>
+__global__ __launch_bounds__(CF::NT, 2) void gemm_gl_grouped_kernel(GlGroup g) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
+  // problems by DISPATCH order (so every problem's workgroups are dealt over all 8 XCDs: an
+  // XCD-contiguous remap of the whole grid handed one XCD nearly all of dW_lin's long k-ranges,
+  // 616 vs ~330 us), then the XCD-major remap inside the problem (L0 = its first dispatch index;
+  // L - L0 with equal residues mod 8 share an XCD, whatever L0 % 8 is)
+  const int L = blockIdx.x;
+  int pi = 0;
+#pragma unroll
+  for (int k = 1; k < GMAXP; ++k)
+    if (k < g.n && L >= g.p[k].wg0) pi = k;
+  GlProb p = g.p[0];
+#pragma unroll
+  for (int k = 1; k < GMAXP; ++k)
+    if (k == pi) p = g.p[k];
+  const int ntot = p.gm * p.gn * p.nsplit;
+  const int Ll = L - p.wg0;
+  const int xcd = Ll % 8, q8 = ntot / 8, r8 = ntot % 8;
+  const int local = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Ll / 8;
+  const int ntiles = p.gm * p.gn;
+  const int zsplit = local / ntiles, tile = local % ntiles;
+  constexpr int GROUP = 8;
+  const int gsize = GROUP * p.gn;
+  const int first_m = (tile / gsize) * GROUP;
+  const int gm_here = min(p.gm - first_m, GROUP);
+  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
+  const int m0 = tm * CF::BM, n0 = tn * BN;
+  const int kbeg = zsplit * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+  if (kbeg >= kend) return;
+  if (p.nsplit > 1)
+    gl_tile<A_KC, B_KC, EPI_NONE, true, CF>(smem, p.M, p.N, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, nullptr, 0.0f, m0, n0,
+                                            kbeg, kend - kbeg, p.part + (long long)zsplit * p.M * p.N);
+  else
+    gl_tile<A_KC, B_KC, EPI_NONE, false, CF>(smem, p.M, p.N, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, nullptr, p.beta, m0,
+                                             n0, kbeg, kend - kbeg, nullptr);
+}
+
+// The split-K combine of every split problem of a group, one launch: unit u of problem p is four
+// columns (vec) or one element; the arithmetic of gemm_gl_reduce_kernel<vec> (slabs in order z =
+// 0 .. S-1 from zero, then + beta C).
+__global__ __launch_bounds__(256) void gemm_gl_grouped_reduce_kernel(GlGroup g) {
+  const int u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= g.total_units) return;
+  int pi = -1;
+#pragma unroll
+  for (int k = 0; k < GMAXP; ++k)
+    if (k < g.n && g.p[k].nsplit > 1 && u >= g.p[k].u0) pi = k;
+  if (pi < 0) return;
+  GlProb p = g.p[0];
+#pragma unroll
+  for (int k = 1; k < GMAXP; ++k)
+    if (k == pi) p = g.p[k];
+  const long long mn = (long long)p.M * p.N;
+  const int S = p.nsplit;
+  if (p.vec) {
+    const long long i = 4LL * (u - p.u0);
+    if (i >= mn) return;
+    const float* pp = p.part + i;
+    const int r = (int)(i / p.N), c = (int)(i - (long long)r * p.N);
+    float* cp = p.C + (long long)r * p.ldc + c;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z0 = 0; z0 < S; z0 += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w)
+        v[w] = z0 + w < S ? *reinterpret_cast<const float4*>(pp + (long long)(z0 + w) * mn) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        if (z0 + w < S) { a.x += v[w].x; a.y += v[w].y; a.z += v[w].z; a.w += v[w].w; }
+      }
+    }
+    if (p.beta != 0.0f) {
+      const float4 o = *reinterpret_cast<const float4*>(cp);
+      a.x += p.beta * o.x; a.y += p.beta * o.y; a.z += p.beta * o.z; a.w += p.beta * o.w;
+    }
+    *reinterpret_cast<float4*>(cp) = a;
+  } else {
+    const long long i = u - p.u0;
+    if (i >= mn) return;
+    const int r = (int)(i / p.N), c = (int)(i - (long long)r * p.N);
+    float* cp = p.C + (long long)r * p.ldc + c;
+    float a = 0.f;
+    for (int z = 0; z < S; ++z) a += p.part[(long long)z * mn + i];
+    *cp = p.beta != 0.0f ? a + p.beta * *cp : a;
+  }
+}
+
 typedef Cfg<128, 2> C128;  // 128 x 128, double buffer, two workgroups per CU (the round-2 default)
 typedef Cfg<256, 3> C256;  // 256 x 128, three stages, one workgroup per CU
 typedef Cfg<128, 3> C128S3;  // 128 x 128, three stages (measured slower: A/B knob only)
@@ -777,4 +906,85 @@ DL4SS_API int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, co
   if (!a_kc && b_kc) return launch<false, true>(GGL_ARGS);
   return launch<false, false>(GGL_ARGS);
 #undef GGL_ARGS
+}
+
+// Workspace bytes of dl4ss_gemm_bf16_gl_grouped: the split-K slabs of every problem, each at a
+// 256-B aligned offset.
+DL4SS_API long long dl4ss_gemm_bf16_gl_grouped_ws_bytes(int n, const int* M, const int* N, const int* K,
+                                                         const int* splitk) {
+  if (n < 1 || n > GMAXP || !M || !N || !K || !splitk) return -1;
+  long long tot = 0;
+  for (int i = 0; i < n; ++i) {
+    const long long b = dl4ss_gemm_bf16_gl_ws_bytes(M[i], N[i], K[i], splitk[i], 1);
+    tot += (b + 255) / 256 * 256;
+  }
+  return tot;
+}
+
+// Grouped C_i = op(A_i) op(B_i) + beta_i C_i for i < n (n <= 16) in ONE launch (+ one split-K combine
+// launch): the backward's weight gradients.  Every problem has the layout rules of
+// dl4ss_gemm_bf16_gl with the SAME transA / transB, no bias, EPI_NONE; splitk[i] as there (the
+// same slabs and fixed-order sums, so each C_i is bitwise the single launch's).
+DL4SS_API int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const int* M, const int* N, const int* K,
+                                         const void* const* A, const long long* lda, const void* const* B,
+                                         const long long* ldb, float* const* C, const long long* ldc,
+                                         const float* beta, const int* splitk, void* ws, long long ws_bytes,
+                                         void* stream) {
+  DL4SS_REQUIRE(n >= 1 && n <= GMAXP && M && N && K && A && lda && B && ldb && C && ldc && beta && splitk);
+  const bool a_kc = !transA, b_kc = transB;
+  GlGroup g{};
+  long long off = 0;
+  int wg = 0, units = 0;
+  char* w = reinterpret_cast<char*>(ws);
+  for (int i = 0; i < n; ++i) {
+    DL4SS_REQUIRE(M[i] > 0 && N[i] > 0 && K[i] > 0 && A[i] && B[i] && C[i]);
+    DL4SS_REQUIRE(lda[i] % 8 == 0 && ldb[i] % 8 == 0 && ((uintptr_t)A[i] & 15) == 0 && ((uintptr_t)B[i] & 15) == 0);
+    const int k8 = (K[i] + 7) & ~7;
+    DL4SS_REQUIRE(!a_kc || lda[i] >= k8);
+    DL4SS_REQUIRE(!b_kc || ldb[i] >= k8);
+    DL4SS_REQUIRE(a_kc || lda[i] >= ((M[i] + 7) & ~7));
+    DL4SS_REQUIRE(b_kc || ldb[i] >= ((N[i] + 7) & ~7));
+    GlProb& p = g.p[i];
+    p.A = reinterpret_cast<const unsigned short*>(A[i]);
+    p.B = reinterpret_cast<const unsigned short*>(B[i]);
+    p.C = C[i];
+    p.lda = lda[i]; p.ldb = ldb[i]; p.ldc = ldc[i];
+    p.beta = beta[i];
+    p.M = M[i]; p.N = N[i]; p.K = K[i];
+    p.gm = (M[i] + C128::BM - 1) / C128::BM;
+    p.gn = (N[i] + BN - 1) / BN;
+    int sk = splitk[i] < 1 ? 1 : splitk[i];
+    int kps = (K[i] + sk - 1) / sk;
+    kps = (kps + BK - 1) / BK * BK;
+    sk = (K[i] + kps - 1) / kps;
+    p.nsplit = sk;
+    p.kps = kps;
+    p.wg0 = wg;
+    wg += p.gm * p.gn * sk;
+    p.part = nullptr;
+    p.vec = (N[i] % 4 == 0 && ldc[i] % 4 == 0 && ((uintptr_t)C[i] & 15) == 0) ? 1 : 0;
+    p.u0 = units;
+    if (sk > 1) {
+      const long long b = (long long)sk * M[i] * N[i] * 4;
+      DL4SS_REQUIRE(w && off + b <= ws_bytes);
+      p.part = reinterpret_cast<float*>(w + off);
+      off += (b + 255) / 256 * 256;
+      const long long mn = (long long)M[i] * N[i];
+      units += (int)(p.vec ? mn / 4 : mn);
+    }
+  }
+  g.n = n;
+  g.total_wg = wg;
+  g.total_units = units;
+  hipStream_t st = as_stream(stream);
+  if (a_kc && b_kc) hipLaunchKernelGGL((gemm_gl_grouped_kernel<true, true, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
+  else if (a_kc) hipLaunchKernelGGL((gemm_gl_grouped_kernel<true, false, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
+  else if (b_kc) hipLaunchKernelGGL((gemm_gl_grouped_kernel<false, true, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
+  else hipLaunchKernelGGL((gemm_gl_grouped_kernel<false, false, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
+  DL4SS_CHECK_LAUNCH();
+  if (units > 0) {
+    hipLaunchKernelGGL(gemm_gl_grouped_reduce_kernel, dim3(cdiv(units, 256)), dim3(256), 0, st, g);
+    DL4SS_CHECK_LAUNCH();
+  }
+  return 0;
 }

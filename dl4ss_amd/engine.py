@@ -206,11 +206,16 @@ class SepTrainer:
             self.xb0 = torch.empty(BT, p8(D0), **bf)
             self.outb = [torch.empty(BT, p8(2 * H), **bf) for _ in range(net.L)]
             self.hprevb = [torch.empty(BT, 2 * p8(H), **bf) for _ in range(net.L)]
-            self.dGb = torch.empty(BT, 2 * NGH, **bf)
+            # every layer's bf16 dG (and GRU dGh) stays until the end of backward: the weight
+            # gradients of all layers run as one grouped GEMM launch after the last BPTT
+            self.dGb_l = [torch.empty(BT, 2 * NGH, **bf) for _ in range(net.L)]
+            self.dGb = self.dGb_l[0]
             # GRU dGh: each direction's gate columns start 16-B aligned (900 -> 904,
-            # DL4SS_RNN_DGH_PAD8) so both directions' dW_hh are one batched LDS-DMA GEMM
+            # DL4SS_RNN_DGH_PAD8): 16-B aligned LDS-DMA operand rows for each direction's dW_hh
             self.ngh_p8 = p8(NGH)
-            self.dGhb = torch.empty(BT, 2 * self.ngh_p8, **bf) if net.cell == "gru" else None
+            self.dGhb_l = [torch.empty(BT, 2 * self.ngh_p8, **bf) for _ in range(net.L)] if net.cell == "gru" else None
+            self.dGhb = self.dGhb_l[0] if self.dGhb_l else None
+            self._dw_group = None
             # zero row padding (never written): gemm_gl reads k-contiguous rows in 8-element chunks
             self.dPreb = torch.zeros(BT, p8(F * net.E), **bf)
             # gemm_gl split-K slabs (the largest split of _backward_fast)
@@ -363,6 +368,44 @@ class SepTrainer:
         return self.loss
 
     # ------------------------------------------------------------------ backward
+    def _weight_grad_group(self):
+        """The step's weight gradients (dW_lin, then every layer's dW_ih and both directions'
+        dW_hh) as one grouped gemm_gl launch + one split-K combine (ops.GroupedGemm), after the last
+        BPTT: one at a time they under-fill the chip (dW_ih 95 tiles x 4 splits, dW_hh 2 x 30 tiles
+        x 8 splits, each with its own ramp and tail).  Each gradient is bitwise what a single
+        launch with the same split factor produces (tests/test_gemm_grouped_gpu.py).  The weight gradients
+        accumulate (beta 1) onto the zeroed flat gradient: the reference's loss.backward()
+        (TDAA_beta/main_run_sstune_EvalVer.py:673)."""
+        if self._dw_group is not None:
+            return self._dw_group
+        net, H = self.net, self.net.H
+        NGH = _ngate(net.cell) * H
+        FE = self.F * net.E
+        g = net.grad
+        hp8 = self.p8(H)
+        gru = self.dGhb_l is not None
+        ldgh = self.ngh_p8 if gru else NGH
+        # split-K factors of the grouped launch (C2 bench, 20 steps, r03_dwg: dW_lin / dW_ih / dW_hh
+        # 2/4/8 -> 4.434 ms per step, 2/4/4 4.424, 2/3/6 4.420, 1/2/4 4.405, 2/2/4 4.400): fewer, longer
+        # k-ranges than the single launches wanted, and smaller slabs for the combine
+        s_lin, s_ih, s_hh = 2, 2, 4
+        probs = [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
+                      transA=True, transB=False, beta=1.0, splitk=s_lin)]
+        # longest k-ranges first (dW_lin 63 k-tiles per workgroup, dW_ih 32, dW_hh 16): the short
+        # ones fill the tail
+        for l in range(net.L - 1, -1, -1):
+            xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
+            probs.append(dict(A=self.dGb_l[l], B=xb, out=net.cat_view("weight_ih", l, g), transA=True, transB=False,
+                              beta=1.0, splitk=s_ih))
+        for l in range(net.L - 1, -1, -1):
+            src = self.dGhb_l[l] if gru else self.dGb_l[l]
+            whh = net.cat_view("weight_hh", l, g)
+            for d in range(2):
+                probs.append(dict(A=src[:, d * ldgh:d * ldgh + NGH], B=self.hprevb[l][:, d * hp8:d * hp8 + H],
+                                  out=whh[d * NGH:(d + 1) * NGH], transA=True, transB=False, beta=1.0, splitk=s_hh))
+        self._dw_group = ops.GroupedGemm(probs, net.device)
+        return self._dw_group
+
     def _backward_fast(self):
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
@@ -371,42 +414,48 @@ class SepTrainer:
         g = net.grad
         cell = CELLS[net.cell]
         dPreb = self.dPreb[:, :FE]
-        hLb = self.outb[-1][:, :2 * H]
         st = _lib.stream_ptr()
-        gru = self.dGhb is not None
+        gru = self.dGhb_l is not None
+        grouped = net.L <= 5  # <= 16 problems per grouped launch
+        dwg = self._weight_grad_group() if grouped else None
         self.rnn_ws_all[1].zero_()  # every layer's BPTT hand-off workspace, one fill
         # gemm_gl split-K factors, measured per shape at C2 (tools/gemm_gl_bench.py --sweep): dH
         # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
         # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
         dH = self.dH[0]
         ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk=3, ws=self.gl_ws)  # input gradient first
-        ops.gemm_bf16_gl(dPreb, hLb, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk=2,
-                         ws=self.gl_ws)
+        if not grouped:
+            ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
+                             beta=1.0, splitk=2, ws=self.gl_ws)
         _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                   _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part), self.colsum_part.numel() * 4, st)
         hp8 = self.p8(H)
-        dGb, dGhb = self.dGb, self.dGhb if gru else self.dGb
         ldgh = self.ngh_p8 if gru else NGH  # dW_hh operand: direction d at column d * ldgh
         for l in range(net.L - 1, -1, -1):
+            dGb = self.dGb_l[l]
+            dGhb = self.dGhb_l[l] if gru else dGb
             _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED | (DGH_PAD8 if gru else 0), B, T, H, _lib.ptr(dH),
                       _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), None, None,
-                      _lib.ptr(dGb), _lib.ptr(self.dGhb) if gru else None, _lib.ptr(net.cat_view("bias_ih", l, g)),
+                      _lib.ptr(dGb), _lib.ptr(dGhb) if gru else None, _lib.ptr(net.cat_view("bias_ih", l, g)),
                       _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self._ws_slot(l, True)), self.ws_bytes,
                       _lib.ptr(self.status), st)
-            if l > 0:  # the input gradient first: it is all the next BPTT waits on
+            if l > 0:  # the input gradient: all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
                 ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next)
-            xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
-            ops.gemm_bf16_gl(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), beta=1.0, splitk=4,
-                             ws=self.gl_ws)
-            # both directions' dW_hh in one launch: member d = columns d*ldgh of dGh, d*pad8(H) of h_{t-1}
-            ops.gemm_bf16_gl(dGhb[:, :NGH], self.hprevb[l][:, :H], transA=True,
-                             out=net.cat_view("weight_hh", l, g)[:NGH], beta=1.0, splitk=8, batch=2, strideA=ldgh,
-                             strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT, ws=self.gl_ws)
+            if not grouped:
+                xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
+                ops.gemm_bf16_gl(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), beta=1.0, splitk=4,
+                                 ws=self.gl_ws)
+                # both directions' dW_hh in one launch: member d = columns d*ldgh of dGh, d*pad8(H) of h_{t-1}
+                ops.gemm_bf16_gl(dGhb[:, :NGH], self.hprevb[l][:, :H], transA=True,
+                                 out=net.cat_view("weight_hh", l, g)[:NGH], beta=1.0, splitk=8, batch=2, strideA=ldgh,
+                                 strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT, ws=self.gl_ws)
             if l > 0:
                 dH = dH_next
+        if grouped:
+            dwg.run()
 
     def backward(self):
         net, B, T, H = self.net, self.B, self.T, self.net.H

@@ -204,6 +204,58 @@ def gemm_bf16_gl(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE,
     return out
 
 
+class GroupedGemm:
+    """A fixed list of bf16 GEMM problems C_i = op(A_i) @ op(B_i) + beta_i C_i run as ONE grouped
+    launch (dl4ss_gemm_bf16_gl_grouped; + one split-K combine launch).  Each problem is a dict
+    with A, B (bf16 views, 16-B aligned rows), out (fp32 view), transA, transB, beta, splitk and
+    optionally M, N, K (else from the shapes).  The argument arrays are built once: the tensors
+    must stay alive (and at the same addresses) for as long as run() is called."""
+
+    def __init__(self, problems, device):
+        import ctypes
+        n = len(problems)
+        if not 1 <= n <= 16:
+            raise RuntimeError("GroupedGemm: 1..16 problems")
+        ta, tb = int(problems[0]["transA"]), int(problems[0]["transB"])
+        dims, self._keep = [], []
+        for p in problems:
+            A, B, out = p["A"], p["B"], p["out"]
+            _mat_bf16(A, "GroupedGemm(A)")
+            _mat_bf16(B, "GroupedGemm(B)")
+            _mat(out, "GroupedGemm(out)")
+            if int(p["transA"]) != ta or int(p["transB"]) != tb:
+                raise RuntimeError("GroupedGemm: every problem needs the same transA / transB")
+            M, K = (A.shape[1], A.shape[0]) if ta else (A.shape[0], A.shape[1])
+            Kb, N = (B.shape[1], B.shape[0]) if tb else (B.shape[0], B.shape[1])
+            M, N, K = p.get("M", M), p.get("N", N), p.get("K", K)
+            if p.get("K") is None and K != Kb:
+                raise RuntimeError(f"GroupedGemm: inner dims differ ({K} vs {Kb})")
+            dims.append((M, N, K))
+            self._keep += [A, B, out]
+        Iv = lambda xs: (ctypes.c_int * n)(*xs)
+        Lv = lambda xs: (ctypes.c_longlong * n)(*xs)
+        Pv = lambda xs: (ctypes.c_void_p * n)(*xs)
+        self.n, self.ta, self.tb = n, ta, tb
+        self.M, self.N, self.K = Iv([d[0] for d in dims]), Iv([d[1] for d in dims]), Iv([d[2] for d in dims])
+        self.A = Pv([p["A"].data_ptr() for p in problems])
+        self.lda = Lv([p["A"].stride(0) for p in problems])
+        self.B = Pv([p["B"].data_ptr() for p in problems])
+        self.ldb = Lv([p["B"].stride(0) for p in problems])
+        self.C = Pv([p["out"].data_ptr() for p in problems])
+        self.ldc = Lv([p["out"].stride(0) for p in problems])
+        self.beta = (ctypes.c_float * n)(*[float(p.get("beta", 0.0)) for p in problems])
+        self.splitk = Iv([int(p.get("splitk", 1)) for p in problems])
+        nb = _lib.query("dl4ss_gemm_bf16_gl_grouped_ws_bytes", n, self.M, self.N, self.K, self.splitk)
+        if nb < 0:
+            raise RuntimeError("GroupedGemm: bad problem list")
+        self.ws = torch.empty(max(int(nb), 1), device=device, dtype=torch.uint8)
+
+    def run(self):
+        _lib.call("dl4ss_gemm_bf16_gl_grouped", self.n, self.ta, self.tb, self.M, self.N, self.K, self.A, self.lda,
+                  self.B, self.ldb, self.C, self.ldc, self.beta, self.splitk, _lib.ptr(self.ws), self.ws.numel(),
+                  _lib.stream_ptr())
+
+
 def to_bf16(x, out=None):
     """bf16 copy (round to nearest even) of a contiguous fp32 CUDA tensor."""
     _f32c(x, "to_bf16")

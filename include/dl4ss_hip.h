@@ -95,6 +95,17 @@ int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, const void* 
                        long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta,
                        int splitk, int batch, long long strideA, long long strideB, long long strideC, void* ws,
                        long long ws_bytes, void* stream);
+/* Grouped form: n <= 16 independent problems C_i = op(A_i) op(B_i) + beta_i C_i (same transA /
+ * transB for all, no bias, EPI_NONE, per-problem split-K factor) as ONE GEMM launch plus one
+ * split-K combine launch; each C_i bitwise equal to dl4ss_gemm_bf16_gl with the same split factor.
+ * The backward's weight gradients (dW_lin, every layer's dW_ih and both directions' dW_hh), which
+ * the reference accumulates in loss.backward() (TDAA_beta/main_run_sstune_EvalVer.py:673).  The
+ * arrays are host arrays of n entries; ws holds dl4ss_gemm_bf16_gl_grouped_ws_bytes bytes. */
+long long dl4ss_gemm_bf16_gl_grouped_ws_bytes(int n, const int* M, const int* N, const int* K, const int* splitk);
+int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const int* M, const int* N, const int* K,
+                               const void* const* A, const long long* lda, const void* const* B, const long long* ldb,
+                               float* const* C, const long long* ldc, const float* beta, const int* splitk, void* ws,
+                               long long ws_bytes, void* stream);
 /* 2-D form with row padding: y[r*ldy + c] = bf16(x[r*ldx + c]) (c < cols), 0 up to ldy. */
 int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, void* stream);
 /* out[n] += sum_m A[m*lda + n] for a bf16 matrix A (bias gradient from bf16 dPre). */

@@ -1,0 +1,78 @@
+"""Grouped gemm_gl launch (dl4ss_gemm_bf16_gl_grouped, ops.GroupedGemm): the backward's weight
+gradients as one launch + one split-K combine.  Every problem of a group must be BITWISE what the
+single launch (dl4ss_gemm_bf16_gl) with the same split factor produces -- same tiles, same slabs,
+same fixed-order combine -- including beta accumulation onto existing values, unsplit problems
+(written directly), ragged edges and N % 4 != 0 (the scalar combine)."""
+import pytest
+import torch
+
+from dl4ss_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(g, dev, *shape):
+    return ops.to_bf16(torch.randn(*shape, generator=g).to(dev))
+
+
+# (M, N, K, splitk): the C2 / C4 weight-gradient shapes (K = B*T) and ragged small ones
+PROBS = [(6450, 600, 8032, 2), (2400, 600, 8032, 4), (1200, 300, 8032, 8), (1200, 300, 8032, 8),
+         (2400, 129, 8032, 4), (900, 300, 1000, 3), (130, 257, 700, 1), (64, 72, 64, 2), (17, 9, 130, 5)]
+
+
+@pytest.mark.parametrize("ta,tb", [(True, False), (False, True), (True, True), (False, False)])
+def test_grouped_matches_single_launches(dev, ta, tb):
+    g = torch.Generator(device="cpu").manual_seed(11 + 2 * ta + tb)
+    probs, singles = [], []
+    for (M, N, K, sk) in PROBS:
+        A = _bf(g, dev, *((K, (M + 7) // 8 * 8) if ta else (M, (K + 7) // 8 * 8)))
+        B = _bf(g, dev, *((N, (K + 7) // 8 * 8) if tb else (K, (N + 7) // 8 * 8)))
+        if not ta:
+            A[:, K:] = 0  # k-contiguous rows: zero padding up to K rounded to 8
+        if tb:
+            B[:, K:] = 0
+        Av = A[:, :M] if ta else A[:, :K]
+        Bv = B[:, :K] if tb else B[:, :N]
+        C0 = torch.randn(M, N, generator=g).to(dev)
+        beta = 1.0 if sk != 3 else 0.0
+        out = C0.clone()
+        ref = C0.clone()
+        probs.append(dict(A=Av, B=Bv, out=out, transA=ta, transB=tb, beta=beta, splitk=sk, M=M, N=N, K=K))
+        singles.append(ops.gemm_bf16_gl(Av, Bv, transA=ta, transB=tb, out=ref, beta=beta, splitk=sk, M=M, N=N, K=K))
+    grp = ops.GroupedGemm(probs, dev)
+    grp.run()
+    torch.cuda.synchronize()
+    for p, r, shp in zip(probs, singles, PROBS):
+        assert torch.equal(p["out"], r), shp
+    # a second run accumulates again (beta 1) with the same bits as a second single launch
+    grp.run()
+    for p, r, (M, N, K, sk) in zip(probs, singles, PROBS):
+        ops.gemm_bf16_gl(p["A"], p["B"], transA=ta, transB=tb, out=r, beta=p["beta"], splitk=sk, M=M, N=N, K=K)
+    torch.cuda.synchronize()
+    for p, r, shp in zip(probs, singles, PROBS):
+        assert torch.equal(p["out"], r), shp
+
+
+def test_grouped_against_fp64(dev):
+    g = torch.Generator(device="cpu").manual_seed(5)
+    probs, refs = [], []
+    for (M, N, K, sk) in [(300, 200, 1000, 4), (129, 1, 64, 1), (515, 136, 2000, 8)]:
+        A = _bf(g, dev, K, (M + 7) // 8 * 8)[:, :M]
+        B = _bf(g, dev, K, (N + 7) // 8 * 8)[:, :N]
+        out = torch.zeros(M, N, device=dev)
+        probs.append(dict(A=A, B=B, out=out, transA=True, transB=False, beta=0.0, splitk=sk))
+        Ad, Bd = A.double().cpu(), B.double().cpu()
+        refs.append((Ad.t() @ Bd, Ad.abs().t() @ Bd.abs()))
+    ops.GroupedGemm(probs, dev).run()
+    torch.cuda.synchronize()
+    for p, (ref, mag) in zip(probs, refs):
+        err = (p["out"].double().cpu() - ref).abs()
+        assert bool((err <= 2e-6 * mag + 1e-30).all())
+
+
+def test_grouped_rejects_mixed_layouts(dev):
+    A = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
+    out = torch.zeros(64, 64, device=dev)
+    with pytest.raises(RuntimeError):
+        ops.GroupedGemm([dict(A=A, B=A, out=out, transA=True, transB=False),
+                         dict(A=A, B=A, out=out, transA=False, transB=False)], dev)
