@@ -983,28 +983,43 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     return;
   }
   if (pfw) {
-    if (XW) xstart(XPF{});
-    for (int s = 0; s < T; ++s) {
-      if (!XW) {
-        ld.commit(sin + (s & 1) * BC * 32 * 4);
-        if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
+    // Prefetch waves 5-6.  A wave's role is a compile-time pair (its fused-projection tile slots,
+    // whether it holds a matvec tile), so no branch keeps the other role's fragments live: wave 6
+    // (two projection tiles at H = 300 LSTM, no matvec) and wave 5 (one projection tile + matvec
+    // tile 4) -- one shared body for both kept 2 x XK W_ih fragments and the matvec's W_hh / h
+    // fragments live together and spilled 45 VGPRs at XK = 20.
+    auto pf_loop = [&](auto ntl, auto with_mv) __attribute__((always_inline)) {
+      constexpr bool MV = decltype(with_mv)::value;
+      if (XW) xstart(ntl);
+      for (int s = 0; s < T; ++s) {
+        if (!XW) {
+          ld.commit(sin + (s & 1) * BC * 32 * 4);
+          if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
+        }
+        STAMP(0)
+        __syncthreads();  // B1
+        STAMP(1)
+        if constexpr (MV) matvec();
+        // XW: at a block start the rows of the next block (consumed from this step on) landed
+        // before B2; the block after it may stay in flight
+        if (XW && s % SPB == 0) xwait(max(0, min(SPB, T - (s / SPB + 2) * SPB)));
+        STAMP(2)
+        __syncthreads();  // B2
+        STAMP(3)
+        if (XW) xstep(ntl, s);
+        // step s + 3 SPB's rows into slot s % NSLOT, issued after B2 (off the matvec -> B2 path); that
+        // slot held step s's rows, last read by the chain of block s / SPB, which ended before B1(s)
+        if (XW && s + NSLOT < T) xdma(s + NSLOT);
+        STAMP(4)
       }
-      STAMP(0)
-      __syncthreads();  // B1
-      STAMP(1)
-      matvec();
-      // XW: at a block start the rows of the next block (consumed from this step on) landed
-      // before B2; the block after it may stay in flight
-      if (XW && s % SPB == 0) xwait(max(0, min(SPB, T - (s / SPB + 2) * SPB)));
-      STAMP(2)
-      __syncthreads();  // B2
-      STAMP(3)
-      if (XW) xstep(XPF{}, s);
-      // step s + 3 SPB's rows into slot s % NSLOT, issued after B2 (off the matvec -> B2 path); that
-      // slot held step s's rows, last read by the chain of block s / SPB, which ended before B1(s)
-      if (XW && s + NSLOT < T) xdma(s + NSLOT);
-      STAMP(4)
-    }
+    };
+    // (fused projection: wave 6 holds no matvec tile and wave 5 one projection tile --
+    // dl4ss_birnn_fwd_xw_supported admits at most 5 MFMA tiles; without it the slot count is moot)
+    using XP1 = std::integral_constant<int, 1>;
+    if (wv == 6 && !mv)
+      pf_loop(XPF{}, std::false_type{});
+    else
+      pf_loop(XP1{}, std::true_type{});
     STAMP_FLUSH
     return;
   }
@@ -2162,7 +2177,10 @@ DL4SS_API int dl4ss_birnn_fwd_xw_supported(int cell, int B, int T, int H, int Ki
   if (!(cell == CELL_LSTM || cell == CELL_GRU) || B <= 0 || T <= 0 || H <= 0 || Kin <= 0) return 0;
   Plan p;
   if (!make_plan(cell, B, H, p, true)) return 0;
-  return (p.fwd_pk && T < 65535 && Kin <= XKMAX * 32) ? 1 : 0;
+  // at most 5 MFMA tiles (R <= 80 gate rows): prefetch wave 6 then holds no matvec tile and wave 5
+  // one projection tile, the compile-time roles of rnn_fwd_pk_kernel's prefetch branch
+  const int ngate = cell == CELL_LSTM ? 4 : 3;
+  return (p.fwd_pk && T < 65535 && Kin <= XKMAX * 32 && (ngate * p.J + 15) / 16 <= 5) ? 1 : 0;
 }
 
 // dl4ss_birnn_fwd_ex with the input projection fused into the recurrence (bf16 mode only): instead

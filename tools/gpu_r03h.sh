@@ -1,0 +1,10 @@
+# round 3: compile-time prefetch-wave roles of the packed forward (no VGPR spill at XK = 20):
+# recurrence / step / robustness tests, bench line, stamps, kernel trace (TAG)
+R=$GRAFT_REPO_ROOT
+TAG=${TAG:-r03_prog}
+cd $R && mkdir -p gpurun_out/$TAG && export TMPDIR=/tmp &&
+timeout -k 10 900 python -u -m pytest tests/test_kernels_gpu.py tests/test_rnn_xw_gpu.py tests/test_robust_gpu.py tests/test_step_gpu.py tests/test_configs_full_gpu.py tests/test_ref_fixtures_gpu.py tests/test_recursive_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/$TAG/tests.log 2>&1 &&
+timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-stft-standalone > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err &&
+timeout -k 10 200 python -u tools/rnn_stamps.py --bf16 > gpurun_out/$TAG/stamps.txt 2>&1 &&
+cd /tmp &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/$TAG/trace -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stft-standalone > $R/gpurun_out/$TAG/bench_trace.log 2>&1
