@@ -340,7 +340,8 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
 // lanes), then dl, the lane's dPre pairs (written back as bf16 over its own V words) and its dq
 // terms.  V reaches LDS by LDS-DMA (`global_load_lds_dwordx4`, no staging registers) from the 16-B
 // aligned word below the tile (the tile's first word sits `off` words into the LDS image); dPre leaves by coalesced 4-B stores whose
-// (t, f) destination changes only at frame boundaries (compares, no division).  Only the
+// (t, f) destination changes only at frame boundaries, as 16-B stores from each frame segment's first
+// 16-B aligned destination word.  Only the
 // logits' summation order differs from attn_kernel (quad partials instead of one serial chain);
 // dq is per-lane partials -> wave xor-shuffle tree -> waves 0..3 in order (deterministic).
 __device__ __forceinline__ float quad_xor1(float v) {
@@ -511,16 +512,30 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(A
       }
     }
     if constexpr (GRAD) {
-      // bf16 dPre rows (b*T + t) of the padded matrix: word i of the tile belongs to frame
-      // t0 + (i >= ib1) + (i >= ib2) + ..., at word (r0 - t F) EP + i of that row
+      // bf16 dPre rows (b*T + t) of the padded matrix: the tile's words [s, e) of frame t go to
+      // words (r0 - t F) EP + i of that row, one contiguous segment per frame (at most 3 here).
+      // Rows start 16-B aligned (ldpb % 8 == 0), so each segment is written as 16-B stores from its
+      // first 16-B aligned destination word on (four LDS words each: the source is only 4-B
+      // aligned), with its <= 3 head and <= 3 tail words stored singly: a quarter of the store
+      // instructions of a word-per-lane copy.
       __syncthreads();
       const int t0 = r0 / a.F;
-      const int ib1 = ((t0 + 1) * a.F - r0) * EP, fw = a.F * EP;
       const long long rowb = (long long)b * a.T;
-      for (int i = tid; i < nr * EP; i += NT) {
-        int t = t0, ib = ib1;
-        while (i >= ib) { ++t; ib += fw; }
-        a.dPreB[((rowb + t) * a.ldpb >> 1) + (long long)(r0 - t * a.F) * EP + i] = sv[off + i];
+      const int ntot = nr * EP;
+      for (int t = t0, sw = 0; sw < ntot; ++t) {
+        const int ew = min(ntot, ((t + 1) * a.F - r0) * EP);  // end of frame t's words in the tile
+        unsigned* dst = a.dPreB + ((rowb + t) * a.ldpb >> 1) + (long long)(r0 - t * a.F) * EP;  // + i
+        const int lead = (int)((4 - (((uintptr_t)(dst + sw)) >> 2)) & 3);  // words before the first aligned one
+        const int i0 = min(ew, sw + lead);
+        const int nq = (ew - i0) >> 2;
+        for (int q = tid; q < nq; q += NT) {
+          const int i = i0 + 4 * q;
+          *reinterpret_cast<uint4*>(dst + i) = make_uint4(sv[off + i], sv[off + i + 1], sv[off + i + 2], sv[off + i + 3]);
+        }
+        const int te = i0 + 4 * nq;  // tail words [te, ew), head words [sw, i0)
+        if (tid < i0 - sw) dst[sw + tid] = sv[off + sw + tid];
+        if (tid >= 4 && tid - 4 < ew - te) dst[te + tid - 4] = sv[off + te + tid - 4];
+        sw = ew;
       }
     }
   }

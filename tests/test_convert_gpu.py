@@ -1,0 +1,40 @@
+"""fp32 -> bf16 conversions of the bf16 step (convert.hip): the multi-segment row-padded form that
+writes every layer's W_ih and the Linear weight copy in one launch (dl4ss_f32_to_bf16_2d_multi),
+bitwise against torch's round-to-nearest-even bf16 cast, with zero row padding -- on 16-B aligned
+segments (8-column chunks) and on segments whose rows are not (the 4-B pair path)."""
+import ctypes
+
+import pytest
+import torch
+
+from dl4ss_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def test_f32_to_bf16_2d_multi_matches_torch(dev):
+    g = torch.Generator(device="cpu").manual_seed(2)
+    # (rows, cols, ldx, ldy, x element offset): aligned 600 / 129 / 300-wide rows, and rows that
+    # start 4 B off a 16-B boundary (x offset 1, odd ldx) or with ldy % 8 != 0
+    shapes = [(2400, 600, 600, 600, 0), (2400, 129, 129, 136, 0), (6450, 600, 600, 608, 0), (37, 131, 133, 138, 1),
+              (5, 7, 9, 8, 3)]
+    xs, ys, keep = [], [], []
+    for rows, cols, ldx, ldy, off in shapes:
+        base = torch.randn(rows * ldx + off + 4, generator=g).to(dev)
+        x = base[off:off + rows * ldx].view(rows, ldx)
+        y = torch.full((rows, ldy), -1.0, device=dev).to(torch.bfloat16)
+        xs.append(x)
+        ys.append(y)
+        keep.append(base)
+    n = len(shapes)
+    P = ctypes.c_void_p
+    _lib.call("dl4ss_f32_to_bf16_2d_multi", n, (P * n)(*[x.data_ptr() for x in xs]),
+              (ctypes.c_longlong * n)(*[s[2] for s in shapes]), (ctypes.c_int * n)(*[s[0] for s in shapes]),
+              (ctypes.c_int * n)(*[s[1] for s in shapes]), (P * n)(*[y.data_ptr() for y in ys]),
+              (ctypes.c_longlong * n)(*[s[3] for s in shapes]), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    for (rows, cols, ldx, ldy, off), x, y in zip(shapes, xs, ys):
+        ref = x[:, :cols].to(torch.bfloat16)
+        assert torch.equal(y[:, :cols].view(torch.int16), ref.view(torch.int16)), (rows, cols)
+        if ldy > cols:
+            assert bool((y[:, cols:].float() == 0).all()), (rows, cols)
