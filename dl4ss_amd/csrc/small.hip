@@ -10,11 +10,14 @@ namespace {
 //   ADDJUST: EvalVer.py:373-375 and 606-608 (q <- q + adjust(h, q)), no bias
 // one workgroup per utterance: mean over T of h (B,T,D) then K tiny matvecs
 // ---------------------------------------------------------------------------
-// mean_t h[b, :, c]: block = 64 columns x 4 time phases, grid (B, ceil(D/64));
-// each thread keeps 4 independent loads in flight, phases combined in fixed order
-__global__ __launch_bounds__(256) void time_mean_kernel(const float* __restrict__ h, int T, int D,
-                                                        float* __restrict__ mean_out) {
-  __shared__ float sp[4][64];
+// mean_t h[b, :, c]: block = 64 columns x 16 time phases (1024 threads), grid (B, ceil(D/64));
+// each thread sums t = ph, ph + 16, ... with 4 independent loads in flight, the 16 phases are
+// combined by a fixed tree.  (4 phases of 256 threads kept too few loads in flight per CU: 11.8 us
+// for the 19 MB of the C2 step.)
+constexpr int TM_PH = 16;
+__global__ __launch_bounds__(64 * TM_PH) void time_mean_kernel(const float* __restrict__ h, int T, int D,
+                                                               float* __restrict__ mean_out) {
+  __shared__ float sp[TM_PH][64];
   const int b = blockIdx.x;
   const int c = blockIdx.y * 64 + (threadIdx.x & 63);
   const int ph = threadIdx.x >> 6;
@@ -22,19 +25,26 @@ __global__ __launch_bounds__(256) void time_mean_kernel(const float* __restrict_
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < D) {
     int t = ph;
-    for (; t + 12 < T; t += 16) {
+    for (; t + 3 * TM_PH < T; t += 4 * TM_PH) {
       s0 += hb[(long long)t * D];
-      s1 += hb[(long long)(t + 4) * D];
-      s2 += hb[(long long)(t + 8) * D];
-      s3 += hb[(long long)(t + 12) * D];
+      s1 += hb[(long long)(t + TM_PH) * D];
+      s2 += hb[(long long)(t + 2 * TM_PH) * D];
+      s3 += hb[(long long)(t + 3 * TM_PH) * D];
     }
-    for (; t < T; t += 4) s0 += hb[(long long)t * D];
+    for (; t < T; t += TM_PH) s0 += hb[(long long)t * D];
   }
   sp[ph][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (ph == 0 && c < D) {
     const int l = threadIdx.x;
-    mean_out[(long long)b * D + c] = ((sp[0][l] + sp[1][l]) + (sp[2][l] + sp[3][l])) / (float)T;
+    float v[TM_PH];
+#pragma unroll
+    for (int i = 0; i < TM_PH; ++i) v[i] = sp[i][l];
+#pragma unroll
+    for (int w = TM_PH / 2; w > 0; w >>= 1)
+#pragma unroll
+      for (int i = 0; i < w; ++i) v[i] += v[i + w];
+    mean_out[(long long)b * D + c] = v[0] / (float)T;
   }
 }
 
@@ -86,10 +96,10 @@ __global__ __launch_bounds__(64) void query_fwd_kernel(const float* __restrict__
 //   dW_adj[o][c] += sum_b u[b][o] mean[b][c]  (c < D);  sum_{b,k} dq[b,k,o] Emb[idx[b,k]][c-D]
 // Every dh / dW_adj element has one owner thread and a fixed summation order; only the
 // embedding rows (speaker ids shared across the batch) use atomics.
-__global__ __launch_bounds__(64) void query_bwd_dh_kernel(const float* __restrict__ dq,
-                                                          const float* __restrict__ wadj, int T, int D, int K,
-                                                          int W, float* __restrict__ dh_bcast) {
-  const int b = blockIdx.y, c = blockIdx.x * 64 + threadIdx.x;
+__device__ __forceinline__ void query_bwd_dh(int bx, int by, const float* __restrict__ dq,
+                                             const float* __restrict__ wadj, int T, int D, int K, int W,
+                                             float* __restrict__ dh_bcast) {
+  const int b = by, c = bx * 64 + threadIdx.x;
   if (c >= D) return;
   const float* dqb = dq + (long long)b * K * W;
   float g0 = 0.f, g1 = 0.f;
@@ -106,10 +116,9 @@ __global__ __launch_bounds__(64) void query_bwd_dh_kernel(const float* __restric
 // d_emb[id] += sum over the rows bk with idx[bk] == id, in bk order: the block of the first
 // such row owns the label and sums every row of it (no atomics: a speaker drawn twice in a
 // batch gets the same bits on every run)
-__global__ __launch_bounds__(64) void query_bwd_emb_kernel(const float* __restrict__ dq, const int* __restrict__ idx,
-                                                           int BK, const float* __restrict__ wadj, int D, int W,
-                                                           float* __restrict__ demb) {
-  const int bk = blockIdx.x;
+__device__ __forceinline__ void query_bwd_emb(int bk, const float* __restrict__ dq, const int* __restrict__ idx,
+                                              int BK, const float* __restrict__ wadj, int D, int W,
+                                              float* __restrict__ demb) {
   const int id = idx[bk];
   if (id < 0) return;
   for (int j = 0; j < bk; ++j)
@@ -132,17 +141,16 @@ __global__ __launch_bounds__(64) void query_bwd_emb_kernel(const float* __restri
   }
 }
 
-__global__ __launch_bounds__(64) void query_bwd_w_kernel(const float* __restrict__ dq, const int* __restrict__ idx,
-                                                         const float* __restrict__ emb,
-                                                         const float* __restrict__ mean, int B, int D, int K, int W,
-                                                         float* __restrict__ dwadj) {
+__device__ __forceinline__ void query_bwd_w(int bx, int by, float* sm, const float* __restrict__ dq,
+                                            const int* __restrict__ idx, const float* __restrict__ emb,
+                                            const float* __restrict__ mean, int B, int D, int K, int W,
+                                            float* __restrict__ dwadj) {
   // block (column chunk, o): the o-th dq column (and its per-utterance sums u) and the
   // speaker ids staged in LDS, then 8 independent loads in flight per thread
-  extern __shared__ float sm[];
   float* sdq = sm;            // [B*K]  dq[bk][o]
   float* su = sdq + B * K;    // [B]    u[b][o]
   int* sid = reinterpret_cast<int*>(su + B);  // [B*K]
-  const int o = blockIdx.y, c = blockIdx.x * 64 + threadIdx.x;
+  const int o = by, c = bx * 64 + threadIdx.x;
   for (int i = threadIdx.x; i < B * K; i += 64) {
     sdq[i] = dq[(long long)i * W + o];
     sid[i] = idx[i];
@@ -180,6 +188,37 @@ __global__ __launch_bounds__(64) void query_bwd_w_kernel(const float* __restrict
     }
   }
   dwadj[(long long)o * (D + W) + c] += ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+// The three query backward parts as ONE launch (64-thread blocks, role by block range: the
+// embedding rows, dh_bcast, dW_adj): one after another they were three ~10-13 us latency-bound
+// launches in the step; side by side they overlap.  Each part's arithmetic is unchanged.
+struct QbArgs {
+  const float* dq;
+  const int* idx;
+  const float* emb;
+  const float* wadj;
+  const float* mean;
+  int B, T, D, K, W;
+  float* demb;
+  float* dwadj;
+  float* dh;
+  int n_emb, n_dh_x, n_dh, n_w_x;
+};
+__global__ __launch_bounds__(64) void query_bwd_kernel(QbArgs a) {
+  extern __shared__ float sm[];
+  int blk = blockIdx.x;
+  if (blk < a.n_emb) {
+    query_bwd_emb(blk, a.dq, a.idx, a.B * a.K, a.wadj, a.D, a.W, a.demb);
+    return;
+  }
+  blk -= a.n_emb;
+  if (blk < a.n_dh) {
+    query_bwd_dh(blk % a.n_dh_x, blk / a.n_dh_x, a.dq, a.wadj, a.T, a.D, a.K, a.W, a.dh);
+    return;
+  }
+  blk -= a.n_dh;
+  query_bwd_w(blk % a.n_w_x, blk / a.n_w_x, sm, a.dq, a.idx, a.emb, a.mean, a.B, a.D, a.K, a.W, a.dwadj);
 }
 
 // out[n] (+)= sum_m A[m*lda + n]   (bias gradients); block = 64 columns x 4 row lanes
@@ -249,7 +288,7 @@ DL4SS_API int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* id
   DL4SS_REQUIRE(!w_adj || mean_out);  // ADJUST needs the time mean (also saved for the backward)
   hipStream_t st = as_stream(stream);
   if (mean_out) {
-    hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(256), 0, st, h, T, D, mean_out);
+    hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(64 * TM_PH), 0, st, h, T, D, mean_out);
     DL4SS_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(query_fwd_kernel, dim3(W, B, cdiv(K, 4)), dim3(64), 0, st, mean_out, D, idx, emb, w_adj, K, W,
@@ -261,7 +300,7 @@ DL4SS_API int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* id
 DL4SS_API int dl4ss_time_mean(const float* h, int B, int T, int D, float* mean_out, void* stream) {
   DL4SS_REQUIRE(h && mean_out && B >= 0 && T > 0 && D > 0);
   if (B == 0) return 0;
-  hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(256), 0, as_stream(stream), h, T, D, mean_out);
+  hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(64 * TM_PH), 0, as_stream(stream), h, T, D, mean_out);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
@@ -271,21 +310,22 @@ DL4SS_API int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* i
                               float* dh_bcast, void* stream) {
   DL4SS_REQUIRE(dq && idx && B > 0 && K > 0 && W > 0);
   hipStream_t st = as_stream(stream);
-  if (d_emb) {
-    hipLaunchKernelGGL(query_bwd_emb_kernel, dim3(B * K), dim3(64), 0, st, dq, idx, B * K, w_adj, D, W, d_emb);
-    DL4SS_CHECK_LAUNCH();
-  }
-  if (w_adj && dh_bcast) {
-    hipLaunchKernelGGL(query_bwd_dh_kernel, dim3(cdiv(D, 64), B), dim3(64), 0, st, dq, w_adj, T, D, K, W, dh_bcast);
-    DL4SS_CHECK_LAUNCH();
-  }
+  QbArgs a{dq, idx, emb, w_adj, mean, B, T, D, K, W, d_emb, d_wadj, dh_bcast, 0, 0, 0, 0};
+  a.n_emb = d_emb ? B * K : 0;
+  a.n_dh_x = (int)cdiv(D, 64);
+  a.n_dh = (w_adj && dh_bcast) ? a.n_dh_x * B : 0;
+  a.n_w_x = (int)cdiv(D + W, 64);
+  int n_w = 0;
+  size_t smem = 0;
   if (w_adj && d_wadj) {
     DL4SS_REQUIRE(mean && emb);
-    const size_t smem = sizeof(float) * (2 * (size_t)B * K + B);
-    hipLaunchKernelGGL(query_bwd_w_kernel, dim3(cdiv(D + W, 64), W), dim3(64), smem, st, dq, idx, emb, mean, B, D, K,
-                       W, d_wadj);
-    DL4SS_CHECK_LAUNCH();
+    n_w = a.n_w_x * W;
+    smem = sizeof(float) * (2 * (size_t)B * K + B);
   }
+  const int nblk = a.n_emb + a.n_dh + n_w;
+  if (nblk == 0) return 0;
+  hipLaunchKernelGGL(query_bwd_kernel, dim3(nblk), dim3(64), smem, st, a);
+  DL4SS_CHECK_LAUNCH();
   return 0;
 }
 
