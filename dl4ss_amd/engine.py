@@ -187,6 +187,7 @@ class SepTrainer:
         # attention kernel writes bf16 dPre, the weights and the layer-0 features are converted
         # once per step.  Rows are padded to multiples of 8 (16-B aligned operand rows).
         self.fast = precision == "bf16" and self.rnn_precision == "bf16"
+        self.dh_split = int(os.environ.get("DL4SS_DH_SPLIT", "3"))  # dH split-K (tuning knob, A/B runs)
         # Forward input projections x W_ih^T + b_ih formed inside the packed recurrence kernel
         # (dl4ss_birnn_fwd_xw) instead of a gemm_gl launch + a G buffer round trip; bitwise the same
         # G (tests/test_rnn_xw_gpu.py).  Each tile's projection of a block of 16 / BC steps is one
@@ -423,7 +424,7 @@ class SepTrainer:
         # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
         # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
         dH = self.dH[0]
-        ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk=3, ws=self.gl_ws)  # input gradient first
+        ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk=self.dh_split, ws=self.gl_ws)  # input gradient first
         if not grouped:
             ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
                              beta=1.0, splitk=2, ws=self.gl_ws)
