@@ -1450,6 +1450,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 //        4 polls the NG producers' partials of the own J units into LDS;
 //        5-7 per-step operand prefetch.
 // --------------------------------------------------------------------------
+// BPTT per-step operand loads (prefetch waves): issued after B1, in the cell phase, not beside the
+// polling sweeps in the CU's memory queue (BWD_PF_LATE), as slot-major items (BWD_PF_SLOTMAJOR)
+#ifndef BWD_PF_LATE
+#define BWD_PF_LATE 1
+#endif
+#ifndef BWD_PF_SLOTMAJOR
+#define BWD_PF_SLOTMAJOR 1
+#endif
 __device__ __forceinline__ unsigned pack24(float v) {
   const unsigned u = __float_as_uint(v);
   return (u + 0x80u) >> 8;  // round to nearest (ties away) on the dropped 8 bits
@@ -1532,14 +1540,31 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   //   0 dOut, 1..4 act, 5 c (LSTM) / h_prev (GRU), 6 c_prev (LSTM), 7 unused
   constexpr int WPF = WPOLL + BWD_NPW;  // waves WPOLL .. WPF-1 poll
   constexpr int NPF = NT - WPF * 64;
+  // slot-major items (item = slot * BC*J + cell): a load instruction's lanes read consecutive
+  // units of one operand row -- a few cache lines per instruction instead of one per lane-octet;
+  // the slots in use only (LSTM 0-6, GRU 0-5: 3 instructions instead of 4).  With the issue after
+  // B1, cell-major items (8 operands of a cell on 8 lanes: conflict-free commits) held the
+  // prefetch waves ~650 cycles past the cell phase at B2 (stamps, profiles/r03_pfmap_stamps.txt);
+  // the commit's 8-way LDS conflict this order costs is off the critical path
+#if BWD_PF_SLOTMAJOR
+  constexpr int NSL = CELL == CELL_LSTM ? 7 : 6;
+  constexpr int NQ = (BC * 20 * NSL + NPF - 1) / NPF;
+  const int ncell = BC * J;
+#else
   constexpr int NQ = (BC * 20 * 8 + NPF - 1) / NPF;
+#endif
   StepLoader<NQ> ld;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int i = tid - WPF * 64 + q * NPF;  // item = cell * 8 + slot
+    const int i = tid - WPF * 64 + q * NPF;
+#if BWD_PF_SLOTMAJOR
+    const int slot = i / ncell, cell = i % ncell;
+    const bool on = wv >= WPF && i >= 0 && slot < NSL;
+#else
     const int slot = i & 7, cell = i >> 3;
-    const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
     const bool on = wv >= WPF && cell < BC * J;
+#endif
+    const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
     const bool valid = on && ib < a.B && ij < H;
     const float* p = nullptr;
     int stride = 2 * H, shift = 0;
@@ -1648,9 +1673,18 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   if (wv >= WPF) {
     for (int s = 0; s < T; ++s) {
       ld.commit(sop + (s & 1) * 2 * SOPP);
+#if BWD_PF_LATE
+      // the next step's operand loads go out after B1, in the cell phase: not in the CU's memory
+      // queue beside the polling sweeps (MI355X_MICROARCH.md handoff-1to1: the hand-off price sits
+      // in the consumer CU's queue); they still have the cell phase and the next poll window to land
+      __syncthreads();  // B1
+      if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+      __syncthreads();  // B2
+#else
       if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
       __syncthreads();  // B1
       __syncthreads();  // B2
+#endif
       if (s + 1 == T) break;
     }
     return;
