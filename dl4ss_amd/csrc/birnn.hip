@@ -562,7 +562,7 @@ static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
 // (k-step ks on wave ks % 4) instead of whole on wave 5 -- wave 5 shares SIMD 1 with wave 1, whose
 // matvec then ran its 10 MFMAs beside wave 5's 10 (stamps: wave 5 629 vs wave 0 404 cycles from
 // B1, every other wave waiting at B2 for it)
-#define FWD_SPLIT4 0  // off until measured on the GPU (libdl4ss_hip_s4.so A/B in tools/gpu_r03p.sh)
+#define FWD_SPLIT4 0  // measured slower: 7882 vs 8102 mixtures/s (profiles/r03_split4.jsonl)
 #endif
 #ifndef XW_MAP
 // fused projection tile -> wave map (rnn_fwd_pk_kernel): 1 = second tiles on the prefetch waves
