@@ -1520,6 +1520,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 #ifndef BWD_PF_SLOTMAJOR
 #define BWD_PF_SLOTMAJOR 1
 #endif
+// the cell lanes' dG / dGh stores of step s-1 issued after B1 of step s (before the cell update)
+// instead of right after the publish: measured slower, 7994 vs 8085 mixtures/s
+// (profiles/r03_dglate.jsonl) -- their issue then sits on the cell phase's critical path
+#ifndef BWD_DG_LATE
+#define BWD_DG_LATE 0
+#endif
 __device__ __forceinline__ unsigned pack24(float v) {
   const unsigned u = __float_as_uint(v);
   return (u + 0x80u) >> 8;  // round to nearest (ties away) on the dropped 8 bits
@@ -1787,6 +1793,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     __syncthreads();  // B1
     STAMP(1)
     if (tid == 0) TRACE(3, s);
+    if (BWD_DG_LATE && s > 0) store_dg();  // step s-1's (pt, pgi, pgh)
     if (tid < BC * 32) {
       float dgi[NGATE], dgh[NGATE];
 #pragma unroll
@@ -1894,7 +1901,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       }
       if (wv == 3) TRACE(0, s);
     }
-    store_dg();  // this step's dG / dGh, after the publish (off the critical path)
+    if (!BWD_DG_LATE) store_dg();  // this step's dG / dGh, after the publish (off the critical path)
     STAMP(6)
   }
   // fused bias gradients: this cell's sums over t, one plain store per (row, gate) into the
