@@ -62,6 +62,7 @@ SIGNATURES = {
     "dl4ss_time_mean": [P, I, I, I, P, P],
     "dl4ss_bss_corr": [P, I, I, I, I, P, P],
     "dl4ss_mix_sources_ex": [P, P, P, I, I, I, P, P, P, P],
+    "dl4ss_mix_sources_rot": [P, P, P, P, I, I, I, P, P, P, P],
     "dl4ss_f32_to_bf16_2d_multi": [I, P, P, P, P, P, P, P],
     "dl4ss_mask_attn_loss_bf16v": [I, I, I, I, I, I, I, P, P, P, LL, P, LL, LL, P, F, F, P, P, LL, P, P, P, P, P],
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],

@@ -2,10 +2,46 @@
 speakers of a split, the reference's per-source normalisation + gain rules and its
 STFT features, computed on the GPU kernels (dl4ss_mix_sources, dl4ss_stft_fwd) and
 handed back in the reference's numpy batch-dict layout."""
+import random
+
 import numpy as np
 import torch
 
 from dl4ss_amd import ops, synth
+
+
+def draw_shifts(lengths):
+    """The list loaders' AUGMENT_DATA draw, one per source in line order:
+    ``random_shift = random.sample(range(len(signal)), 1)[0]`` over the cropped source's
+    own length (TDAA_beta/predata_fromList.py:150-151, predata_fromList_cRM_123.py:198-200),
+    on the module-level ``random`` like the reference.  lengths (B, K) -> (B, K) int32."""
+    L = np.asarray(lengths)
+    out = np.zeros(L.shape, np.int32)
+    for b in range(L.shape[0]):
+        for k in range(L.shape[1]):
+            out[b, k] = random.sample(range(int(L[b, k])), 1)[0]
+    return out
+
+
+def torch_multi_augment(cfg, n):
+    """Torch_multi/predata_multiAims_dB.py:164-166 (and _3dB.py:179-181) with AUGMENT_DATA set:
+    the shift is drawn like the list loaders' but applied as ``signal[s:] + signal[:s]``, a
+    numpy broadcast of lengths n-s and s that raises for every s outside {1, n-1, n/2}.  The
+    reference therefore stops at its first source with this ValueError (with probability
+    1 - 3/n; config_WSJ0_dB.py:112 sets the flag, and Torch_multi/ holds no config_WSJ0_dB of
+    its own).  This build raises the same error; for the three shifts where numpy broadcasts,
+    the reference continues with a folded SUM of two slices (oracle.dsp.augment_torch_multi,
+    pinned by tests/golden/ref_r1_augment.npz), which this build does not reproduce -- it
+    raises NotImplementedError there instead of training on different data."""
+    if not getattr(cfg, "AUGMENT_DATA", False):
+        return
+    s = random.sample(range(n), 1)[0]
+    a, b = n - s, s
+    if a == b or a == 1 or b == 1:
+        raise NotImplementedError(
+            "AUGMENT_DATA with the Torch_multi loaders: the reference's signal[s:] + signal[:s] "
+            f"(predata_multiAims_dB.py:166) broadcasts for s={s} of n={n} into a folded sum, not reproduced here")
+    raise ValueError(f"operands could not be broadcast together with shapes ({a},) ({b},) ")
 
 
 def split_speakers(cfg, split):
@@ -61,9 +97,13 @@ def list_prepare_data(cfg, mode, split, complex_targets, mix_k, seed=1):
     lp = list_path(split, mix_k)
     data_path = cfg.aim_path + "/data"
     B = cfg.BATCH_SIZE
+    # AUGMENT_DATA rotates every TRAIN source (predata_fromList_cRM_123.py:198: `and
+    # train_or_test=='train'`); the shifts run through dl4ss_mix_sources_rot on the GPU
+    augment = bool(getattr(cfg, "AUGMENT_DATA", False)) and split == "train"
     if lp and os.path.exists(lp) and os.path.isdir(os.path.join(data_path, "train")):
         all_spk = sorted(os.listdir(os.path.join(data_path, "train")))
-        lb = wsj0list.ListBatches(lp, data_path, split, B, cfg.MAX_LEN, shuffle=bool(cfg.SHUFFLE_BATCH), seed=seed)
+        lb = wsj0list.ListBatches(lp, data_path, split, B, cfg.MAX_LEN, shuffle=bool(cfg.SHUFFLE_BATCH), seed=seed,
+                                  augment=augment)
         batch_total = lb.batch_total
         dev = torch.device("cuda")
 
@@ -84,7 +124,7 @@ def list_prepare_data(cfg, mode, split, complex_targets, mix_k, seed=1):
         def batches():
             for _ in range(batch_total):
                 db = rng.uniform(-2.5, 2.5, size=(B, mix_k))
-                yield maker.make(B, complex_targets=complex_targets, db_list=db)
+                yield maker.make(B, complex_targets=complex_targets, db_list=db, augment=augment)
     for dev_batch in batches():
         if mode == "global":
             T, F = dev_batch["mix_mag"].shape[1:3]
@@ -113,12 +153,17 @@ class BatchMaker:
                                                             "eval_test": 2}[split] * 7919
         self.gen = synth.SyntheticMixtures(n_samples=cfg.MAX_LEN, k=k, num_labels=len(self.speakers), seed=sd)
 
-    def make(self, B, complex_targets=False, db_list=None, gain_rule="db2"):
+    def make(self, B, complex_targets=False, db_list=None, gain_rule="db2", augment=False):
         """Returns the device tensors of one batch: dict with src (B,K,N) scaled sources,
         mix (B,N), mix_c (B,T,F,2), mix_mag (B,T,F), src_feat (B,K,T,F) magnitude or
-        (B,K,T,F,2) complex, names (B lists of K names).  gain_rule: see gains_of."""
+        (B,K,T,F,2) complex, names (B lists of K names).  gain_rule: see gains_of.
+        augment: the list loaders' train-split rotation (draw_shifts); the Torch_multi
+        loaders pass ``augment="torch_multi"`` (torch_multi_augment)."""
         cfg = self.cfg
         N, K = cfg.MAX_LEN, self.k
+        if augment == "torch_multi":
+            torch_multi_augment(cfg, N)
+            augment = False
         src, spk, u = self.gen.batch(B)
         if db_list is not None:  # list-driven loaders: gains 10^(dB_i/20) (predata_fromList_cRM_123.py:206,227)
             gains = 10.0 ** (np.asarray(db_list, dtype=np.float64) / 20.0)
@@ -127,7 +172,8 @@ class BatchMaker:
         dev = torch.device("cuda")
         raw = torch.from_numpy(src.astype(np.float32)).to(dev)
         g = torch.from_numpy(np.ascontiguousarray(gains, dtype=np.float32)).to(dev)
-        s, m = ops.mix_sources(raw, g)
+        shifts = torch.from_numpy(draw_shifts(np.full((B, K), N))).to(dev) if augment else None
+        s, m = ops.mix_sources(raw, g, shifts=shifts)
         Xc, Xm = ops.stft(m, complex_out=True, mag_out=True, log=bool(cfg.IS_LOG_SPECTRAL))
         if complex_targets:
             Sc, _ = ops.stft(s.view(B * K, N), complex_out=True, mag_out=False)

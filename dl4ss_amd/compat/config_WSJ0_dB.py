@@ -13,6 +13,9 @@ MAX_EPOCH = 600
 EPOCH_SIZE = 300
 quchong_alpha = 1
 dB = 5
-# the reference sets AUGMENT_DATA = True here, but its augmentation line is a numpy
-# broadcast error (predata_multiAims_dB.py:166): disabled in this build
-AUGMENT_DATA = False
+# TDAA_beta/config_WSJ0_dB.py:111-112: set False, then True.  The list loaders
+# (predata_fromList, predata_fromList_cRM_123) rotate every train source
+# (dl4ss_mix_sources_rot); the Torch_multi loaders' form of the same line is a numpy
+# broadcast error (predata_multiAims_dB.py:166) that this build raises as the reference
+# does (compat._data.torch_multi_augment) -- run them with AUGMENT_DATA = False.
+AUGMENT_DATA = True

@@ -58,7 +58,7 @@ def prepare_data(mode, train_or_test, gain_rule=GAIN_RULE, cfg=None):
     mix_k = random.randint(cfg.MIN_MIX, cfg.MAX_MIX)
     maker = BatchMaker(cfg, train_or_test, mix_k, seed_offset=random.randrange(1 << 20))
     while True:
-        dev = maker.make(cfg.BATCH_SIZE, gain_rule=gain_rule)
+        dev = maker.make(cfg.BATCH_SIZE, gain_rule=gain_rule, augment="torch_multi")
         if mode == 'global':
             spk = sorted(all_spk_train)
             d2i = {s: i for i, s in enumerate(spk)}

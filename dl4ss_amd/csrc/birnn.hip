@@ -139,6 +139,9 @@ __device__ __forceinline__ float sum_partials16(const float* p, int stride) {
   return v[0];
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// (no NaN special case on the recurrence's critical path: values formed here by arithmetic
+// are canonical quiet NaNs 0x7FC00000 / 0xFFC00000 when non-finite, which round to NaN; the
+// fp32 weights arriving as arbitrary bit patterns go through bf16_bits_rne)
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
   unsigned u = __float_as_uint(f);
   u += 0x7FFF + ((u >> 16) & 1);
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = ks * 32 + 8 * (lane >> 4) + j;
-        afrag[ks][j] = (short)bf16_rne((rv && k < H) ? wrow[k] : 0.0f);
+        afrag[ks][j] = (short)bf16_bits_rne((rv && k < H) ? wrow[k] : 0.0f);
       }
     for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;  // bf16 image incl. padding rows/cols
   }
@@ -670,7 +673,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = ks * 32 + 8 * (lane >> 4) + j;
-        afrag[ks][j] = (short)bf16_rne((rv && k < H) ? wrow[k] : 0.0f);
+        afrag[ks][j] = (short)bf16_bits_rne((rv && k < H) ? wrow[k] : 0.0f);
       }
   }
   // split4: cell wave w's k-steps w, w + 4, w + 8 of tile 4 (zero beyond KSMAX / H)
@@ -686,7 +689,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = (wv + 4 * i) * 32 + 8 * (lane >> 4) + j;
-        afx[i][j] = (short)bf16_rne((rv && wv + 4 * i < KSMAX && k < H) ? wrow[k] : 0.0f);
+        afx[i][j] = (short)bf16_bits_rne((rv && wv + 4 * i < KSMAX && k < H) ? wrow[k] : 0.0f);
       }
   }
   for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;
@@ -1239,7 +1242,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
           const int rr = ks * 32 + 8 * (lane >> 4) + j;
           const int q = rr / J, u = rr % J;
           const bool ok = mv && k < H && rr < R && j0 + u < H;
-          afr[t][ks][j] = (short)bf16_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
+          afr[t][ks][j] = (short)bf16_bits_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
         }
     }
   }
@@ -1579,7 +1582,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         const int rr = ks * 32 + 8 * (lane >> 4) + j;
         const int q = rr / J, u = rr % J;
         const bool ok = mv && k < H && rr < R && j0 + u < H;
-        afr[t][ks][j] = (short)bf16_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
+        afr[t][ks][j] = (short)bf16_bits_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
       }
   }
 

@@ -28,6 +28,15 @@ __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
+// fp32 -> bf16 bits, round to nearest even.  A NaN stays a quiet NaN: the plain rounding add
+// carries a NaN with high mantissa bits (e.g. 0x7FFFFFFF) into the exponent / sign (-> -0 or
+// inf) and would hide a non-finite weight or feature from the C3 hazard and the guards.
+__device__ __forceinline__ unsigned bf16_bits_rne(float f) {
+  const unsigned u = __float_as_uint(f);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (u >> 16) | 0x40u;
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
 // Wave64 reductions (CDNA wavefront is 64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

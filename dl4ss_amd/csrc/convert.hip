@@ -22,8 +22,7 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, unsigned short* 
     *reinterpret_cast<uint2*>(y + i) = make_uint2(lo, hi);
   } else {
     for (long long j = i; j < n; ++j) {
-      const unsigned u = __float_as_uint(x[j]);
-      y[j] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+      y[j] = (unsigned short)bf16_bits_rne(x[j]);
     }
   }
 }
@@ -35,8 +34,7 @@ __global__ void f32_to_bf16_2d_kernel(const float* __restrict__ x, long long ldx
   const long long r = i / ldy, c = i - r * ldy;
   unsigned short o = 0;
   if (c < cols) {
-    const unsigned u = __float_as_uint(x[r * ldx + c]);
-    o = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    o = (unsigned short)bf16_bits_rne(x[r * ldx + c]);
   }
   y[i] = o;
 }
@@ -58,10 +56,7 @@ struct CvtSegs {
 // (16-B aligned x and y rows): each lane converts 8-column chunks with two 16-B loads and one 16-B
 // store (a workgroup per row with one 4-B pair per thread ran at ~2.8 TB/s); otherwise pairs of
 // columns as one 4-B word (ldy even).  Columns >= cols are zero either way.
-__device__ __forceinline__ unsigned bf16_bits(float f) {
-  const unsigned u = __float_as_uint(f);
-  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-}
+__device__ __forceinline__ unsigned bf16_bits(float f) { return bf16_bits_rne(f); }
 __global__ __launch_bounds__(256) void f32_to_bf16_multi_kernel(CvtSegs sg) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= sg.row0[sg.n]) return;

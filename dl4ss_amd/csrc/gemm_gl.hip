@@ -248,8 +248,7 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
         unsigned short hb[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const unsigned u = __float_as_uint(xs[c]);
-          hb[c] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+          hb[c] = (unsigned short)bf16_bits_rne(xs[c]);
         }
         if (col + 4 <= N) {  // two 4-B stores: ldc is only required even (V rows of F * E = 6450)
           *reinterpret_cast<unsigned*>(cb) = hb[0] | ((unsigned)hb[1] << 16);
@@ -331,8 +330,7 @@ __device__ __forceinline__ void store4(float4 x, int row, int col, int N, float*
     unsigned short hb[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const unsigned u = __float_as_uint(xs[c]);
-      hb[c] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+      hb[c] = (unsigned short)bf16_bits_rne(xs[c]);
     }
     if (col + 4 <= N) {  // two 4-B stores: ldc is only required even (V rows of F * E = 6450)
       *reinterpret_cast<unsigned*>(cb) = hb[0] | ((unsigned)hb[1] << 16);

@@ -9,6 +9,12 @@
 //
 // Layout: raw (B, K, N) fp32 -> scaled sources (B, K, N) and mixture (B, N), each
 // contiguous so that one STFT launch covers all sources and one all mixtures.
+//
+// Train-time augmentation (config.AUGMENT_DATA): after the normalisation each source is
+// rotated by a per-source shift s, signal = np.append(signal[s:], signal[:s]), BEFORE the
+// zero-padding, i.e. over the source's own length len (TDAA_beta/predata_fromList.py:150-151,
+// TDAA_beta/predata_fromList_cRM_123.py:198-200).  Mean and peak are rotation-invariant, so the
+// statistics pass is unchanged and the mixing pass reads x[(i + s) mod len].
 #include "common.h"
 
 namespace {
@@ -70,11 +76,14 @@ __global__ __launch_bounds__(256) void source_stats_kernel(const float* __restri
 // grid (ceil(N/1024), B): normalise, gain, write sources and their sum
 __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw, const SrcPart* __restrict__ part,
                                                   const float* __restrict__ gains, const int* __restrict__ lens,
-                                                  int K, int N, float* __restrict__ out_src,
+                                                  const int* __restrict__ shifts, int K, int N,
+                                                  float* __restrict__ out_src,
                                                   float* __restrict__ out_mix) {
   const int b = blockIdx.y;
-  // per-source (mean, 1 / max|x - mean|) from the NSPLIT partials, fixed order
+  // per-source (mean, 1 / max|x - mean|) from the NSPLIT partials, fixed order; the shift
+  // reduced modulo the source's length (0 = no rotation)
   __shared__ float2 sstat[16];
+  __shared__ int sshift[16];
   if (threadIdx.x < K) {
     const long long src = (long long)b * K + threadIdx.x;
     const int len = lens ? min(max(lens[src], 0), N) : N;
@@ -89,6 +98,12 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
     const float meanf = len > 0 ? (float)(s / len) : 0.f;
     const float pk = len > 0 ? fmaxf(mx - meanf, meanf - mn) : 0.f;
     sstat[threadIdx.x] = make_float2(meanf, pk > 0.f ? 1.0f / pk : 0.f);
+    int sh = 0;
+    if (shifts && len > 0) {
+      sh = shifts[src] % len;
+      if (sh < 0) sh += len;
+    }
+    sshift[threadIdx.x] = sh;
   }
   __syncthreads();
   const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
@@ -101,7 +116,20 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
     const float* x = raw + src * N;
     float* o = out_src + ((long long)b * K + k) * N;
     const int len = lens ? min(max(lens[src], 0), N) : N;  // zero beyond the source's own length
-    if (i + 3 < len && ((N & 3) == 0)) {
+    const int sh = sshift[k];
+    if (sh != 0) {  // rotated: out[i] = x[(i + sh) mod len] for i < len
+      float* a = &acc.x;
+      for (int q = 0; q < 4 && i + q < N; ++q) {
+        float v = 0.0f;
+        if (i + q < len) {
+          int j = i + q + sh;
+          j -= j >= len ? len : 0;
+          v = (x[j] - st.x) * g;
+        }
+        o[i + q] = v;
+        a[q] += v;
+      }
+    } else if (i + 3 < len && ((N & 3) == 0)) {
       float4 v = *reinterpret_cast<const float4*>(x + i);
       v.x = (v.x - st.x) * g; v.y = (v.y - st.x) * g; v.z = (v.z - st.x) * g; v.w = (v.w - st.x) * g;
       *reinterpret_cast<float4*>(o + i) = v;
@@ -126,8 +154,9 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
 
 }  // namespace
 
-DL4SS_API int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gains, int B, int K, int N,
-                                   float* stats_ws, float* out_src, float* out_mix, void* stream) {
+DL4SS_API int dl4ss_mix_sources_rot(const float* raw, const int* lengths, const int* shifts, const float* gains,
+                                    int B, int K, int N, float* stats_ws, float* out_src, float* out_mix,
+                                    void* stream) {
   DL4SS_REQUIRE(B >= 0 && K >= 1 && K <= 16 && N > 0);
   if (B == 0) return 0;  // empty batch: no-op (an empty tensor's pointer may be null)
   DL4SS_REQUIRE(raw && gains && out_src && out_mix && stats_ws);
@@ -135,10 +164,15 @@ DL4SS_API int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const f
   SrcPart* part = reinterpret_cast<SrcPart*>(stats_ws);
   hipLaunchKernelGGL(source_stats_kernel, dim3(B * K, NSPLIT), dim3(256), 0, as_stream(stream), raw, N, lengths, part);
   DL4SS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(mix_kernel, dim3(cdiv(N, 1024), B), dim3(256), 0, as_stream(stream), raw, part, gains, lengths, K,
-                     N, out_src, out_mix);
+  hipLaunchKernelGGL(mix_kernel, dim3(cdiv(N, 1024), B), dim3(256), 0, as_stream(stream), raw, part, gains, lengths,
+                     shifts, K, N, out_src, out_mix);
   DL4SS_CHECK_LAUNCH();
   return 0;
+}
+
+DL4SS_API int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gains, int B, int K, int N,
+                                   float* stats_ws, float* out_src, float* out_mix, void* stream) {
+  return dl4ss_mix_sources_rot(raw, lengths, nullptr, gains, B, K, N, stats_ws, out_src, out_mix, stream);
 }
 
 DL4SS_API int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N, float* stats_ws,

@@ -242,14 +242,14 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ A
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2s,
-                                                   int* __restrict__ status, const float* __restrict__ dp_flag,
-                                                   float* __restrict__ loss) {
+                                                   const int* __restrict__ status, int* __restrict__ refused,
+                                                   const float* __restrict__ dp_flag, float* __restrict__ loss) {
   // refuse the update when a recurrence hand-off of this step timed out on this rank
   // (status[0]) or on any data-parallel peer (dp_flag: the all-reduced status flag)
   if ((status && status[0]) || (dp_flag && dp_flag[0] != 0.f)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       if (loss) loss[0] = __builtin_nanf("");
-      if (status) status[1] += 1;  // refused-update count: the host rolls its step count back by it
+      if (refused) refused[0] += 1;  // refused-update count: the host rolls its step count back by it
     }
     return;
   }
@@ -339,23 +339,10 @@ DL4SS_API int dl4ss_colsum(const float* A, long long lda, int M, int N, float* o
   return 0;
 }
 
-DL4SS_API int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-                                    float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
-                                    void* stream);
-
-DL4SS_API int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-                         float beta2, float eps, int step, void* stream) {
-  return dl4ss_adam_guarded_dp(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, nullptr, nullptr, stream);
-}
-
-DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-                                 float beta2, float eps, int step, int* status, float* loss, void* stream) {
-  return dl4ss_adam_guarded_dp(p, g, m, v, n, lr, beta1, beta2, eps, step, status, nullptr, loss, stream);
-}
-
-DL4SS_API int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
-                                    float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
-                                    void* stream) {
+namespace {
+int adam_launch(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                float eps, int step, const int* status, int* refused, const float* dp_flag, float* loss,
+                void* stream) {
   DL4SS_REQUIRE(p && g && m && v && n >= 0 && step >= 1);
   if (n == 0) return 0;
   // bias corrections in double on the host, as torch computes them in Python floats
@@ -363,9 +350,29 @@ DL4SS_API int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   const unsigned grid = (unsigned)min(8192LL, (n / 4 + 255) / 256 + 1);
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr, beta1, beta2, eps,
-                     bc1, bc2s, status, dp_flag, loss);
+                     bc1, bc2s, status, refused, dp_flag, loss);
   DL4SS_CHECK_LAUNCH();
   return 0;
+}
+}  // namespace
+
+DL4SS_API int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                         float beta2, float eps, int step, void* stream) {
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+// status: ONE int (the hand-off word), read only; a refusal shows as loss[0] = NaN
+DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                                 float beta2, float eps, int step, int* status, float* loss, void* stream) {
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, nullptr, nullptr, loss, stream);
+}
+
+// status: 2 ints {hand-off word, refused-update count}; the count is incremented per refusal
+DL4SS_API int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                                    float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
+                                    void* stream) {
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, status ? status + 1 : nullptr, dp_flag, loss,
+                     stream);
 }
 
 __global__ void status_flag_kernel(const int* __restrict__ status, float* __restrict__ flag) {

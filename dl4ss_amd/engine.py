@@ -221,7 +221,7 @@ class SepTrainer:
             self.dPreb = torch.zeros(BT, p8(F * net.E), **bf)
             # gemm_gl split-K slabs (the largest split of _backward_fast)
             FE_ = F * net.E
-            gl_need = max(_lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, FE_, 3, 1),
+            gl_need = max(_lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, FE_, max(1, self.dh_split), 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", FE_, 2 * H, BT, 2, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", 2 * NGH, 2 * H, BT, 4, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", NGH, H, BT, 8, 2))

@@ -61,10 +61,12 @@ def istft(S, conj=False, out=None):
     return out
 
 
-def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=None):
+def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=None, shifts=None):
     """raw (B, K, N) fp32 sources, gains (B, K) fp32 -> (scaled sources (B, K, N),
     mixture (B, N)) -- normalise, gain, sum.  lengths (B, K) int32: each
-    source's own length (normalised over it, zero beyond; list-file wavs)."""
+    source's own length (normalised over it, zero beyond; list-file wavs).  shifts (B, K)
+    int32: the AUGMENT_DATA rotation np.append(x[s:], x[:s]) over the source's own length,
+    after the normalisation (TDAA_beta/predata_fromList_cRM_123.py:198-200)."""
     _f32c(raw, "mix_sources")
     _f32c(gains, "mix_sources(gains)")
     B, K, N = raw.shape
@@ -78,8 +80,11 @@ def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=N
         stats_ws = torch.empty(B * K * 32, device=raw.device, dtype=torch.float32)
     if lengths is not None and (lengths.dtype != torch.int32 or tuple(lengths.shape) != (B, K)):
         raise RuntimeError("mix_sources: lengths must be (B, K) int32")
-    _lib.call("dl4ss_mix_sources_ex", _lib.ptr(raw), _lib.ptr(lengths), _lib.ptr(gains), B, K, N, _lib.ptr(stats_ws),
-              _lib.ptr(out_src), _lib.ptr(out_mix), _lib.stream_ptr())
+    if shifts is not None and (shifts.dtype != torch.int32 or tuple(shifts.shape) != (B, K) or not shifts.is_cuda
+                               or not shifts.is_contiguous()):
+        raise RuntimeError("mix_sources: shifts must be a contiguous (B, K) int32 CUDA tensor")
+    _lib.call("dl4ss_mix_sources_rot", _lib.ptr(raw), _lib.ptr(lengths), _lib.ptr(shifts), _lib.ptr(gains), B, K, N,
+              _lib.ptr(stats_ws), _lib.ptr(out_src), _lib.ptr(out_mix), _lib.stream_ptr())
     return out_src, out_mix
 
 
@@ -227,9 +232,19 @@ class GroupedGemm:
                 raise RuntimeError("GroupedGemm: every problem needs the same transA / transB")
             M, K = (A.shape[1], A.shape[0]) if ta else (A.shape[0], A.shape[1])
             Kb, N = (B.shape[1], B.shape[0]) if tb else (B.shape[0], B.shape[1])
+            shapeA, shapeB = (M, K), (Kb, N)
             M, N, K = p.get("M", M), p.get("N", N), p.get("K", K)
             if p.get("K") is None and K != Kb:
                 raise RuntimeError(f"GroupedGemm: inner dims differ ({K} vs {Kb})")
+            if not any(x in p for x in ("M", "N", "K")):
+                if tuple(out.shape) != (M, N):
+                    raise RuntimeError(f"GroupedGemm: out shape {tuple(out.shape)} != {(M, N)}")
+            # explicit M / N / K: the kernel and its combine must stay inside every view
+            # (the argument arrays are frozen here, so a wrong view would be written past silently)
+            if not (0 < M <= shapeA[0] and 0 < K <= shapeA[1] and K <= shapeB[0] and 0 < N <= shapeB[1]):
+                raise RuntimeError(f"GroupedGemm: M, N, K = {(M, N, K)} exceed the operand views")
+            if not (out.shape[0] >= M and out.shape[1] >= N and out.stride(0) >= N):
+                raise RuntimeError(f"GroupedGemm: out view {tuple(out.shape)} (ldc {out.stride(0)}) < {(M, N)}")
             dims.append((M, N, K))
             self._keep += [A, B, out]
         Iv = lambda xs: (ctypes.c_int * n)(*xs)
@@ -278,8 +293,8 @@ def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, 
     """torch Adam step on flat buffers; with ``status`` (the recurrence hand-off status word,
     2 ints: {timed out, refused-update count}) the update is refused on device when a hand-off
     of this step timed out, loss[0] is set to NaN and status[1] counts the refusal
-    (dl4ss_adam_guarded); with ``dp_flag`` (the all-reduced status flag behind the flat
-    gradient) also when a data-parallel peer's hand-off timed out (dl4ss_adam_guarded_dp)."""
+    (dl4ss_adam_guarded_dp's 2-int status form); with ``dp_flag`` (the all-reduced status flag
+    behind the flat gradient) also when a data-parallel peer's hand-off timed out."""
     for t in (p, g, m, v):
         _f32c(t, "adam")
     if status is not None and status.numel() < 2:

@@ -15,8 +15,10 @@ Restates the real-data input of ``TDAA_beta/predata_fromList_cRM_123.py:90-255``
 * source wav = ``data_path/{train | eval_test}/<spk>/<sample>.wav`` (``:176-180``: 'test'
   reads eval_test, every other split train), first channel only (``:182-183``), cropped to
   MAX_LEN (``:187-188``);
-* per source on the GPU (``dl4ss_mix_sources_ex``): mean removal and peak normalisation over
-  the source's own length, zero-padding to MAX_LEN, gain 10^(dB/20), sum (``:192-237``);
+* per source on the GPU (``dl4ss_mix_sources_rot``): mean removal and peak normalisation over
+  the source's own length, on the train split with AUGMENT_DATA a rotation by a shift drawn
+  ``random.sample(range(len), 1)[0]`` per source (``:197-200``), zero-padding to MAX_LEN, gain
+  10^(dB/20), sum (``:192-237``);
   then the STFTs (mixture complex + magnitude, sources magnitude or complex) -- the batch
   the reference builds with librosa on the host (``:209-255``).
 
@@ -122,9 +124,10 @@ class ListBatches:
     Each batch: raw (B, k, max_len) float32 (cropped, zero-padded, NOT yet normalised),
     lengths (B, k) int32, gains (B, k) float32 = 10^(dB/20), speakers / sample names per
     row.  ``batch_total = len(lines) // B`` batches per epoch (the reference's
-    ``batch_mix``); ``shuffle`` reorders the lines once per epoch (config.SHUFFLE_BATCH)."""
+    ``batch_mix``); ``shuffle`` reorders the lines once per epoch (config.SHUFFLE_BATCH).
+    augment: draw each source's rotation (shifts (B, k) int32 in the batch, else None)."""
 
-    def __init__(self, list_path, data_path, split, batch, max_len, shuffle=False, seed=1):
+    def __init__(self, list_path, data_path, split, batch, max_len, shuffle=False, seed=1, augment=False):
         with open(list_path) as f:
             self.lines = [l for l in f.readlines() if l.strip()]
         self.items = [parse_line(l) for l in self.lines]
@@ -134,18 +137,22 @@ class ListBatches:
         self.k = ks.pop()
         self.data_path, self.split, self.B, self.max_len = data_path, split, batch, max_len
         self.shuffle, self.rng = shuffle, random.Random(seed)
+        self.augment = augment
         self.batch_total = len(self.items) // batch
 
     def load(self, item):
         raw = np.zeros((self.k, self.max_len), dtype=np.float32)
         lens = np.zeros(self.k, dtype=np.int32)
+        shifts = np.zeros(self.k, dtype=np.int32)
         for j, (spk, name, _) in enumerate(item):
             x, rate = read_wav(source_path(self.data_path, self.split, spk, name))
             x = resample(x, rate)[:self.max_len]
             raw[j, :len(x)] = x
             lens[j] = len(x)
+            if self.augment:  # predata_fromList_cRM_123.py:198-199, drawn per source in line order
+                shifts[j] = random.sample(range(len(x)), 1)[0]
         gains = np.array([10.0 ** (db / 20.0) for _, _, db in item], dtype=np.float32)
-        return raw, lens, gains
+        return raw, lens, gains, shifts
 
     def __iter__(self):
         order = list(range(len(self.items)))
@@ -156,7 +163,8 @@ class ListBatches:
             loaded = [self.load(it) for it in rows]
             yield dict(raw=np.stack([l[0] for l in loaded]), lengths=np.stack([l[1] for l in loaded]),
                        gains=np.stack([l[2] for l in loaded]), speakers=[[s for s, _, _ in it] for it in rows],
-                       names=[[n for _, n, _ in it] for it in rows])
+                       names=[[n for _, n, _ in it] for it in rows],
+                       shifts=np.stack([l[3] for l in loaded]) if self.augment else None)
 
 
 def features(batch, device, complex_sources=False):
@@ -166,8 +174,10 @@ def features(batch, device, complex_sources=False):
     raw = torch.from_numpy(batch["raw"]).to(device)
     gains = torch.from_numpy(batch["gains"]).to(device)
     lens = torch.from_numpy(batch["lengths"]).to(device)
+    shifts = batch.get("shifts")
+    shifts = None if shifts is None else torch.from_numpy(np.ascontiguousarray(shifts, np.int32)).to(device)
     B, K, N = raw.shape
-    src, mix = ops.mix_sources(raw, gains, lengths=lens)
+    src, mix = ops.mix_sources(raw, gains, lengths=lens, shifts=shifts)
     Xc, Xm = ops.stft(mix, complex_out=True, mag_out=True)
     if complex_sources:
         Sc, _ = ops.stft(src.view(B * K, N), complex_out=True, mag_out=False)

@@ -64,6 +64,12 @@ int dl4ss_mix_sources(const float* raw, const float* gains, int B, int K, int N,
  * (TDAA_beta/predata_fromList_cRM_123.py:186-201: crop, normalise, then zero-pad). */
 int dl4ss_mix_sources_ex(const float* raw, const int* lengths, const float* gains, int B, int K, int N,
                          float* stats_ws, float* out_src, float* out_mix, void* stream);
+/* As dl4ss_mix_sources_ex, plus the train-split augmentation of the list loaders: source s is
+ * rotated by shifts[s] (B*K int32; NULL = none; taken modulo the source's length) after the
+ * normalisation and before the zero-padding -- np.append(x[s:], x[:s]) over the source's own
+ * length (TDAA_beta/predata_fromList.py:150-151, predata_fromList_cRM_123.py:198-200). */
+int dl4ss_mix_sources_rot(const float* raw, const int* lengths, const int* shifts, const float* gains, int B, int K,
+                          int N, float* stats_ws, float* out_src, float* out_mix, void* stream);
 
 /* ---- dense contractions (MFMA) ------------------------------------------ */
 enum { DL4SS_EPI_NONE = 0, DL4SS_EPI_TANH = 1, DL4SS_EPI_TANH_BF16 = 2 /* tanh, C written as bf16 */ };
@@ -252,14 +258,16 @@ int dl4ss_colsum(const float* A, long long lda, int M, int N, float* out, void* 
 int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
                float eps, int step, void* stream);
 /* dl4ss_adam that refuses a step computed from a timed-out recurrence: when status[0] != 0
- * (a BiRNN hand-off of this step timed out) no parameter or moment changes, loss[0] (if not
- * NULL) is set to NaN, so the step's loss read by the caller reports it, and status[1] (the
- * refused-update count; status points at 2 ints) is incremented. */
+ * (a BiRNN hand-off of this step timed out) no parameter or moment changes and loss[0] (if not
+ * NULL) is set to NaN, so the step's loss read by the caller reports it.  status is ONE int,
+ * only read. */
 int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                        float beta2, float eps, int step, int* status, float* loss, void* stream);
 /* dl4ss_adam_guarded that also refuses when *dp_flag != 0: the data-parallel form, where
  * dp_flag is the slot behind the flat gradient that dl4ss_status_flag filled from each rank's
- * status and the gradient all-reduce combined, so every rank refuses the same steps. */
+ * status and the gradient all-reduce combined, so every rank refuses the same steps.  Here
+ * status points at 2 ints: {hand-off word, refused-update count}; the count is incremented on
+ * every refusal (the host rolls its Adam step count back by it). */
 int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                           float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
                           void* stream);

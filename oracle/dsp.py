@@ -17,8 +17,15 @@ Restates the third-party arithmetic the reference calls at its data boundary:
 * Source preprocessing / mixing:
   ``Torch_multi/predata_multiAims_dB.py:123-197`` (2-spk dB gain on one random
   channel), ``Torch_multi/predata_multiAims_3dB.py:132-145,192-217`` (3-spk
-  gains), ``TDAA_beta/predata_fromList_cRM_123.py:174-237`` (list dB gains).
+  gains), ``TDAA_beta/predata_fromList_cRM_123.py:174-237`` (list dB gains), and the
+  train-split AUGMENT_DATA rotation of the list loaders
+  (``TDAA_beta/predata_fromList.py:150-151``, ``predata_fromList_cRM_123.py:198-200``) beside
+  the Torch_multi loaders' broadcast form of the same line
+  (``Torch_multi/predata_multiAims_dB.py:164-166``, ``predata_multiAims_3dB.py:179-181``).
+  Pinned to the reference's own statements by ``tests/golden/ref_r1_augment.npz``.
 """
+import math
+
 import numpy as np
 
 N_FFT = 256
@@ -103,14 +110,68 @@ def istft(S_ft, hop=HOP, conj=False, dtype=np.float32):
 # R1: preprocessing and mixing
 # ----------------------------------------------------------------------------
 
-def normalise_source(x, max_len):
-    """Crop, x -= mean, x /= max|x|, zero-pad (predata_multiAims_dB.py:156-175)."""
+def normalise_source(x, max_len, shift=None, broadcast=False):
+    """Crop, x -= mean, x /= max|x|, [rotate], zero-pad (predata_multiAims_dB.py:156-175).
+
+    shift: the list loaders' AUGMENT_DATA branch on the train split,
+    ``signal = np.append(signal[s:], signal[:s])`` with s drawn from range(len(signal))
+    -- a rotation over the source's OWN (cropped) length, before the zero-padding
+    (predata_fromList.py:150-151, predata_fromList_cRM_123.py:198-200).  broadcast=True:
+    the Torch_multi loaders' form of that line instead (``augment_torch_multi``)."""
     x = np.asarray(x, dtype=np.float64)[:max_len].copy()
     x -= np.mean(x)
     x /= np.max(np.abs(x))
+    if shift is not None:
+        x = augment_torch_multi(x, shift) if broadcast else np.append(x[shift:], x[:shift])
     if x.shape[0] < max_len:
         x = np.append(x, np.zeros(max_len - x.shape[0]))
     return x
+
+
+def augment_torch_multi(x, shift):
+    """Torch_multi/predata_multiAims_dB.py:164-166 (and _3dB.py:179-181): the same
+    augmentation written ``signal[s:] + signal[:s]`` -- a numpy broadcast of two slices of
+    lengths len-s and s, which raises ValueError unless one of them has length 1 or both
+    are equal (s in {1, len-1, len/2}); then it is an elementwise SUM, not a rotation."""
+    x = np.asarray(x, dtype=np.float64)
+    return x[shift:] + x[:shift]
+
+
+def mix_sources_f32(raw, gains, lengths=None, shifts=None):
+    """fp32 restatement of the mixing kernel's arithmetic (``mixing.hip``), for bit-exact
+    comparison of the index work (crop length, rotation, zero-padding) and of the values:
+
+    mean = fp32(sum_fp64 / len) (the sum correctly rounded here, a fixed tree there -- they
+    agree after the fp32 rounding unless the fp64 mean sits within ~1e-12 relative of an fp32
+    rounding boundary); peak = max(max x - mean, mean - min x) in fp32 (= max |fl(x - mean)|,
+    fp32 subtraction being monotonic); g = fp32(gain * fp32(1 / peak));
+    out[i] = fp32(fp32(x[(i + s) mod len] - mean) * g) for i < len, 0 beyond;
+    mixture = sum over k in order 0..K-1 in fp32.
+
+    raw (B, K, N) float32, gains (B, K) float32, lengths / shifts (B, K) int or None."""
+    raw = np.asarray(raw, np.float32)
+    B, K, N = raw.shape
+    gains = np.asarray(gains, np.float32)
+    src = np.zeros((B, K, N), np.float32)
+    for b in range(B):
+        for k in range(K):
+            ln = N if lengths is None else int(min(max(int(lengths[b][k]), 0), N))
+            if ln == 0:
+                continue
+            x = raw[b, k, :ln]
+            mean = np.float32(math.fsum(x.astype(np.float64).tolist()) / ln)
+            pk = max(np.float32(x.max() - mean), np.float32(mean - x.min()))
+            inv = np.float32(1.0) / pk if pk > 0 else np.float32(0.0)
+            g = np.float32(gains[b, k] * inv)
+            y = (x - mean).astype(np.float32) * g
+            s = 0 if shifts is None else int(shifts[b][k]) % ln
+            if s:
+                y = np.append(y[s:], y[:s])
+            src[b, k, :ln] = y
+    mix = np.zeros((B, N), np.float32)
+    for k in range(K):
+        mix = (mix + src[:, k]).astype(np.float32)
+    return src, mix
 
 
 def mix_sources(sources, gains):

@@ -28,6 +28,10 @@ ref_c3_crm.npz       TDAA_beta/main_run_sstune_cRM_EvalVer.py:645-752 (cRM branc
                      inverse compression :688, complex MSE :720-743)
 ref_c4_3spk.npz      Torch_multi/main_run_multi_selfSS_dB.py:457-532 (3 speakers)
 ref_inception_keys.npz  state_dict names / shapes of Torch_multi/myNet.py's Inception3
+ref_r1_augment.npz   the per-source preprocessing statements of the four loaders
+                     (TDAA_beta/predata_fromList.py:135-154, predata_fromList_cRM_123.py:183-202,
+                     Torch_multi/predata_multiAims_dB.py:149-168, predata_multiAims_3dB.py:164-183):
+                     crop, mean removal, peak normalisation, the AUGMENT_DATA shift, zero-pad
 ref_small.npz        top_k_mask (EvalVer.py:390-405, GRID.py:227-244), multi_label_vector
                      (TDAA_beta/test_multi_labels_speech.py:287-300), LR schedules
                      (EvalVer.py:570-575, selfSS_dB.py:442-444)
@@ -472,6 +476,72 @@ def make_c4(B=2, K=3, N=2048, seed=14, wseed=104):
     return out
 
 
+# ----------------------------------------------------------------------------- R1 augmentation
+R1_LOADERS = {  # tag: (file, line of `for k,spk in enumerate(aim_spk_k):`, statements kept, train-split guard)
+    "fromlist": ("TDAA_beta/predata_fromList.py", 126, (135, 154), True),
+    "fromlist_crm": ("TDAA_beta/predata_fromList_cRM_123.py", 174, (183, 202), True),
+    "multiaims_db": ("Torch_multi/predata_multiAims_dB.py", 131, (149, 168), False),
+    "multiaims_3db": ("Torch_multi/predata_multiAims_3dB.py", 146, (164, 183), False),
+}
+
+
+class _ShiftDraw:
+    """Stands in for the ``random`` module at the shift line: ``random.sample(range(n), 1)``
+    returns the chosen shift and records n (the population the reference draws from)."""
+
+    def __init__(self, shift):
+        self.shift, self.pop = shift, None
+
+    def sample(self, population, k):
+        assert k == 1
+        self.pop = len(population)
+        assert 0 <= self.shift < self.pop
+        return [self.shift]
+
+
+def make_r1(seed=16, max_len=1000):
+    out = {}
+    r = np.random.Generator(np.random.PCG64(seed))
+    # wav-like float64 inputs (sf.read of 16-bit PCM: int / 32768) of full, short and long length
+    sigs = [np.round(r.normal(0.0, 0.1, size=n) * 32768).clip(-32768, 32767) / 32768.0 + 0.01
+            for n in (max_len, 625, 1250, 2)]
+    for tag, (rel, loop_line, keep, guarded) in R1_LOADERS.items():
+        check_line(rel, keep[0] - 1, "signal,rate=sf.read(spk_speech_path)")
+        check_line(rel, keep[1] + 1, "signal=np.append(signal,np.zeros(config.MAX_LEN-signal.shape[0]))")
+        code = loop_body(rel, loop_line, [keep])
+        ci = 0
+        for si, x in enumerate(sigs):
+            n = min(len(x), max_len)
+            shifts = sorted({0, 1, n - 1, n // 2, int(r.integers(0, n)), int(r.integers(0, n))})
+            for aug, split in [(True, "train"), (True, "valid"), (False, "train")]:
+                for sh in (shifts if aug else [0]):
+                    cfg = types.SimpleNamespace(MAX_LEN=max_len, FRAME_RATE=8000, AUGMENT_DATA=aug)
+                    draw = _ShiftDraw(sh)
+                    ns = dict(np=np, config=cfg, random=draw, signal=x.copy(), rate=8000, train_or_test=split,
+                              mix_len=0)
+                    key = f"r1/{tag}/{ci}"
+                    out[f"{key}/sig"] = np.int64(si)
+                    out[f"{key}/aug"] = np.bool_(aug)
+                    out[f"{key}/split"] = np.array(split)
+                    out[f"{key}/shift"] = np.int64(sh)
+                    try:
+                        exec(code, ns)
+                        out[f"{key}/out"] = np.asarray(ns["signal"], np.float64)
+                        out[f"{key}/error"] = np.array("")
+                    except ValueError as e:
+                        out[f"{key}/out"] = np.zeros(0)
+                        out[f"{key}/error"] = np.array(str(e))
+                    out[f"{key}/drawn_from"] = np.int64(-1 if draw.pop is None else draw.pop)
+                    ci += 1
+        out[f"r1/{tag}/count"] = np.int64(ci)
+        out[f"r1/{tag}/guarded"] = np.bool_(guarded)
+    for si, x in enumerate(sigs):
+        out[f"r1/sig/{si}"] = x
+    out["r1/max_len"] = np.int64(max_len)
+    np.savez_compressed(os.path.join(HERE, "ref_r1_augment.npz"), **out)
+    return out
+
+
 # ----------------------------------------------------------------------------- small pieces
 class _FakeOpt:
     def __init__(self, lr):
@@ -567,8 +637,9 @@ def make_inception():
 def main():
     torch.manual_seed(1)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    which = sys.argv[1:] or ["small", "c2", "c1", "c3", "c4", "inception"]
-    fns = dict(small=make_small, c2=make_c2, c1=make_c1, c3=make_c3, c4=make_c4, inception=make_inception)
+    which = sys.argv[1:] or ["small", "c2", "c1", "c3", "c4", "inception", "r1"]
+    fns = dict(small=make_small, c2=make_c2, c1=make_c1, c3=make_c3, c4=make_c4, inception=make_inception,
+               r1=make_r1)
     for w in which:
         sink = io.StringIO()
         with contextlib.redirect_stdout(sink):

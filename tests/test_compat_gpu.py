@@ -119,8 +119,15 @@ def test_prepare_data_contract_and_features(dev):
     import predata_multiAims_dB as pdb
 
     c = pdb.config  # config_WSJ0_dB (predata_multiAims_dB.py:7), a copy of config's constants
-    bs, ml = c.BATCH_SIZE, c.MAX_LEN
+    bs, ml, aug = c.BATCH_SIZE, c.MAX_LEN, c.AUGMENT_DATA
     c.BATCH_SIZE, c.MAX_LEN = 3, 8000
+    # with config_WSJ0_dB.py:112's AUGMENT_DATA = True the reference loader stops at its first
+    # source (signal[s:] + signal[:s], predata_multiAims_dB.py:166); so does this one
+    import random
+    random.seed(4)
+    with pytest.raises(ValueError, match="could not be broadcast"):
+        next(pdb.prepare_data('once', 'train'))
+    c.AUGMENT_DATA = False
     try:
         g = pdb.prepare_data('global', 'train')
         spk, d2i, i2d, T, F, frames, n = next(g)
@@ -147,7 +154,7 @@ def test_prepare_data_contract_and_features(dev):
                 # peak-normalised then gained: max|x| is 1 or the dB gain 10^(5/20 u) <= 1.78
                 assert 0.999 < np.abs(w).max() < 1.7783
     finally:
-        c.BATCH_SIZE, c.MAX_LEN = bs, ml
+        c.BATCH_SIZE, c.MAX_LEN, c.AUGMENT_DATA = bs, ml, aug
 
 
 def test_fromlist_crm_loader(dev):

@@ -38,3 +38,34 @@ def test_f32_to_bf16_2d_multi_matches_torch(dev):
         assert torch.equal(y[:, :cols].view(torch.int16), ref.view(torch.int16)), (rows, cols)
         if ldy > cols:
             assert bool((y[:, cols:].float() == 0).all()), (rows, cols)
+
+
+def test_bf16_conversions_keep_nan_payloads_nan(dev):
+    """round-to-nearest-even by integer add carried a NaN with high mantissa bits
+    (0x7FFFFFFF, 0xFFFFFFFF) into the sign / exponent (-> -0 / +0 / inf).  Every conversion path
+    must keep NaN a NaN, and inf / finite values as torch rounds them."""
+    from dl4ss_amd import ops
+
+    bits = torch.tensor([0x7FFFFFFF, -1, 0x7F800001, 0x7FC00000, 0x7F800000, -8388608, 0x3F800000, 0x7F7FFFFF] * 4,
+                        dtype=torch.int32)
+    x = bits.view(torch.float32).to(dev)
+    ref = x.cpu().to(torch.bfloat16)
+    for n in (32, 30):  # the flat path: 4-wide, then with a scalar tail
+        y = ops.to_bf16(x[:n].contiguous()).cpu()
+        r = ref[:n]
+        assert torch.equal(torch.isnan(y), torch.isnan(r))
+        fin = ~torch.isnan(r)
+        assert torch.equal(y[fin].view(torch.int16), r[fin].view(torch.int16))
+    # the 2-D multi-segment path (8-column chunks and the 4-B pair path)
+    P = ctypes.c_void_p
+    x2 = x.view(4, 8).contiguous()
+    for ldy in (8, 10):
+        y2 = torch.zeros(4, ldy, device=dev, dtype=torch.bfloat16)
+        _lib.call("dl4ss_f32_to_bf16_2d_multi", 1, (P * 1)(x2.data_ptr()), (ctypes.c_longlong * 1)(8),
+                  (ctypes.c_int * 1)(4), (ctypes.c_int * 1)(8), (P * 1)(y2.data_ptr()), (ctypes.c_longlong * 1)(ldy),
+                  _lib.stream_ptr())
+        torch.cuda.synchronize()
+        y2 = y2[:, :8].cpu().reshape(-1)
+        assert torch.equal(torch.isnan(y2), torch.isnan(ref))
+        fin = ~torch.isnan(ref)
+        assert torch.equal(y2[fin].view(torch.int16), ref[fin].view(torch.int16))

@@ -147,11 +147,13 @@ def test_grid_driver_recursive_extraction(dev):
     import config_WSJ0_dB as cfg
     import main_run_multi_selfSS_recuReal_GRID as drv
 
-    saved = (cfg.BATCH_SIZE, cfg.MAX_LEN)
-    cfg.BATCH_SIZE, cfg.MAX_LEN = 1, 4000
+    # the Torch_multi loader this driver imports runs only with AUGMENT_DATA off
+    # (predata_multiAims_dB.py:166, compat._data.torch_multi_augment)
+    saved = (cfg.BATCH_SIZE, cfg.MAX_LEN, cfg.AUGMENT_DATA)
+    cfg.BATCH_SIZE, cfg.MAX_LEN, cfg.AUGMENT_DATA = 1, 4000, False
     try:
         res = drv.main(max_batches=1, log=lambda *a: None)
     finally:
-        cfg.BATCH_SIZE, cfg.MAX_LEN = saved
+        cfg.BATCH_SIZE, cfg.MAX_LEN, cfg.AUGMENT_DATA = saved
     names = res[0][0]
     assert len(names) == 2 and names[0] is not None and names[0] != names[1]

@@ -76,3 +76,18 @@ def test_grouped_rejects_mixed_layouts(dev):
     with pytest.raises(RuntimeError):
         ops.GroupedGemm([dict(A=A, B=A, out=out, transA=True, transB=False),
                          dict(A=A, B=A, out=out, transA=False, transB=False)], dev)
+
+
+def test_grouped_rejects_views_it_would_write_past(dev):
+    """out must be (M, N) (or, with explicit M / N / K, hold them), and explicit
+    dimensions must stay inside the operand views -- the argument arrays are frozen at build."""
+    A = torch.zeros(128, 64, device=dev, dtype=torch.bfloat16)  # transA: K = 128 rows, M = 64
+    B = torch.zeros(128, 32, device=dev, dtype=torch.bfloat16)
+    ok = dict(A=A, B=B, transA=True, transB=False)
+    ops.GroupedGemm([dict(ok, out=torch.zeros(64, 32, device=dev))], dev)
+    with pytest.raises(RuntimeError, match="out shape"):
+        ops.GroupedGemm([dict(ok, out=torch.zeros(32, 32, device=dev))], dev)
+    with pytest.raises(RuntimeError, match="exceed"):
+        ops.GroupedGemm([dict(ok, out=torch.zeros(80, 32, device=dev), M=80)], dev)
+    with pytest.raises(RuntimeError, match="out view"):
+        ops.GroupedGemm([dict(ok, out=torch.zeros(64, 16, device=dev), N=32)], dev)

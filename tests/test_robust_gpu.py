@@ -131,3 +131,41 @@ def test_write_through_handoff_matches_plain(dev, cell):
     assert torch.equal(l0, l1)
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
+
+
+def test_adam_guarded_keeps_its_one_int_status_contract(dev):
+    """the public dl4ss_adam_guarded takes ONE status int (read only); a refusal shows
+    only as loss[0] = NaN.  The word after it must stay untouched (an external caller's 1-int
+    status would otherwise be written past); the 2-int count lives in dl4ss_adam_guarded_dp."""
+    n = 1000
+    p = torch.randn(n, device=dev)
+    g, m, v = torch.randn(n, device=dev), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    p0 = p.clone()
+    st = torch.tensor([1, 777], dtype=torch.int32, device=dev)
+    loss = torch.zeros(1, device=dev)
+    _lib.call("dl4ss_adam_guarded", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), n, 2e-4, 0.9, 0.999, 1e-8, 1,
+              _lib.ptr(st), _lib.ptr(loss), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert st.tolist() == [1, 777] and torch.isnan(loss[0]).item() and torch.equal(p, p0)
+    st[0] = 0
+    _lib.call("dl4ss_adam_guarded", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), n, 2e-4, 0.9, 0.999, 1e-8, 1,
+              _lib.ptr(st), _lib.ptr(loss), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert st.tolist() == [0, 777] and not torch.equal(p, p0)
+    st = torch.tensor([1, 5], dtype=torch.int32, device=dev)
+    ops.adam_(p, g, m, v, 2, status=st, loss=loss)
+    torch.cuda.synchronize()
+    assert st.tolist() == [1, 6]
+
+
+def test_dh_split_above_three_fits_the_workspace(dev, monkeypatch):
+    """the gemm_gl workspace is sized with the trainer's own dH split
+    (DL4SS_DH_SPLIT), so split factors above 3 run instead of raising on the first backward."""
+    B, K, N = 4, 2, 4000
+    monkeypatch.setenv("DL4SS_DH_SPLIT", "6")
+    net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=5)
+    tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+    assert tr.dh_split == 6
+    loss = tr.step(*_batch(dev, B, K, N, 6))
+    tr.check()
+    assert np.isfinite(float(loss[0].item()))
