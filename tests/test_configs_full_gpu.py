@@ -8,8 +8,12 @@ test_step_gpu.py): the HIP step vs the CPU oracle on identical synthetic mixture
       on a repeated batch, HIP vs oracle, on the same seed.
 * C4  3 speakers (predata_multiAims_3dB gains), BiGRU-2L without ADDJUST (selfSS_dB model),
       B = 32, N = 32000 -- fp32 and bf16.
-* C5  recursive extraction at N = 32000 (T = 251) vs oracle/recursive.py: speaker ids
-      bit-exact, probabilities / masks as test_recursive_gpu.py.
+* C5  recursive extraction at N = 32000 (T = 251) vs oracle/recursive.py: fp32 speaker ids
+      bit-exact, probabilities / masks as test_recursive_gpu.py; bf16 at B = 1 and B = 32 with
+      unconditional decided-step asserts.
+* C1 / C3 / C4 in three modes: fp32, mixed (fp32 GEMMs + bf16 recurrent matvec, the mode their
+  throughput is quoted in; masked magnitude within 1e-3) and all-bf16 operands (outside 1e-3 on
+  these BiGRU nets; bound 1e-2).
 """
 import numpy as np
 import pytest
@@ -25,22 +29,33 @@ from test_recursive_gpu import _feats, _models, _ours  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 BF16 = dict(precision="bf16", tol_loss=1e-2, tol_grad=5e-2, tol_pred=1e-2)
+# the mixed mode the C1 / C3 / C4 throughput is quoted in: exact fp32 GEMMs,
+# bf16 MFMA recurrent matvec (fp32 state); masked magnitude within the north-star 1e-3
+MIXED = dict(precision="fp32", rnn_precision="bf16", tol_loss=1e-3, tol_grad=5e-2, tol_pred=1e-3)
+# The all-bf16 operand mode misses 1e-3 on the BiGRU nets (measured C1 2.1e-3, C4 2.2e-3, C3 4.4e-3;
+# tools/parity_probe.py, profiles/r04_parity_configs.jsonl): checked here against its own 1e-2 bound
+# and never quoted as an in-bar throughput.
+MODES = {"fp32": {}, "mixed": MIXED, "bf16": BF16}
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_c1_full_size(dev, precision):
-    kw = BF16 if precision == "bf16" else {}
-    _compare_step(dev, "gru", 2, 1, 2, 40000, "label", loss_channels=101, adjust=False, **kw)
+@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16"])
+def test_c1_full_size(dev, mode):
+    _compare_step(dev, "gru", 2, 1, 2, 40000, "label", loss_channels=101, adjust=False, **MODES[mode])
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_c4_full_size_3spk(dev, precision):
-    kw = BF16 if precision == "bf16" else {}
-    _compare_step(dev, "gru", 2, 32, 3, 32000, "label", adjust=False, **kw)
+@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16"])
+def test_c4_full_size_3spk(dev, mode):
+    _compare_step(dev, "gru", 2, 32, 3, 32000, "label", adjust=False, **MODES[mode])
 
 
-def test_c3_full_size_step(dev):
-    _compare_step(dev, "gru", 2, 16, 2, 32000, "crm", tol_grad=5e-3)
+@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16"])
+def test_c3_full_size_step(dev, mode):
+    """The cRM step at B = 16: the masked complex spectrogram P = M (x) X within 1e-3 rel-L2 in
+    fp32 (measured 1.2e-4) and mixed mode (6.1e-4); bf16 operands 4.4e-3 (bound 1e-2)."""
+    kw = dict(MODES[mode])
+    if mode == "fp32":
+        kw["tol_grad"] = 5e-3
+    _compare_step(dev, "gru", 2, 16, 2, 32000, "crm", **kw)
 
 
 def _c3_run(dev, seed, S, stop_at_non_finite=True):
@@ -102,3 +117,47 @@ def test_c5_full_length_recursive(dev):
     for s in range(2):
         assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < 2e-5
     assert (out["masks"].cpu() - ref["masks"]).abs().max() < 1e-4
+
+
+# bf16 C5: the classifier probabilities' measured bf16 error is <= 9e-5 (B = 32, T = 251,
+# profiles/r04_parity_configs.jsonl); a decision counts as decided when every gap between the
+# consecutive sorted probabilities up to the chosen rank (+1) exceeds DECIDED = 5e-4
+DECIDED = 5e-4
+
+
+def _decided(prob, pick_rank):
+    p = prob.sort(descending=True).values
+    return bool((p[:pick_rank + 1] - p[1:pick_rank + 2]).min() > DECIDED)
+
+
+@pytest.mark.parametrize("B,seed", [(1, 11), (32, 7)])
+def test_c5_full_length_recursive_bf16(dev, B, seed):
+    """C5 in the bf16 mode it is benched in, at T = 251 against oracle/recursive.py, with
+    unconditional asserts: at least 3/4 of the B x 2 extraction decisions are decided (margin
+    above DECIDED), the speaker ids are equal on EVERY decided step (and on every step of this
+    data, measured), probabilities within 5e-4 abs, masks within 3e-2 abs."""
+    mix, cls, emb = _models(seed)
+    X = _feats(B, 32000, seed)
+    T = X.shape[1]
+    with torch.no_grad():
+        ref = orc.recursive_extract(lambda x: mix(x), cls, emb.weight, X)
+    out = _ours(dev, mix, cls, emb, B, T, "bf16").run(X.to(dev))
+    torch.cuda.synchronize()
+    spk, rspk = out["spk"].cpu().long(), ref["spk"]
+    decided = 0
+    for b in range(B):
+        seen = []
+        for s in range(2):
+            order = ref["probs"][s][b].sort(descending=True, stable=True).indices.tolist()
+            rank = next(i for i, k in enumerate(order) if k not in seen)
+            seen.append(order[rank])
+            if _decided(ref["probs"][s][b], rank):
+                decided += 1
+                assert int(spk[b, s]) == int(rspk[b, s]), (b, s, spk[b], rspk[b])
+    assert decided >= (3 * 2 * B + 3) // 4, (decided, 2 * B)
+    for s in range(2):
+        assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < DECIDED
+    agree = spk == rspk
+    rows = agree.all(dim=1)
+    assert bool(rows.any())
+    assert (out["masks"][rows].cpu() - ref["masks"][rows]).abs().max() < 3e-2

@@ -75,7 +75,7 @@ def test_recursive_fp32_matches_oracle(dev, B, n, seed):
 
 
 def test_recursive_bf16_close(dev):
-    B, n, seed = 1, 128 * 39, 11
+    B, n, seed = 1, 128 * 39, 6  # first-decision margin 3.8e-3 (seed 11's was 2.4e-4: undecided)
     mix, cls, emb = _models(seed)
     X = _feats(B, n, seed)
     T = X.shape[1]
@@ -84,11 +84,13 @@ def test_recursive_bf16_close(dev):
     out = _ours(dev, mix, cls, emb, B, T, "bf16").run(X.to(dev))
     torch.cuda.synchronize()
     for s in range(2):
-        assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < 1e-2
+        assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < 5e-4
+    # unconditional: this mixture's first decision has a margin of several times the bf16
+    # probability error (<= 9e-5 measured), so the ids and the first mask must match
     p = ref["probs"][0][0].sort(descending=True).values
-    if float(p[0] - p[1]) > 2e-2:  # decision margin above the bf16 error
-        assert int(out["spk"][0, 0]) == int(ref["spk"][0, 0])
-        assert (out["masks"][:, 0].cpu() - ref["masks"][:, 0]).abs().max() < 3e-2
+    assert float(p[0] - p[1]) > 5e-4, float(p[0] - p[1])
+    assert int(out["spk"][0, 0]) == int(ref["spk"][0, 0])
+    assert (out["masks"][:, 0].cpu() - ref["masks"][:, 0]).abs().max() < 3e-2
 
 
 def test_classifier_select_and_test_mode(dev):

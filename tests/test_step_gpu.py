@@ -29,10 +29,11 @@ def _oracle_features(src, gains, crm):
     return t(feats), t(X), t(Y)
 
 
-def _setup(dev, cell, L, B, K, N, mode, seed=3, adjust=True, loss_channels=None, precision="fp32"):
+def _setup(dev, cell, L, B, K, N, mode, seed=3, adjust=True, loss_channels=None, precision="fp32", rnn_precision=None):
     crm = mode == "crm"
     net = engine.SepNet(cell=cell, num_layers=L, crm=crm, adjust=adjust, device=dev, seed=seed)
-    tr = engine.SepTrainer(net, B, K, N, mode=mode, loss_channels=loss_channels, precision=precision)
+    tr = engine.SepTrainer(net, B, K, N, mode=mode, loss_channels=loss_channels, precision=precision,
+                           rnn_precision=rnn_precision)
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=seed)
     src, spk, u = gen.batch(B)
     gains = synth.gains_for(u, K)
@@ -42,9 +43,12 @@ def _setup(dev, cell, L, B, K, N, mode, seed=3, adjust=True, loss_channels=None,
 
 
 def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, loss_channels=None, adjust=True,
-                  precision="fp32", tol_pred=1e-3):
+                  precision="fp32", tol_pred=1e-3, rnn_precision=None):
+    """One training step, HIP vs oracle: loss, masked magnitude (cRM: the masked complex
+    spectrogram) rel-L2 < tol_pred, every gradient, and (fp32) the Adam-updated parameters.
+    Returns {"masked_rel_l2": ...}."""
     net, tr, src, spk, gains, ref = _setup(dev, cell, L, B, K, N, mode, adjust=adjust, loss_channels=loss_channels,
-                                           precision=precision)
+                                           precision=precision, rnn_precision=rnn_precision)
     feats, X, Y = _oracle_features(src, gains, mode == "crm")
     idx = torch.from_numpy(spk)
     # --- oracle step
@@ -82,9 +86,12 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
     # loss
     l = float(loss[0].cpu())
     assert abs(l - float(loss_ref)) / abs(float(loss_ref)) < tol_loss, (l, float(loss_ref))
-    # masked magnitude (the north-star parity metric): relative L2 <= 1e-3 (fp32)
-    if mode == "label":
-        pr = pred.cpu().view(B, K, T, F)
+    # masked magnitude (the north-star parity metric): relative L2 <= 1e-3 (fp32); cRM: the
+    # masked complex spectrogram P = M (x) X (cRM_EvalVer.py:720-728); PIT: channel order
+    # differs from the label-ordered reference, compared in _pit_full_size instead
+    rel = None
+    if mode in ("label", "crm"):
+        pr = pred.cpu().view(pred_ref.shape)
         rel = ((pr - pred_ref).norm() / pred_ref.norm()).item()
         assert rel < tol_pred, rel
     # gradients (report every tensor's relative error on failure)
@@ -95,8 +102,8 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
         errs[name] = (ours - gr).abs().max().item() / denom if denom > 0 else ours.abs().max().item()
     bad = {k: v for k, v in errs.items() if v > tol_grad}
     assert not bad, (bad, errs)
-    if precision != "fp32":
-        return  # a first Adam step is ~lr*sign(g): not comparable where bf16 moved a small gradient's sign
+    if precision != "fp32" or tr.rnn_precision != "fp32":
+        return {"masked_rel_l2": rel}  # a first Adam step is ~lr*sign(g): not comparable where bf16 moved a small gradient's sign
     # Adam-updated parameters: first step moves each weight by ~lr*sign(g); allow sign
     # disagreements only where the gradient itself is at rounding level
     for name, p in ref.named_parameters():
@@ -116,6 +123,7 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
             ok = (ga <= err_abs) | (diff <= 4 * lr * err_abs * eps / (ga + eps) ** 2)
             assert bool(ok[moved].all()), (name, int(moved.sum()), gr[moved & ~ok][:8])
             assert moved.float().mean().item() < 1e-2, name
+    return {"masked_rel_l2": rel}
 
 
 def test_step_bilstm_label_order(dev):
@@ -263,7 +271,7 @@ def test_step_bitwise_reproducible(dev, precision, mode, B, cell, K):
     assert torch.equal(p0, p1)
 
 
-def _pit_full_size(dev, cell, L, B, K, N, precision, adjust=True, tag="c2", tol_pred=1e-3):
+def _pit_full_size(dev, cell, L, B, K, N, precision, adjust=True, tag="c2", tol_pred=1e-3, rnn_precision=None):
     """PIT at full size: the permutation indices the HIP step selects (dl4ss_pit_select over
     all K! assignments) against the oracle's om.pit_assign, bit-exactly on every utterance
     whose best and second-best assignment costs are not tied within the mode's arithmetic
@@ -274,7 +282,8 @@ def _pit_full_size(dev, cell, L, B, K, N, precision, adjust=True, tag="c2", tol_
     import json
     import os
 
-    net, tr, src, spk, gains, ref = _setup(dev, cell, L, B, K, N, "pit", precision=precision, adjust=adjust)
+    net, tr, src, spk, gains, ref = _setup(dev, cell, L, B, K, N, "pit", precision=precision, adjust=adjust,
+                                           rnn_precision=rnn_precision)
     feats, X, Y = _oracle_features(src, gains, False)
     with torch.no_grad():
         mask, V, h, q = ref(feats, torch.from_numpy(spk))
@@ -300,6 +309,7 @@ def _pit_full_size(dev, cell, L, B, K, N, precision, adjust=True, tag="c2", tol_
     agree = (perm == perm_ref).all(dim=1).numpy()
     ident = torch.arange(K).expand(B, K)
     rec = {"config": tag, "cell": cell, "layers": L, "K": K, "permutations": len(perms), "precision": precision,
+           "rnn_precision": tr.rnn_precision,
            "masked_magnitude_rel_l2": rel, "perm_agree": int(agree.sum()), "B": B, "N": N,
            "decided": int(decided.sum()), "agree_on_decided": int(agree[decided].sum()),
            "min_margin": float(margin.min()), "median_margin": float(np.median(margin)),
@@ -307,7 +317,8 @@ def _pit_full_size(dev, cell, L, B, K, N, precision, adjust=True, tag="c2", tol_
            "masked_magnitude_bar": tol_pred}
     out = os.environ.get("DL4SS_PARITY_OUT")
     if out:
-        with open(out.replace(".json", f"_{tag}_{precision}.json"), "w") as f:
+        suffix = precision if tr.rnn_precision == precision else f"{precision}_rnn{tr.rnn_precision}"
+        with open(out.replace(".json", f"_{tag}_{suffix}.json"), "w") as f:
             json.dump(rec, f)
     print(json.dumps(rec))
     assert agree[decided].all(), rec
@@ -325,23 +336,31 @@ def test_step_c2_full_size_pit_indices(dev, precision):
     assert rec["decided"] == rec["B"], rec
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_step_c4_full_size_pit_3spk_indices(dev, precision):
+# (precision, rnn_precision): fp32 parity mode; the mixed mode (fp32 GEMMs, bf16 MFMA recurrent
+# matvec) that C1 / C3 / C4 throughput is quoted in; the all-bf16 operand mode
+C4_MODES = [("fp32", "fp32"), ("fp32", "bf16"),
+            pytest.param("bf16", "bf16", marks=pytest.mark.xfail(
+                strict=True, reason="bf16 GEMM operands on the BiGRU nets: 2.2e-3 > the 1e-3 bar "
+                                    "(tests/test_bf16_budget_cpu.py reproduces it by emulation)"))]
+
+
+@pytest.mark.parametrize("precision,rnn_precision", C4_MODES)
+def test_step_c4_full_size_pit_3spk_indices(dev, precision, rnn_precision):
     """K = 3 PIT (6 assignments, pit_select_kernel<3> / finalize_kernel<3>) at the full C4 size:
     3-spk mixed-SNR gains (predata_multiAims_3dB), BiGRU-2L without ADDJUST (the selfSS_dB
     model), B = 32, N = 32000.  Under the identity assignment the PIT loss is the reference's
     3-spk loss (Torch_multi/main_run_multi_selfSS_dB.py:513-521); here the chosen assignment
     must equal om.pit_assign on every decided utterance and most utterances must be decided
-    (measured: 32 / 32 decided and equal, 25 of them a non-identity assignment).
+    (measured: 32 / 32 decided and equal, 25 of them a non-identity assignment), and the masked
+    magnitude must be within the north-star 1e-3 (measured: fp32 3.2e-7, mixed 2.9e-4).
 
-    Masked magnitude: fp32 within the north-star 1e-3 (measured 3.2e-7).  bf16 mode: 3e-3
-    (measured 2.2e-3).  That gap is the bf16 rounding of the Linear operands and of V itself on
-    this BiGRU model, not a kernel defect: rounding only V = tanh(Linear) to bf16 in the fp32
-    oracle already gives 0.96e-3 on the BiGRU-2L models and 0.18e-3 on the BiLSTM-4L model, and
-    adding the bf16 Linear operands 1.7e-3 vs 0.25e-3 (B = 4, N = 32000, CPU emulation).  The
-    headline C2 bf16 step meets 1e-3 (test_step_c2_full_size_pit_indices)."""
-    rec = _pit_full_size(dev, "gru", 2, 32, 3, 32000, precision, adjust=False, tag="c4",
-                         tol_pred=1e-3 if precision == "fp32" else 3e-3)
+    The all-bf16 operand mode misses the bar on this model (2.2e-3, strict xfail): every bf16
+    operand of the non-recurrent GEMMs costs ~1e-3 here (features 0.7e-3, W_ih 1.5e-3, the Linear's
+    h 0.9e-3 and W 0.9e-3, V 0.9e-3), the bf16 recurrent matvec only 0.3e-3
+    (tools/bf16_budget.py, tests/test_bf16_budget_cpu.py) -- so the mixed mode keeps the
+    recurrence on bf16 MFMA and the GEMMs exact."""
+    rec = _pit_full_size(dev, "gru", 2, 32, 3, 32000, precision, adjust=False, tag="c4", tol_pred=1e-3,
+                         rnn_precision=rnn_precision)
     assert rec["decided"] >= rec["B"] * 3 // 4, rec
 
 

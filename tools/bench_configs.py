@@ -39,12 +39,13 @@ def _time(fn, steps, warmup):
 
 
 def train_config(name, cell, L, B, K, N, mode, precision, steps, warmup, loss_channels=None, adjust=True,
-                 eval_istft=False, emb_scale=1.0):
+                 eval_istft=False, emb_scale=1.0, rnn_precision=None):
     dev = torch.device("cuda")
     net = engine.SepNet(cell=cell, num_layers=L, crm=mode == "crm", adjust=adjust, device=dev, seed=1)
     if emb_scale != 1.0:  # the query embedding (N(0,1) rows at init) scaled: logits stay below saturation
         net.view("emb.layer.weight").mul_(emb_scale)
-    tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision, loss_channels=loss_channels)
+    tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision, loss_channels=loss_channels,
+                           rnn_precision=rnn_precision)
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1)
     src, spk, u = gen.batch(B)
     raw = torch.from_numpy(src.astype(np.float32)).to(dev)
@@ -75,7 +76,7 @@ def train_config(name, cell, L, B, K, N, mode, precision, steps, warmup, loss_ch
     timed = [float(x.item()) for x in losses[warmup:]]
     lv = timed[-1]
     r = {"config": name, "value": B / dt, "unit": "mixtures/s", "ms_per_step": dt * 1e3, "batch": B,
-         "precision": precision, "loss": lv, "timed_losses": timed,
+         "precision": precision, "rnn_precision": tr.rnn_precision, "loss": lv, "timed_losses": timed,
          "window_finite": bool(np.all(np.isfinite(timed))), "data": "synthetic", "n_gpus": 1}
     if emb_scale != 1.0:
         r["init"] = (f"query embedding scaled by {emb_scale} at init so every cRM logit stays below the 9.02 "
@@ -121,19 +122,22 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
+    ap.add_argument("--rnn-precision", default=None, choices=["fp32", "bf16"],
+                    help="recurrent matvec precision (default: --precision)")
     a = ap.parse_args()
+    rp = dict(rnn_precision=a.rnn_precision)
     for c in a.configs:
         if c == "c1":
             r = train_config("C1: BiGRU-2L, B=1, 101-channel loss, N=40000", "gru", 2, 1, 2, 40000, "label",
-                             a.precision, a.steps, a.warmup, loss_channels=101, adjust=False)
+                             a.precision, a.steps, a.warmup, loss_channels=101, adjust=False, **rp)
         elif c == "c3":  # with the reference's N(0,1) query embedding the cRM logits saturate at init
             # (cRM_EvalVer.py:688: the loss is non-finite from the first steps, as in the reference);
             # the throughput is timed on a finite window (emb_scale) and reports every timed loss
             r = train_config("C3: cRM BiGRU-2L, B=16, N=32000, + mask-apply iSTFT", "gru", 2, 16, 2, 32000, "crm",
-                             a.precision, a.steps, a.warmup, eval_istft=True, emb_scale=0.1)
+                             a.precision, a.steps, a.warmup, eval_istft=True, emb_scale=0.1, **rp)
         elif c == "c4":
-            r = train_config("C4: 3-spk mixed SNR BiGRU-2L, B=32, N=32000", "gru", 2, 32, 3, 32000, "label",
-                             a.precision, a.steps, a.warmup)
+            r = train_config("C4: 3-spk mixed SNR BiGRU-2L (no ADDJUST), B=32, N=32000", "gru", 2, 32, 3, 32000,
+                             "label", a.precision, a.steps, a.warmup, adjust=False, **rp)
         elif c == "c5":  # the reference's replica: one mixture at a time
             r = recursive_config(a.precision, a.steps, a.warmup)
         elif c == "c5x32":  # 32 independent extractions (rows) per launch: the same latency-bound chain
