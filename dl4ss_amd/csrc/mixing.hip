@@ -73,15 +73,16 @@ __global__ __launch_bounds__(256) void source_stats_kernel(const float* __restri
   }
 }
 
-// grid (ceil(N/1024), B): normalise, gain, write sources and their sum.  The products are
-// __fmul_rn: hipcc contracts (x - m) * g + acc into one fma by default, which would make the
-// mixture differ in the last bit from the sum of the stored sources (the reference's
-// wav_mix = wav_mix + signal, predata_fromList_cRM_123.py:225-229)
+// grid (ceil(N/1024), B): normalise, gain, write sources and their sum.  fp contraction is off
+// here: hipcc fuses (x - m) * g + acc into one fma by default (and __fmul_rn is a plain
+// product), which would make the mixture differ in the last bit from the sum of the stored
+// sources (the reference's wav_mix = wav_mix + signal, predata_fromList_cRM_123.py:225-229)
 __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw, const SrcPart* __restrict__ part,
                                                   const float* __restrict__ gains, const int* __restrict__ lens,
                                                   const int* __restrict__ shifts, int K, int N,
                                                   float* __restrict__ out_src,
                                                   float* __restrict__ out_mix) {
+#pragma clang fp contract(off)
   const int b = blockIdx.y;
   // per-source (mean, 1 / max|x - mean|) from the NSPLIT partials, fixed order; the shift
   // reduced modulo the source's length (0 = no rotation)
@@ -127,21 +128,21 @@ __global__ __launch_bounds__(256) void mix_kernel(const float* __restrict__ raw,
         if (i + q < len) {
           int j = i + q + sh;
           j -= j >= len ? len : 0;
-          v = __fmul_rn(x[j] - st.x, g);
+          v = (x[j] - st.x) * g;
         }
         o[i + q] = v;
         a[q] += v;
       }
     } else if (i + 3 < len && ((N & 3) == 0)) {
       float4 v = *reinterpret_cast<const float4*>(x + i);
-      v.x = __fmul_rn(v.x - st.x, g); v.y = __fmul_rn(v.y - st.x, g);
-      v.z = __fmul_rn(v.z - st.x, g); v.w = __fmul_rn(v.w - st.x, g);
+      v.x = (v.x - st.x) * g; v.y = (v.y - st.x) * g;
+      v.z = (v.z - st.x) * g; v.w = (v.w - st.x) * g;
       *reinterpret_cast<float4*>(o + i) = v;
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     } else {
       float* a = &acc.x;
       for (int q = 0; q < 4 && i + q < N; ++q) {
-        const float v = i + q < len ? __fmul_rn(x[i + q] - st.x, g) : 0.0f;
+        const float v = i + q < len ? (x[i + q] - st.x) * g : 0.0f;
         o[i + q] = v;
         a[q] += v;
       }
