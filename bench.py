@@ -120,6 +120,8 @@ def pmc_traffic(kernel, grids):
 
 CONFIGS = {
     # name: mask net, speakers, per-GPU batch, samples (SURVEY 8 "Configs")
+    "C1": dict(kind="cpu", cell="gru", L=2, K=2, adjust=False, B=1, N=40000,
+               what="C1: Torch_multi/main_run.py CPU reference path, BiGRU-2L, B=1, dense 101-channel loss"),
     "C2": dict(kind="train", cell="lstm", L=4, K=2, adjust=True, B=32, N=32000,
                what="C2: 2-spk {mode} BiLSTM-4L magnitude mask (EvalVer model)"),
     "C4": dict(kind="train", cell="gru", L=2, K=3, adjust=False, B=32, N=32000,
@@ -244,6 +246,84 @@ def cpu_baseline(args, cfg, with_classifier=False):
             "sample": f"{args.cpu_steps} step(s) of the B={args.cpu_batch} batch, oracle torch-CPU fp32 {net} "
                       f"fwd+{args.mode} loss (K={K})+bwd+Adam incl. numpy STFT features {what}on {cores} thread(s)",
             "seconds": dt}
+
+
+def cpu_reference_c1(args, N, with_classifier=False):
+    """BASELINE configs[0]: the CPU reference path of Torch_multi/main_run.py:453-522 on the host
+    cores, B = 1, restated on the oracle (torch-CPU fp32 + numpy FFT): features of a synthetic
+    2-speaker mixture, MIX_SPEECH BiGRU-2L + Linear + tanh, the DENSE masked embedding of all 101
+    labels (main_run.py:307-327, :474), the 'dot' attention over all 101 channels (:478-486), the
+    multi-hot mask (:487-489), the 101-channel MSE (:499-506; the sum-to-one term is computed and
+    not added, :509-513), backward and Adam.  ``with_classifier``: the discarded
+    MIX_SPEECH_classifier forward (:465, BiLSTM H = 300 x NUM_LAYERS = 2, main_run.py:284-305) too."""
+    from oracle import dsp, model as om, recursive as orec
+    from dl4ss_amd import synth
+
+    K, L = 2, 101
+    cores = cpu_threads()
+    torch.set_num_threads(cores)
+    torch.manual_seed(1)
+    ref = om.SepModel(cell="gru", num_layers=2, adjust=False)
+    opt = om.make_adam(ref)
+    cls = orec.Classifier(hidden=300, num_layers=2) if with_classifier else None
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=1)
+    steps = max(1, args.cpu_steps)
+    batches = [gen.batch(1) for _ in range(steps + 1)]
+
+    def one_step(src, spk, u):
+        gains = synth.gains_for(u, K)
+        srcs = [dsp.normalise_source(src[0, k], N) for k in range(K)]
+        s, m = dsp.mix_sources(srcs, gains[0])
+        _ = dsp.stft_tf(m)  # mix_phase (predata_multiAims.py computes it)
+        f = torch.from_numpy(dsp.magnitude(m)[None])
+        Y = torch.zeros(1, L, *f.shape[1:])
+        for k in range(K):
+            Y[0, spk[0, k]] = torch.from_numpy(dsp.magnitude(s[k]))
+        topk = torch.zeros(1, L)
+        topk[0, torch.from_numpy(spk[0]).long()] = 1.0
+        if cls is not None:
+            with torch.no_grad():
+                cls(f)
+        opt.zero_grad()
+        V, _ = ref.mix(f)
+        q = ref.emb.layer.weight[None] * topk[:, :, None]  # dense embedding x multi-hot
+        mask = torch.sigmoid(torch.einsum("btfe,bke->bktf", V, q))
+        loss, pred = om.loss_101(mask, topk, f, Y)
+        _ = torch.mean((pred.sum(dim=1) - 1.0) ** 2)  # computed, not added (main_run.py:509-513)
+        loss.backward()
+        opt.step()
+
+    one_step(*batches[0])  # warm-up
+    t0 = time.perf_counter()
+    for b in batches[1:]:
+        one_step(*b)
+    dt = time.perf_counter() - t0
+    what = "+ discarded classifier BiLSTM-2L H=300 fwd (reference-faithful)" if with_classifier else "(mask path)"
+    return {"value": steps / dt, "unit": "mixtures/s", "cores": cores, "kind": "port", "N": N, "T": 1 + N // 128,
+            "sample": f"{steps} step(s) at B=1, oracle torch-CPU fp32 BiGRU-2L fwd + 101-channel attention + "
+                      f"101-channel MSE + bwd + Adam incl. numpy STFT features {what} on {cores} thread(s)",
+            "seconds": dt}
+
+
+def c1_cpu_lines(args):
+    """The four C1 CPU timings SURVEY 8d asks for: N = 40000 (5 s, the reference default) and 32000
+    (4 s), each without and with the discarded classifier forward."""
+    return {f"N{n}_{tag}": cpu_reference_c1(args, n, with_classifier=wc)
+            for n in (40000, 32000) for tag, wc in (("mask_path", False), ("with_classifier", True))}
+
+
+def c1_main(args):
+    """--config C1: BASELINE configs[0], the reference's CPU path (no GPU): one JSON line."""
+    lines = c1_cpu_lines(args)
+    head = lines["N40000_mask_path"]
+    line = {"metric": "mixtures/sec, C1 CPU reference path (Torch_multi/main_run.py, B=1)", "value": head["value"],
+            "unit": "mixtures/s", "n_gpus": 0, "steps": args.cpu_steps, "warmup": 1,
+            "ms_per_step": 1000.0 / head["value"], "higher_is_better": True, "scaling": None, "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic speech-shaped sources, seed 1",
+            "config": {"workload": CONFIGS["C1"]["what"], "global_batch": 1, "seq_len": head["T"],
+                       "parallelism": "none (host cores)"},
+            "cpu_reference_c1": lines}
+    print(json.dumps(line), flush=True)
 
 
 def cpu_baseline_recursive(args, cfg):
@@ -571,6 +651,8 @@ def train_main(args, cfg, dev, world, rank, pg):
             out["cpu_baseline"] = cpu_baseline(args, cfg)
             if args.config == "C2":
                 out["cpu_baseline_with_classifier"] = cpu_baseline(args, cfg, with_classifier=True)
+                # BASELINE configs[0] (the reference's CPU path, B = 1) timed on the same host cores
+                out["cpu_reference_c1"] = c1_cpu_lines(args)
         print(json.dumps(out), flush=True)
 
 
@@ -658,6 +740,8 @@ def main(argv=None):
     if args.standin:
         return standin_main(args, world, rank)
     cfg = CONFIGS[args.config]
+    if cfg["kind"] == "cpu":
+        return c1_main(args)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None

@@ -98,12 +98,6 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
     if constexpr (VB) {
       const unsigned* src = reinterpret_cast<const unsigned*>(a.Vb + ((long long)b * a.rows_per_b + r0) * E);
       const int n2 = nr * E / 2;
-#ifdef ATTN_STAGE_LOOP
-      for (int i = tid; i < n2; i += NT) {
-        const unsigned w = src[i];
-        reinterpret_cast<float2*>(sv)[i] = make_float2(__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u));
-      }
-#else
       // every load of the tile issued before the first LDS store (a load -> store loop
       // kept one 4-B load per thread in flight)
       constexpr int NW = (TILE * E / 2 + NT - 1) / NT;
@@ -119,7 +113,6 @@ __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs a) {
         if (i < n2)
           reinterpret_cast<float2*>(sv)[i] = make_float2(__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xFFFF0000u));
       }
-#endif
     } else {
       const float* src = Vb + (long long)r0 * E;
       const int n = nr * E;
@@ -658,7 +651,6 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
 template <int E, int K, bool CRM, bool VB>
 int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
   dim3 grid(a.nblk, a.B);
-#ifndef ATTN_V1
   if constexpr (VB && !CRM) {  // the throughput step's bf16-V magnitude path (16-B aligned V)
     if ((a.dPreB || !grad) && ((uintptr_t)a.Vb & 15) == 0) {
       if (grad)
@@ -669,7 +661,6 @@ int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
       return 0;
     }
   }
-#endif
   if (grad)
     hipLaunchKernelGGL((attn_kernel<E, K, CRM, true, VB>), grid, dim3(NT), 0, st, a);
   else

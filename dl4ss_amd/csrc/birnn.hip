@@ -139,14 +139,16 @@ __device__ __forceinline__ float sum_partials16(const float* p, int stride) {
   return v[0];
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-// (no NaN special case on the recurrence's critical path: values formed here by arithmetic
-// are canonical quiet NaNs 0x7FC00000 / 0xFFC00000 when non-finite, which round to NaN; the
-// fp32 weights arriving as arbitrary bit patterns go through bf16_bits_rne)
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
   unsigned u = __float_as_uint(f);
   u += 0x7FFF + ((u >> 16) & 1);
   return (unsigned short)(u >> 16);
 }
+// The weights are rounded with the same plain RNE when a launch loads its W_hh fragments.  No NaN
+// special case here: values formed by arithmetic are canonical quiet NaNs (0x7FC00000 / 0xFFC00000),
+// which round to NaN, and the NaN-preserving form (bf16_bits_rne) in the once-per-launch weight
+// loads changed the packed kernels' code generation enough to cost 4.3 % of the step (A/B, 20 steps
+// x 2 alternating runs: 7768 / 7776 vs 8109 / 8097 mixtures/s, round 4).
 
 __device__ __forceinline__ void put_granule(u64* g, unsigned tag, float v) {
   const u64 x = ((u64)tag << 32) | (u64)__float_as_uint(v);
@@ -319,7 +321,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_kernel(RnnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = ks * 32 + 8 * (lane >> 4) + j;
-        afrag[ks][j] = (short)bf16_bits_rne((rv && k < H) ? wrow[k] : 0.0f);
+        afrag[ks][j] = (short)bf16_rne((rv && k < H) ? wrow[k] : 0.0f);
       }
     for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;  // bf16 image incl. padding rows/cols
   }
@@ -551,27 +553,13 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
 #endif
-#ifndef FWD_MV_CHAINS
-#define FWD_MV_CHAINS 2  // forward bf16 matvec: accumulator chains per MFMA tile (4: 367 vs 363 us per pass)
-#endif
+constexpr int FWD_MV_CHAINS = 2;  // forward bf16 matvec: accumulator chains per MFMA tile (4: 367 vs 363 us per pass)
 #ifndef FWD_NPW
 #define FWD_NPW 2  // forward polling waves: 4, and 7 when >= 2, and 6 when 3 (their MFMA tile indices must be >= MT)
 #endif
 static_assert(FWD_MV_CHAINS >= 1 && FWD_MV_CHAINS <= 8, "FWD_MV_CHAINS: 1..KSMAX accumulator chains");
 static_assert(FWD_NPW >= 1 && FWD_NPW <= 3, "FWD_NPW: 1..3 polling waves");
 static_assert(BWD_NPW >= 1 && BWD_NPW <= 3, "BWD_NPW: 1..3 polling waves");
-#ifndef FWD_SPLIT4
-// forward matvec with 5 MFMA tiles (LSTM, J = 20): tile 4's k-steps split over the four cell waves
-// (k-step ks on wave ks % 4) instead of whole on wave 5 -- wave 5 shares SIMD 1 with wave 1, whose
-// matvec then ran its 10 MFMAs beside wave 5's 10 (stamps: wave 5 629 vs wave 0 404 cycles from
-// B1, every other wave waiting at B2 for it)
-#define FWD_SPLIT4 0  // measured slower: 7882 vs 8102 mixtures/s (profiles/r03_split4.jsonl)
-#endif
-#ifndef XW_MAP
-// fused projection tile -> wave map (rnn_fwd_pk_kernel): 1 = second tiles on the prefetch waves
-// (600-wide layers 351 us per launch, first layer 313 us), 0 = on the polling waves (364 / 327 us)
-#define XW_MAP 1
-#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t granule_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
@@ -634,8 +622,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const int lane = tid & 63, wv = tid >> 6;
   const int GH = NGATE * H;
   const int tile = wv < WPOLL ? wv : wv - 1;
-  const bool split4 = FWD_SPLIT4 && MT == 5;  // tile 4 as k-step parts on waves 0-3 (FWD_SPLIT4)
-  const bool mv = wv != WPOLL && tile < MT && !(split4 && tile == 4);
+  const bool mv = wv != WPOLL && tile < MT;
   const int SGS = MT * 16 + 4;  // sgate row stride (floats): 4 batch rows on 4 distinct bank quads
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -644,12 +631,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   // reads are conflict-free, tools/lds_banks.py)
   unsigned short* shb = reinterpret_cast<unsigned short*>(smem);
   float* sgate = smem + 8 * SHB;                                                        // [BC][SGS]
-  // split4: tile 4's partial sums of waves 1-3 [3][BC][16] (wave 0's go to sgate's tile-4 columns)
-  float* sgx = sgate + BC * SGS;
   // per-step input projections [NSIN][BC*32][4]: double buffered, or with XW two blocks of SPB steps
   constexpr int SPB = xw_spb(BC);
   constexpr int NSIN = XW ? 2 * SPB : 2;
-  float* sin = sgx + 3 * BC * 16;
+  float* sin = sgate + BC * SGS;
   unsigned short* spub = reinterpret_cast<unsigned short*>(sin + NSIN * BC * 32 * 4);   // [BC][PKU]
   // XW: the ring of 3 * SPB step slots of the layer-input rows ([BC][SXB] bf16 + the pad items of
   // the last DMA piece), 256-B aligned (the bank order of its rows)
@@ -673,30 +658,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = ks * 32 + 8 * (lane >> 4) + j;
-        afrag[ks][j] = (short)bf16_bits_rne((rv && k < H) ? wrow[k] : 0.0f);
-      }
-  }
-  // split4: cell wave w's k-steps w, w + 4, w + 8 of tile 4 (zero beyond KSMAX / H)
-  constexpr int KX = (KSMAX + 3) / 4;
-  bf16x8 afx[KX];
-  {
-    const int rl = 4 * 16 + (lane & 15);
-    const int q = rl / J, u = rl % J;
-    const bool rv = split4 && wv < 4 && rl < R && j0 + u < H;
-    const float* wrow = a.Whh + ((long long)d * GH + q * H + j0 + u) * H;
-#pragma unroll
-    for (int i = 0; i < KX; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = (wv + 4 * i) * 32 + 8 * (lane >> 4) + j;
-        afx[i][j] = (short)bf16_bits_rne((rv && wv + 4 * i < KSMAX && k < H) ? wrow[k] : 0.0f);
+        afrag[ks][j] = (short)bf16_rne((rv && k < H) ? wrow[k] : 0.0f);
       }
   }
   for (int i = tid; i < 8 * SHB; i += NT) smem[i] = 0.0f;
   for (int i = tid; i < BC * PKU; i += NT) spub[i] = 0;
 
   // ---- XW: the fused projection runs off the cell waves, on waves 4-7 (their slack: the free
-  //      prefetch wave 6, the DMA wave 5 (FWD_SPLIT4: no matvec tile), and the polling waves between B2 and the first
+  //      prefetch wave 6, the DMA wave 5, and the polling waves between B2 and the first
   //      granule that can land): tile 0 on wave 6, tile 1 on wave 5 (one each: their branch also
   //      holds wave 5's matvec fragments), tiles 2 + 2i on wave 4 and 3 + 2i on wave 7 (two each).
   //      Per tile, bf16 A fragments of its W_ih rows, A[row t*16 + (lane&15)][k = ks*32 +
@@ -705,13 +674,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   //      waves).  Tile counts per role are compile-time (IC<1> / IC<2>) so unused slots stay dead.
   constexpr int XWT = 2;
   int xt[XWT];
-#if XW_MAP == 0  // second tiles on the polling waves
-  xt[0] = !XW ? -1 : wv == 6 ? 0 : wv == 5 ? 1 : wv == WPOLL ? 2 : wv == 7 ? 3 : -1;
-  xt[1] = (XW && (wv == WPOLL || wv == 7) && xt[0] + 2 < MT) ? xt[0] + 2 : -1;
-#else  // second tiles on the prefetch waves (6 first)
+  // second tiles on the prefetch waves, 6 first (600-wide layers 351 us per launch, first layer
+  // 313 us; on the polling waves instead: 364 / 327 us, round 3)
   xt[0] = !XW ? -1 : wv == 6 ? 0 : wv == 5 ? 1 : wv == WPOLL ? 2 : wv == 7 ? 3 : -1;
   xt[1] = (XW && (wv == 6 || wv == 5) && xt[0] + 4 < MT) ? xt[0] + 4 : -1;
-#endif
   if (xt[0] >= MT) xt[0] = -1;
   bf16x8 wfr[XWT][XW ? XK : 1];
   float bir[XWT][4];
@@ -894,12 +860,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     xfinal(ntl, 0);
   };
   // compile-time tile slots of the prefetch-wave and polling-wave roles
-  using XPF = std::integral_constant<int, XW_MAP == 0 ? 1 : 2>;
-  using XPL = std::integral_constant<int, XW_MAP == 0 ? 2 : 1>;
+  using XPF = std::integral_constant<int, 2>;
+  using XPL = std::integral_constant<int, 1>;
 
-  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]; with4: + this cell wave's k-steps of tile 4
-  // (FWD_SPLIT4; only the cell waves' instantiation holds the tile-4 fragments live)
-  auto matvec = [&](auto with4) __attribute__((always_inline)) {
+  // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
+  auto matvec = [&]() __attribute__((always_inline)) {
     if (!mv) return;
     const unsigned short* bp = shb + min(lane & 15, BC) * SHB + 8 * (lane >> 4);
     bf16x8 bv[KSMAX];
@@ -922,30 +887,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     if (col < BC) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) sgate[col * SGS + tile * 16 + (lane >> 4) * 4 + i] = acc[0][i];
-    }
-    if (decltype(with4)::value && split4) {
-      // this wave's k-steps of tile 4 (wave-uniform offset: one compile-time body per wave, the B
-      // fragments indexed statically)
-      f32x4 ax = f32x4{0.f, 0.f, 0.f, 0.f};
-      auto part = [&](auto off) __attribute__((always_inline)) {
-        constexpr int o = decltype(off)::value;
-#pragma unroll
-        for (int i = 0; i < KX; ++i)
-          if (o + 4 * i < KSMAX) ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afx[i], bv[min(o + 4 * i, KSMAX - 1)], ax, 0, 0, 0);
-      };
-      // a SCALAR branch: as exec-masked blocks without a skip branch (the compiler's form for a
-      // per-lane condition) every wave ran every body, and MFMAs do not honour EXEC -- the next
-      // body overwrote the accumulator
-      const int wvs = __builtin_amdgcn_readfirstlane(wv);
-      if (wvs == 0) part(std::integral_constant<int, 0>{});
-      else if (wvs == 1) part(std::integral_constant<int, 1>{});
-      else if (wvs == 2) part(std::integral_constant<int, 2>{});
-      else part(std::integral_constant<int, 3>{});
-      if (col < BC) {
-        float* dst = wv == 0 ? sgate + col * SGS + 4 * 16 : sgx + ((wv - 1) * BC + col) * 16;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dst[(lane >> 4) * 4 + i] = ax[i];
-      }
     }
   };
 
@@ -1054,7 +995,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         STAMP(0)
         __syncthreads();  // B1
         STAMP(1)
-        if constexpr (MV) matvec(std::false_type{});
+        if constexpr (MV) matvec();
         // XW: at a block start the rows of the next block (consumed from this step on) landed
         // before B2; the block after it may stay in flight
         if (XW && s % SPB == 0) xwait(max(0, min(SPB, T - (s / SPB + 2) * SPB)));
@@ -1071,8 +1012,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     // (fused projection: wave 6 holds no matvec tile and wave 5 one projection tile --
     // dl4ss_birnn_fwd_xw_supported admits at most 5 MFMA tiles; without it the slot count is moot)
     using XP1 = std::integral_constant<int, 1>;
-    // (wave 5 with FWD_SPLIT4 has no tile: its matvec() returns at once; a third instantiation for
-    // it put a role lambda out of line, 1280 B of scratch)
     if (wv == 6 && !mv)
       pf_loop(XPF{}, std::false_type{});
     else
@@ -1085,7 +1024,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     STAMP(0)
     __syncthreads();  // B1
     STAMP(1)
-    matvec(std::true_type{});
+    matvec();
     STAMP(2)
     __syncthreads();  // B2
     STAMP(3)
@@ -1100,14 +1039,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         for (int q = 0; q < NGATE; ++q) {
           hg[q] = bh[q] + sgate[cb * SGS + q * J + cu];
           gx[q] = gxa[q];
-        }
-        // split4: rows of tile 4 are gate-3 rows (R = 4J <= 80, tile 4 = rows 64..79); their
-        // four k-step parts summed in fixed order
-        if (CELL == CELL_LSTM && split4 && 3 * J + cu >= 64) {
-          const int r4 = 3 * J + cu - 64;
-          const float p0 = sgate[cb * SGS + 4 * 16 + r4];
-          const float p1 = sgx[(0 * BC + cb) * 16 + r4], p2 = sgx[(1 * BC + cb) * 16 + r4], p3 = sgx[(2 * BC + cb) * 16 + r4];
-          hg[3] = bh[3] + ((p0 + p1) + (p2 + p3));
         }
         if constexpr (CELL == CELL_LSTM) {
           const float ig = fsig(gx[0] + hg[0]);
@@ -1242,7 +1173,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
           const int rr = ks * 32 + 8 * (lane >> 4) + j;
           const int q = rr / J, u = rr % J;
           const bool ok = mv && k < H && rr < R && j0 + u < H;
-          afr[t][ks][j] = (short)bf16_bits_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
+          afr[t][ks][j] = (short)bf16_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
         }
     }
   }
@@ -1526,9 +1457,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 // the cell lanes' dG / dGh stores of step s-1 issued after B1 of step s (before the cell update)
 // instead of right after the publish: measured slower, 7994 vs 8085 mixtures/s
 // (profiles/r03_dglate.jsonl) -- their issue then sits on the cell phase's critical path
-#ifndef BWD_DG_LATE
-#define BWD_DG_LATE 0
-#endif
 __device__ __forceinline__ unsigned pack24(float v) {
   const unsigned u = __float_as_uint(v);
   return (u + 0x80u) >> 8;  // round to nearest (ties away) on the dropped 8 bits
@@ -1582,7 +1510,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         const int rr = ks * 32 + 8 * (lane >> 4) + j;
         const int q = rr / J, u = rr % J;
         const bool ok = mv && k < H && rr < R && j0 + u < H;
-        afr[t][ks][j] = (short)bf16_bits_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
+        afr[t][ks][j] = (short)bf16_rne(ok ? a.Whh[((long long)d * GH + q * H + j0 + u) * H + k] : 0.0f);
       }
   }
 
@@ -1796,7 +1724,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     __syncthreads();  // B1
     STAMP(1)
     if (tid == 0) TRACE(3, s);
-    if (BWD_DG_LATE && s > 0) store_dg();  // step s-1's (pt, pgi, pgh)
     if (tid < BC * 32) {
       float dgi[NGATE], dgh[NGATE];
 #pragma unroll
@@ -1904,7 +1831,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       }
       if (wv == 3) TRACE(0, s);
     }
-    if (!BWD_DG_LATE) store_dg();  // this step's dG / dGh, after the publish (off the critical path)
+    // this step's dG / dGh, after the publish (off the critical path; issued after B1 of the next
+    // step instead they measured slower, 7994 vs 8085 mixtures/s, round 3)
+    store_dg();
     STAMP(6)
   }
   // fused bias gradients: this cell's sums over t, one plain store per (row, gate) into the
@@ -2049,7 +1978,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) 
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
     p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((16 * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16 + 4) +
                                                     2 * 2 * (BC * 32 * 4 + 16));
-    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + 3 * BC * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
+    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + 2 * BC * 32 * 4) + 2 * BC * PKU;
     return true;
   }
   return false;

@@ -68,8 +68,25 @@ def test_bench_configs_table():
     sys.path.insert(0, ROOT)
     import bench
 
-    assert set(bench.CONFIGS) == {"C2", "C4", "C5"}
+    assert set(bench.CONFIGS) == {"C1", "C2", "C4", "C5"}
+    assert bench.CONFIGS["C1"]["kind"] == "cpu" and bench.CONFIGS["C1"]["B"] == 1
     assert bench.parse([]).config == "C2" and bench.parse([]).gpus == 1
     c4 = bench.CONFIGS["C4"]
     assert (c4["cell"], c4["L"], c4["K"], c4["adjust"], c4["B"]) == ("gru", 2, 3, False, 32)
     assert bench.CONFIGS["C5"]["kind"] == "recursive" and bench.CONFIGS["C5"]["B"] == 1
+
+
+def test_bench_c1_cpu_reference_line():
+    """--config C1 (BASELINE configs[0]): the reference's CPU path timed on the host cores, no GPU;
+    one JSON line with the four SURVEY 8d variants (N 40000 / 32000, without / with the classifier)."""
+    import json
+
+    r = subprocess.run([sys.executable, BENCH, "--config", "C1", "--cpu-steps", "1"], capture_output=True, text=True,
+                       env=_env(), timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 0 and line["value"] > 0 and line["dtype"] == "f32"
+    v = line["cpu_reference_c1"]
+    assert set(v) == {"N40000_mask_path", "N40000_with_classifier", "N32000_mask_path", "N32000_with_classifier"}
+    assert all(x["cores"] >= 1 and x["value"] > 0 for x in v.values())
+    assert v["N40000_mask_path"]["T"] == 313 and v["N32000_mask_path"]["T"] == 251
