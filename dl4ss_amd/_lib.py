@@ -17,6 +17,7 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 LL = ctypes.c_longlong
 F = ctypes.c_float
+U = ctypes.c_uint
 
 # name -> argtypes (all return int hipError_t)
 SIGNATURES = {
@@ -26,6 +27,7 @@ SIGNATURES = {
     "dl4ss_gemm": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, P],
     "dl4ss_f32_to_bf16": [P, P, LL, P],
     "dl4ss_f32_to_bf16_2d": [P, LL, I, I, P, LL, P],
+    "dl4ss_f32_to_bf16_hilo": [P, LL, I, I, P, LL, I, I, U, P],
     "dl4ss_colsum_bf16": [P, LL, I, I, P, P],
     "dl4ss_colsum_bf16_part_bytes": [I, I],
     "dl4ss_colsum_bf16_det": [P, LL, I, I, P, P, LL, P],

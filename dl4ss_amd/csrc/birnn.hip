@@ -1074,7 +1074,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);   // plain: stays in the group's L2
       }
       if (tid == 0) TRACE(0, s);
+#ifdef EXP_FWD_NO_SAVE
+      if (false) {
+#else
       if (cval) {
+#endif
         const long long bt = (long long)bg * T + t;
         float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
         actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
@@ -1696,6 +1700,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 #pragma unroll
   for (int q = 0; q < NGATE; ++q) sbi[q] = sbh[q] = pgi[q] = pgh[q] = 0.0f;
   auto store_dg = [&]() {
+#ifdef EXP_BWD_NO_DG
+    return;
+#endif
     if (!cval) return;
     const long long go = (long long)((bg * T + pt) * 2 + d) * GH + cj;
     if (a.dG) {

@@ -8,6 +8,8 @@
 // The Linear bias gradient is the column sum of bf16 dPre (dl4ss_colsum_bf16_det: per-256-row-block
 // partials + a fixed-order reduce, bitwise reproducible; EvalVer.py:298 Linear.bias).
 #include "common.h"
+
+#include <algorithm>
 #include <hip/hip_bf16.h>
 
 namespace {
@@ -156,7 +158,47 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restr
   out[n] += a;
 }
 
+// Split-precision operand images: x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (|lo| <= 2^-9 |x|,
+// x - hi - lo <= 2^-17 |x|).  Segment s of a row (width segw >= cols, zero beyond cols) holds hi or lo
+// by bit s of `pattern`; one thread per (row, column < segw) writes all nseg segments, then zeros up
+// to ldy.  The K-concatenated product [x_hi | x_lo | x_hi] . [w_hi | w_hi | w_lo] = x w - x_lo w_lo
+// - (rounding of lo) is fp32-accurate to ~2^-16 relative: one bf16 MFMA GEMM with K' = 3K.
+__global__ __launch_bounds__(256) void f32_to_bf16_hilo_kernel(const float* __restrict__ x, long long ldx, int rows,
+                                                               int cols, unsigned short* __restrict__ y,
+                                                               long long ldy, int segw, int nseg, unsigned pattern) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int wrow = max(segw, (int)(ldy - (long long)(nseg - 1) * segw));  // the last segment also zeroes the tail
+  if (i >= (long long)rows * wrow) return;
+  const long long r = i / wrow;
+  const int c = (int)(i - r * wrow);
+  unsigned short hi = 0, lo = 0;
+  if (c < cols) {
+    const float v = x[r * ldx + c];
+    const unsigned hb = bf16_bits_rne(v);
+    hi = (unsigned short)hb;
+    lo = (unsigned short)bf16_bits_rne(v - __uint_as_float(hb << 16));
+  }
+  unsigned short* yr = y + r * ldy;
+  for (int sg = 0; sg < nseg; ++sg) {
+    const long long col = (long long)sg * segw + c;
+    if ((c < segw || sg == nseg - 1) && col < ldy) yr[col] = ((pattern >> sg) & 1u) ? lo : hi;
+  }
+}
+
 }  // namespace
+
+DL4SS_API int dl4ss_f32_to_bf16_hilo(const float* x, long long ldx, int rows, int cols, void* y, long long ldy,
+                                     int segw, int nseg, unsigned pattern, void* stream) {
+  DL4SS_REQUIRE(x && y && rows >= 0 && cols >= 0 && ldx >= cols && segw >= cols && nseg >= 1 && nseg <= 8);
+  DL4SS_REQUIRE(ldy >= (long long)nseg * segw);
+  if (rows == 0) return 0;
+  const int wrow = (int)std::max<long long>(segw, ldy - (long long)(nseg - 1) * segw);
+  const long long n = (long long)rows * wrow;
+  hipLaunchKernelGGL(f32_to_bf16_hilo_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), x,
+                     ldx, rows, cols, reinterpret_cast<unsigned short*>(y), ldy, segw, nseg, pattern);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
+}
 
 // y[r*ldy + c] = bf16(x[r*ldx + c]) for c < cols, 0 for cols <= c < ldy (row padding for 16-B rows)
 DL4SS_API int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy,

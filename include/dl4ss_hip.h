@@ -112,6 +112,13 @@ int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const int* M, cons
                                const void* const* A, const long long* lda, const void* const* B, const long long* ldb,
                                float* const* C, const long long* ldc, const float* beta, const int* splitk, void* ws,
                                long long ws_bytes, void* stream);
+/* Split-precision operand image: x = hi + lo (hi = bf16(x), lo = bf16(x - hi)); segment s of each
+ * row of y (width segw >= cols, zero-padded; s < nseg <= 8) holds hi, or lo when bit s of pattern
+ * is set; zeros up to ldy.  [x_hi | x_lo | x_hi] against weights [w_hi | w_hi | w_lo] makes one bf16
+ * GEMM with K' = 3 K fp32-accurate (~2^-16): the split forward GEMMs of the "bf16s" step, whose
+ * masked magnitude meets the 1e-3 bar on the BiGRU nets (EvalVer.py:282-299 nn.LSTM / Linear). */
+int dl4ss_f32_to_bf16_hilo(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, int segw,
+                           int nseg, unsigned pattern, void* stream);
 /* 2-D form with row padding: y[r*ldy + c] = bf16(x[r*ldx + c]) (c < cols), 0 up to ldy. */
 int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int cols, void* y, long long ldy, void* stream);
 /* out[n] += sum_m A[m*lda + n] for a bf16 matrix A (bias gradient from bf16 dPre). */

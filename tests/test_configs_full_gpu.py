@@ -35,20 +35,23 @@ MIXED = dict(precision="fp32", rnn_precision="bf16", tol_loss=1e-3, tol_grad=5e-
 # The all-bf16 operand mode misses 1e-3 on the BiGRU nets (measured C1 2.1e-3, C4 2.2e-3, C3 4.4e-3;
 # tools/parity_probe.py, profiles/r04_parity_configs.jsonl): checked here against its own 1e-2 bound
 # and never quoted as an in-bar throughput.
-MODES = {"fp32": {}, "mixed": MIXED, "bf16": BF16}
+# bf16s: the bf16 step with split-precision forward GEMMs and fp32 V (engine.SepTrainer); bf16
+# recurrence and backward -- the mode C1 / C3 / C4 throughput is quoted in, within the 1e-3 bar
+BF16S = dict(precision="bf16s", tol_loss=1e-3, tol_grad=5e-2, tol_pred=1e-3)
+MODES = {"fp32": {}, "mixed": MIXED, "bf16": BF16, "bf16s": BF16S}
 
 
-@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16"])
+@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16", "bf16s"])
 def test_c1_full_size(dev, mode):
     _compare_step(dev, "gru", 2, 1, 2, 40000, "label", loss_channels=101, adjust=False, **MODES[mode])
 
 
-@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16"])
+@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16", "bf16s"])
 def test_c4_full_size_3spk(dev, mode):
     _compare_step(dev, "gru", 2, 32, 3, 32000, "label", adjust=False, **MODES[mode])
 
 
-@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16"])
+@pytest.mark.parametrize("mode", ["fp32", "mixed", "bf16", "bf16s"])
 def test_c3_full_size_step(dev, mode):
     """The cRM step at B = 16: the masked complex spectrogram P = M (x) X within 1e-3 rel-L2 in
     fp32 (measured 1.2e-4) and mixed mode (6.1e-4); bf16 operands 4.4e-3 (bound 1e-2)."""

@@ -69,3 +69,43 @@ def test_bf16_conversions_keep_nan_payloads_nan(dev):
         assert torch.equal(torch.isnan(y2), torch.isnan(ref))
         fin = ~torch.isnan(ref)
         assert torch.equal(y2[fin].view(torch.int16), ref[fin].view(torch.int16))
+
+
+def test_f32_to_bf16_hilo_split_images(dev):
+    """dl4ss_f32_to_bf16_hilo (the bf16s step's split operands): hi = bf16(x), lo = bf16(x - hi),
+    segments by pattern, zero column padding to segw and to ldy -- bitwise against torch; and the
+    K-concatenated product [x_hi | x_lo | x_hi] . [w_hi | w_hi | w_lo] within 2e-5 of fp64 (the
+    single bf16 product: ~4e-3)."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    rows, cols, segw = 37, 129, 136
+    x = torch.randn(rows, cols + 3, generator=g).to(dev)[:, :cols]  # ldx 132 > cols
+    for pattern, ldy in ((0b010, 3 * segw), (0b100, 3 * segw + 8)):
+        y = torch.full((rows, ldy), -3.0, device=dev).to(torch.bfloat16)
+        _lib.call("dl4ss_f32_to_bf16_hilo", _lib.ptr(x, True), x.stride(0), rows, cols, _lib.ptr(y), ldy, segw, 3,
+                  pattern, _lib.stream_ptr())
+        torch.cuda.synchronize()
+        hi = x.cpu().to(torch.bfloat16)
+        lo = (x.cpu() - hi.float()).to(torch.bfloat16)
+        for sg in range(3):
+            ref = lo if (pattern >> sg) & 1 else hi
+            seg = y[:, sg * segw:sg * segw + cols].cpu()
+            assert torch.equal(seg.view(torch.int16), ref.view(torch.int16)), (pattern, sg)
+            assert bool((y[:, sg * segw + cols:(sg + 1) * segw].float() == 0).all())
+        assert bool((y[:, 3 * segw:].float() == 0).all())
+    # the split product
+    from dl4ss_amd import ops
+
+    M, N, K = 64, 48, 129
+    a = torch.randn(M, K, generator=g).to(dev)
+    w = torch.randn(N, K, generator=g).to(dev)
+    A = torch.empty(M, 3 * segw, device=dev, dtype=torch.bfloat16)
+    W = torch.empty(N, 3 * segw, device=dev, dtype=torch.bfloat16)
+    for t, img, pat in ((a, A, 0b010), (w, W, 0b100)):
+        _lib.call("dl4ss_f32_to_bf16_hilo", _lib.ptr(t), t.stride(0), t.shape[0], K, _lib.ptr(img), img.stride(0), segw,
+                  3, pat, _lib.stream_ptr())
+    C = ops.gemm_bf16_gl(A, W, transB=True)
+    ref = a.double().cpu() @ w.double().cpu().t()
+    mag = a.abs().double().cpu() @ w.abs().double().cpu().t()
+    assert float(((C.double().cpu() - ref).abs() / mag).max()) < 2e-5
+    C1 = ops.gemm_bf16_gl(A[:, :segw], W[:, :segw], transB=True)
+    assert float(((C1.double().cpu() - ref).abs() / mag).max()) > 2e-4  # the plain bf16 product, for contrast

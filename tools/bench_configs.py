@@ -121,7 +121,7 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5", "c5x32"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
+    ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16", "bf16s"])
     ap.add_argument("--rnn-precision", default=None, choices=["fp32", "bf16"],
                     help="recurrent matvec precision (default: --precision)")
     a = ap.parse_args()

@@ -22,7 +22,7 @@ from oracle import model as om  # noqa: E402
 from oracle import recursive as orc  # noqa: E402
 from test_step_gpu import _oracle_features  # noqa: E402
 
-MODES = [("bf16", "bf16"), ("fp32", "bf16"), ("fp32", "fp32")]
+MODES = [("bf16", "bf16"), ("bf16s", "bf16"), ("fp32", "bf16"), ("fp32", "fp32")]
 
 
 def masked_rel(cell, L, B, K, N, mode, adjust, loss_channels=None, seed=3, modes=MODES):
