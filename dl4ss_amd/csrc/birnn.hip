@@ -1056,6 +1056,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
           st[0] = rg; st[1] = zg; st[2] = ng; st[3] = hg[2];
         }
       }
+      STAMP(5)
       // stage bf16 h (padded rows / units >= H stage zeros) and publish: lanes 0-3 of
       // each row read 6 staged values (LDS is in order within the wave) and store two
       // tagged granules with one 16-B write-through store
@@ -1073,6 +1074,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         else
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);   // plain: stays in the group's L2
       }
+      STAMP(6)
       if (tid == 0) TRACE(0, s);
 #ifdef EXP_FWD_NO_SAVE
       if (false) {
@@ -1838,6 +1840,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       }
       if (wv == 3) TRACE(0, s);
     }
+    STAMP(5)
     // this step's dG / dGh, after the publish (off the critical path; issued after B1 of the next
     // step instead they measured slower, 7994 vs 8085 mixtures/s, round 3)
     store_dg();

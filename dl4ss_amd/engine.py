@@ -170,7 +170,7 @@ class SepTrainer:
         # (DL4SS_RNN_WS_ZEROED) instead of a memset in front of every recurrence launch
         w8 = (ws + 255) // 256 * 32
         self.rnn_ws_all = torch.empty(2, net.L * w8, device=dev, dtype=torch.int64)  # [fwd | bwd][layer]
-        self._ws_slot = lambda l, bwd: self.rnn_ws_all[int(bwd), l * w8:(l + 1) * w8]
+        self._w8 = w8
         # {hand-off timed out, refused-update count} (the recurrence kernels set [0]; the guarded
         # Adam counts its refusals in [1])
         self.status = torch.zeros(2, device=dev, dtype=torch.int32)
@@ -623,6 +623,12 @@ class SepTrainer:
         self.forward()
         return self.loss_and_grad()
 
+    def _ws_slot(self, l, bwd):
+        """Layer l's hand-off workspace of the forward (bwd False) or BPTT pass.  (A method, not a
+        lambda holding self: a reference cycle leaves a dropped trainer to the garbage collector,
+        which could then free its device buffers in the middle of another trainer's graph capture.)"""
+        return self.rnn_ws_all[int(bwd), l * self._w8:(l + 1) * self._w8]
+
     def capture(self):
         """Record STFT -> forward -> loss -> backward (~70 launches: persistent BiRNN
         kernels, gemm_gl GEMMs, attention, small kernels) as one HIP graph, replayed by
@@ -630,11 +636,22 @@ class SepTrainer:
         all-reduce and Adam (its bias correction is a per-step host scalar) stay eager launches
         around the replay.  Call after at least one eager step(), so every workspace exists
         before the capture."""
+        import gc
+
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._graph_loss = self._graph_body()
-            self.backward()
+        # no garbage collection while the stream is being captured: a collection that frees another
+        # object's device memory mid-capture aborted the process (round 4, a dropped trainer's buffers)
+        gc.collect()
+        was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g):
+                self._graph_loss = self._graph_body()
+                self.backward()
+        finally:
+            if was_enabled:
+                gc.enable()
         torch.cuda.synchronize()
         self.graph = g
         return g

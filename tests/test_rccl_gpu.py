@@ -9,6 +9,7 @@ step with ``process_group=pg`` -- status flag behind the flat gradient -> RCCL a
 * A forced hand-off timeout (dl4ss_debug_set_spin_limit) travels through the real all-reduce as
   the status flag and the guarded Adam refuses the update (the DP refusal path, not a faked flag).
 """
+import gc
 import socket
 
 import numpy as np
@@ -74,6 +75,7 @@ def test_rccl_world1_graph_step_bitwise_equal_to_single_gpu(dev, pg, name):
         runs[tag] = dict(loss=losses, grad=tr.net.grad_ext.clone(), flat=tr.net.flat.clone(), m=tr.m.clone(),
                          v=tr.v.clone(), status=tr.status.tolist(), steps=tr.step_count)
         del tr
+        gc.collect()
         torch.cuda.empty_cache()
     a, b = runs["single"], runs["rccl"]
     assert all(np.isfinite(a["loss"])) and a["loss"] == b["loss"]

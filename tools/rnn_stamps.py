@@ -39,7 +39,9 @@ def main():
 
     dev = torch.device("cuda")
     Bsz, T, H = 32, 251, 300
-    net = engine.SepNet(cell="lstm", num_layers=1, device=dev)
+    # two layers: the forward stamps are the last forward launch's (layer 1, the 600-wide fused
+    # projection, as 3 of the 4 C2 layers), the BPTT stamps the last BPTT launch's (layer 0)
+    net = engine.SepNet(cell="lstm", num_layers=int(os.environ.get("STAMP_LAYERS", "2")), device=dev)
     prec = "bf16" if "--bf16" in sys.argv else "fp32"
     tr = engine.SepTrainer(net, Bsz, 2, 32000, precision=prec)
     stamps = torch.zeros(240 * 16, dtype=torch.int64, device=dev)
@@ -61,8 +63,11 @@ def main():
         tr.backward()
         torch.cuda.synchronize()
         bw = stamps.view(240, 16).double().cpu() / T
-    names_f = ["gather", "bar1", "matvec", "bar2", "cell"]
-    names_b = ["gather", "bar1", "cell", "bar2", "matvec/mfma", "bar3", "publish"]
+    # slot i = cycles from the previous stamp to STAMP(i) (birnn.hip): forward cell waves
+    # B2 -> gates (5) -> publish store issued (6) -> saved-state stores (4); BPTT cell waves
+    # B2 -> MFMA + transpose (4) -> granule publish (5) -> dG stores (6)
+    names_f = ["gather", "bar1", "matvec", "bar2", "saves", "gates", "publish"]
+    names_b = ["gather", "bar1", "cell", "bar2", "matvec/mfma", "publish", "dg_stores"]
     print(f"precision {prec}")
     for title, st, names in (("fwd", fw, names_f), ("bwd", bw, names_b)):
         for role, off in (("thread0 (cell/publish)", 0), ("thread256 (gather)", 8)):
