@@ -553,6 +553,13 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
 #endif
+// s_sleep (units of 64 cycles) between the polling waves' sweeps (0: back to back)
+#ifndef FWD_POLL_SLEEP
+#define FWD_POLL_SLEEP 0
+#endif
+#ifndef BWD_POLL_SLEEP
+#define BWD_POLL_SLEEP 0
+#endif
 constexpr int FWD_MV_CHAINS = 2;  // forward bf16 matvec: accumulator chains per MFMA tile (4: 367 vs 363 us per pass)
 #ifndef FWD_NPW
 #define FWD_NPW 2  // forward polling waves: 4, and 7 when >= 2, and 6 when 3 (their MFMA tile indices must be >= MT)
@@ -939,6 +946,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifdef RNN_TRACE
           if (spins == 0) TRACE(3, s);
 #endif
+          if (FWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(FWD_POLL_SLEEP);
           asm volatile("" ::: "memory");
 #pragma unroll
           for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
@@ -949,6 +957,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
+          if (FWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(FWD_POLL_SLEEP);
           if (++spins > a.spin_limit) {
             atomicOr(a.status, 1);
             return;
@@ -1639,6 +1648,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
+          if (BWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(BWD_POLL_SLEEP);
           asm volatile("" ::: "memory");
 #pragma unroll
           for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, sb + loff[g] * 8, 0, 16);
@@ -1649,6 +1659,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
+          if (BWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(BWD_POLL_SLEEP);
           if (++spins > a.spin_limit) {
             atomicOr(a.status, 2);
             return;
