@@ -553,13 +553,6 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #ifndef BWD_NPW
 #define BWD_NPW 2  // BPTT polling waves
 #endif
-// s_sleep (units of 64 cycles) between the polling waves' sweeps (0: back to back)
-#ifndef FWD_POLL_SLEEP
-#define FWD_POLL_SLEEP 0
-#endif
-#ifndef BWD_POLL_SLEEP
-#define BWD_POLL_SLEEP 0
-#endif
 constexpr int FWD_MV_CHAINS = 2;  // forward bf16 matvec: accumulator chains per MFMA tile (4: 367 vs 363 us per pass)
 #ifndef FWD_NPW
 #define FWD_NPW 2  // forward polling waves: 4, and 7 when >= 2, and 6 when 3 (their MFMA tile indices must be >= MT)
@@ -946,7 +939,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifdef RNN_TRACE
           if (spins == 0) TRACE(3, s);
 #endif
-          if (FWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(FWD_POLL_SLEEP);
           asm volatile("" ::: "memory");
 #pragma unroll
           for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
@@ -957,7 +949,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
-          if (FWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(FWD_POLL_SLEEP);
           if (++spins > a.spin_limit) {
             atomicOr(a.status, 1);
             return;
@@ -1085,11 +1076,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       }
       STAMP(6)
       if (tid == 0) TRACE(0, s);
-#ifdef EXP_FWD_NO_SAVE
-      if (false) {
-#else
       if (cval) {
-#endif
         const long long bt = (long long)bg * T + t;
         float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
         actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
@@ -1648,7 +1635,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
-          if (BWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(BWD_POLL_SLEEP);
           asm volatile("" ::: "memory");
 #pragma unroll
           for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, sb + loff[g] * 8, 0, 16);
@@ -1659,7 +1645,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             done |= (unsigned)m << g;
           }
           if (done == (1u << GLK) - 1) break;
-          if (BWD_POLL_SLEEP) __builtin_amdgcn_s_sleep(BWD_POLL_SLEEP);
           if (++spins > a.spin_limit) {
             atomicOr(a.status, 2);
             return;
@@ -1713,9 +1698,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 #pragma unroll
   for (int q = 0; q < NGATE; ++q) sbi[q] = sbh[q] = pgi[q] = pgh[q] = 0.0f;
   auto store_dg = [&]() {
-#ifdef EXP_BWD_NO_DG
-    return;
-#endif
     if (!cval) return;
     const long long go = (long long)((bg * T + pt) * 2 + d) * GH + cj;
     if (a.dG) {

@@ -675,11 +675,12 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_gl_grouped_kernel(GlGroup g) {
   const int local = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + Ll / 8;
   const int ntiles = p.gm * p.gn;
   const int zsplit = local / ntiles, tile = local % ntiles;
-  constexpr int GROUP = 8;
-  const int gsize = GROUP * p.gn;
-  const int first_m = (tile / gsize) * GROUP;
-  const int gm_here = min(p.gm - first_m, GROUP);
-  const int tm = first_m + (tile % gsize) % gm_here, tn = (tile % gsize) / gm_here;
+  // n fastest: an XCD's contiguous tile range covers whole rows of M-panels, so every A panel
+  // (the big operand of these weight gradients: dPre 103.6 MB, each layer's dG 38.6 MB) is fetched
+  // into one XCD's L2 once and shared by its gn N-tiles there; the small B operand (layer inputs,
+  // h_{t-1}: <= 9.6 MB) is what each XCD re-reads
+  // (the single launch's GROUP = 8 m-swizzle here: 8090 vs 8101 mixtures/s, round 4)
+  const int tm = tile / p.gn, tn = tile % p.gn;
   const int m0 = tm * CF::BM, n0 = tn * BN;
   const int kbeg = zsplit * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
