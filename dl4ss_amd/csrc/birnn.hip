@@ -622,7 +622,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const int lane = tid & 63, wv = tid >> 6;
   const int GH = NGATE * H;
   const int tile = wv < WPOLL ? wv : wv - 1;
-  const bool mv = wv != WPOLL && tile < MT;
+  // With 5 MFMA tiles (LSTM, J = 20) tile 4 runs as two k-step halves on the polling waves 4 and
+  // 7 -- idle from B1 to B2 and on SIMDs 0 and 3 -- instead of whole on wave 5, which shares SIMD 1
+  // with wave 1's tile (stamps: every wave waited ~285 cycles at B2 for it).  Wave 4 takes the
+  // even k-steps, wave 7 the odd ones: exactly the two accumulator chains of a whole-tile matvec
+  // (FWD_MV_CHAINS = 2), summed in the same order by the cell lanes -- bitwise the same gates.
+  const bool t4h = MT == 5 && FWD_NPW == 2;
+  const bool mv = wv != WPOLL && tile < MT && !(t4h && tile == 4);
+  const bool mvh = t4h && (wv == WPOLL || wv == 7);
   const int SGS = MT * 16 + 4;  // sgate row stride (floats): 4 batch rows on 4 distinct bank quads
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -631,10 +638,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   // reads are conflict-free, tools/lds_banks.py)
   unsigned short* shb = reinterpret_cast<unsigned short*>(smem);
   float* sgate = smem + 8 * SHB;                                                        // [BC][SGS]
+  float* sgx = sgate + BC * SGS;  // tile 4's odd-k-step chain (wave 7) [BC][16]; the even one is in sgate
   // per-step input projections [NSIN][BC*32][4]: double buffered, or with XW two blocks of SPB steps
   constexpr int SPB = xw_spb(BC);
   constexpr int NSIN = XW ? 2 * SPB : 2;
-  float* sin = sgate + BC * SGS;
+  float* sin = sgx + BC * 16;
   unsigned short* spub = reinterpret_cast<unsigned short*>(sin + NSIN * BC * 32 * 4);   // [BC][PKU]
   // XW: the ring of 3 * SPB step slots of the layer-input rows ([BC][SXB] bf16 + the pad items of
   // the last DMA piece), 256-B aligned (the bank order of its rows)
@@ -863,6 +871,41 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   using XPF = std::integral_constant<int, 2>;
   using XPL = std::integral_constant<int, 1>;
 
+  // tile 4's half on a polling wave: the even (wave 4, into sgate's tile-4 columns) or odd (wave 7,
+  // into sgx) k-steps as one accumulator chain in k order; afh[i] holds k-step 2i + (wave 7), loaded
+  // inside the polling role (dead in every other role)
+  constexpr int KH = (KSMAX + 1) / 2;
+  auto load_half = [&](bf16x8* afh) __attribute__((always_inline)) {
+    const int rl = 4 * 16 + (lane & 15);
+    const int q = rl / J, u = rl % J;
+    const bool rv = mvh && rl < R && j0 + u < H;
+    const int kpar = wv == 7 ? 1 : 0;
+    const float* wrow = a.Whh + ((long long)d * GH + q * H + j0 + u) * H;
+#pragma unroll
+    for (int i = 0; i < KH; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 2 * i + kpar;
+        const int k = kk * 32 + 8 * (lane >> 4) + j;
+        afh[i][j] = (short)bf16_rne((rv && kk < KSMAX && k < H) ? wrow[k] : 0.0f);
+      }
+  };
+  auto matvec_half = [&](const bf16x8* afh) __attribute__((always_inline)) {
+    const int kpar = wv == 7 ? 1 : 0;
+    const unsigned short* bp = shb + min(lane & 15, BC) * SHB + 8 * (lane >> 4) + kpar * 32;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < KH; ++i)
+      if (2 * i + kpar < KSMAX)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afh[i], *reinterpret_cast<const bf16x8*>(bp + i * 64), acc, 0,
+                                                      0, 0);
+    const int col = lane & 15;
+    if (col < BC) {
+      float* dst = wv == 7 ? sgx + col * 16 : sgate + col * SGS + 4 * 16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[(lane >> 4) * 4 + i] = acc[i];
+    }
+  };
   // sgate[b][tile*16 + row] = sum_k W[row][k] h[b][k]
   auto matvec = [&]() __attribute__((always_inline)) {
     if (!mv) return;
@@ -892,6 +935,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 
   if (pollw) {
     if (XW) xstart(XPL{});
+    bf16x8 afh[KH];
+    load_half(afh);
     // ---- polling wave(s): 16-B unit idx = (b * NG + producer) * 4 + pair; lane holds
     //      units lane + 64 (g FWD_NPW + pwv) (idle lanes re-read unit 0: every load is
     //      unconditional, so the compiler can keep a sweep in flight behind a counted vmcnt)
@@ -968,6 +1013,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       STAMP(0)
       __syncthreads();  // B1
       STAMP(1)
+      if (mvh) matvec_half(afh);
       STAMP(2)
       __syncthreads();  // B2
       STAMP(3)
@@ -1035,9 +1081,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         const int sb = XW ? ((s / SPB) & 1) * SPB + s % SPB : (s & 1);
         const float4 g4 = *reinterpret_cast<const float4*>(sin + sb * BC * 32 * 4 + tid * 4);  // one 16-B read
         const float gxa[4] = {g4.x, g4.y, g4.z, g4.w};
+        // tile 4 (rows 64..79: with J = 20 only gate 3's units 4..19): even chain + odd chain, as the
+        // whole-tile matvec's acc[0] + acc[1]; read unconditionally (a clamped address) and selected
+        const int r3 = (NGATE - 1) * J + cu;
+        const float x4 = sgx[cb * 16 + max(r3 - 64, 0)];
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
-          hg[q] = bh[q] + sgate[cb * SGS + q * J + cu];
+          float mq = sgate[cb * SGS + q * J + cu];
+          if (q == NGATE - 1) mq = (t4h && r3 >= 64) ? mq + x4 : mq;
+          hg[q] = bh[q] + mq;
           gx[q] = gxa[q];
         }
         if constexpr (CELL == CELL_LSTM) {
@@ -1981,7 +2033,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) 
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
     p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((16 * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16 + 4) +
                                                     2 * 2 * (BC * 32 * 4 + 16));
-    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + 2 * BC * 32 * 4) + 2 * BC * PKU;
+    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + BC * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
     return true;
   }
   return false;
