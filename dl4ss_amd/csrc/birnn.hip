@@ -893,12 +893,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   auto matvec_half = [&](const bf16x8* afh) __attribute__((always_inline)) {
     const int kpar = wv == 7 ? 1 : 0;
     const unsigned short* bp = shb + min(lane & 15, BC) * SHB + 8 * (lane >> 4) + kpar * 32;
+    bf16x8 bv[KH];
+#pragma unroll
+    for (int i = 0; i < KH; ++i)
+      if (2 * i + kpar < KSMAX) bv[i] = *reinterpret_cast<const bf16x8*>(bp + i * 64);
+    __builtin_amdgcn_sched_barrier(0);  // every B read before the first MFMA (one LDS round trip)
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < KH; ++i)
-      if (2 * i + kpar < KSMAX)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afh[i], *reinterpret_cast<const bf16x8*>(bp + i * 64), acc, 0,
-                                                      0, 0);
+      if (2 * i + kpar < KSMAX) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afh[i], bv[i], acc, 0, 0, 0);
     const int col = lane & 15;
     if (col < BC) {
       float* dst = wv == 7 ? sgx + col * 16 : sgate + col * SGS + 4 * 16;
