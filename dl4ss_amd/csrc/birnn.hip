@@ -138,6 +138,21 @@ __device__ __forceinline__ float sum_partials16(const float* p, int stride) {
     for (int i = 0; i < w; ++i) v[i] += v[i + w];
   return v[0];
 }
+// Sum of N slot partials p[i * stride], i < N, as a fixed pairwise tree over the next power of two
+// (missing leaves are zero): deterministic, and for N = 16 the tree of sum_partials16.
+template <int N>
+__device__ __forceinline__ float sum_slots(const float* p, int stride) {
+  constexpr int P2 = N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : 16;
+  static_assert(N >= 1 && N <= 16, "1..16 slots");
+  float v[P2];
+#pragma unroll
+  for (int i = 0; i < P2; ++i) v[i] = i < N ? p[i * stride] : 0.0f;
+#pragma unroll
+  for (int w = P2 / 2; w > 0; w >>= 1)
+#pragma unroll
+    for (int i = 0; i < w; ++i) v[i] += v[i + w];
+  return v[0];
+}
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
   unsigned u = __float_as_uint(f);
@@ -1523,6 +1538,13 @@ __device__ __forceinline__ float unpack24(unsigned r) { return __uint_as_float(r
 template <int CELL, int BC>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
+  // partial-sum slots of the gather (polling waves): a lane group of BSL_Q lanes = every (b, quad)
+  // of one slot at J <= 20; BSL_G groups per polling wave; BSL_N slots; GLK producers per lane
+  constexpr int BSL_Q = BC * 5;
+  constexpr int BSL_G = 64 / BSL_Q > 0 ? 64 / BSL_Q : 1;
+  constexpr int BSL_N = BWD_NPW * BSL_G < 16 ? BWD_NPW * BSL_G : 16;
+  constexpr int GLK = (16 + BSL_N - 1) / BSL_N;  // NG <= 16
+  static_assert(BSL_Q <= 64, "one (b, quad) item per lane");
   constexpr int MTWMAX = (HMAX / 16 + 3) / 4;  // MFMA unit tiles per wave (5)
   constexpr int KSRMAX = (4 * 20 + 31) / 32;   // MFMA K-steps over gate rows (3)
   constexpr int SDG = KSRMAX * 32 + 8;         // bf16 row stride of the dgh B image
@@ -1648,22 +1670,27 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   STAMP_DECL
 
   if (wv >= WPOLL && wv < WPF) {
-    // ---- polling waves: 16-B unit idx = (producer * BC + b) * (J/4) + quad, wave pw
-    //      takes the 64-unit blocks pw, pw + BWD_NPW, ...
-    constexpr int GLK = (80 * BC + 64 * BWD_NPW - 1) / (64 * BWD_NPW);  // NG <= 16, J <= 20
+    // ---- polling waves: a lane owns one (b, quad of 4 units) and BSL_P producers of it -- slot
+    //      sl = pw * BSL_G + (lane / (5 BC)), producers sl, sl + BSL_N, ... -- and sums their
+    //      partials in registers: the cell lanes then add BSL_N slot partials instead of NG
+    //      producer partials (16 LDS reads + a 16-leaf tree cost ~150 cycles of the cell phase,
+    //      round-4 stamps).  Lanes of a group read consecutive quads of one producer row (the
+    //      sweep touches as many cache lines as a producer-major map).
     const int pw = wv - WPOLL;
     const int JQ = J / 4;
-    const int n16 = NG * BC * JQ;
-    int loff[GLK], doff[GLK];
+    const int gi = lane / BSL_Q, bq = lane % BSL_Q;
+    const int pb_b = bq / 5, qd = bq % 5;
+    const int sl = pw * BSL_G + gi;
+    const bool lane_on = gi < BSL_G && sl < BSL_N && qd < JQ && pb_b < BC;
+    int loff[GLK];
     bool on[GLK];
 #pragma unroll
     for (int g = 0; g < GLK; ++g) {
-      const int idx = lane + 64 * (g * BWD_NPW + pw);
-      on[g] = idx < n16;
-      const int pb = idx / JQ, qd = idx % JQ;  // pb = producer * BC + b
-      loff[g] = on[g] ? pb * HG + (j0 >> 1) + 2 * qd : 0;  // granule offset within a copy
-      doff[g] = on[g] ? pb * J + 4 * qd : 0;               // sdh[(p * BC + b) * J + u]
+      const int p = sl + BSL_N * g;
+      on[g] = lane_on && p < NG;
+      loff[g] = on[g] ? (p * BC + pb_b) * HG + (j0 >> 1) + 2 * qd : 0;  // granule offset within a copy
     }
+    const int doff = lane_on ? (sl * BC + pb_b) * J + 4 * qd : 0;  // sdh[(slot * BC + b) * J + u]
     for (int s = 0; s < T; ++s) {
       if (s > 0) {
         const unsigned tag = (unsigned)s & 0xFFFFu;
@@ -1705,15 +1732,18 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
             return;
           }
         }
+        float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);  // this lane's producers, summed in order g
 #pragma unroll
         for (int g = 0; g < GLK; ++g) {
           if (on[g]) {
             const unsigned l0 = q[g].x, l1 = q[g].y, h0 = q[g].z, h1 = q[g].w;
-            const float4 v = make_float4(unpack24(l0 & 0xFFFFFFu), unpack24((l0 >> 24) | ((l1 & 0xFFFFu) << 8)),
-                                         unpack24(h0 & 0xFFFFFFu), unpack24((h0 >> 24) | ((h1 & 0xFFFFu) << 8)));
-            *reinterpret_cast<float4*>(sdh + doff[g]) = v;  // 16-B aligned: J % 4 == 0
+            acc4.x += unpack24(l0 & 0xFFFFFFu);
+            acc4.y += unpack24((l0 >> 24) | ((l1 & 0xFFFFu) << 8));
+            acc4.z += unpack24(h0 & 0xFFFFFFu);
+            acc4.w += unpack24((h0 >> 24) | ((h1 & 0xFFFFu) << 8));
           }
         }
+        if (lane_on) *reinterpret_cast<float4*>(sdh + doff) = acc4;  // 16-B aligned: J % 4 == 0
         if (wv == WPOLL) TRACE(1, s);
       }
       STAMP(0)
@@ -1791,11 +1821,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         // them in the same LDS round trip (sdh is zero before the first gather)
         const float4 o0 = *reinterpret_cast<const float4*>(sop + (s & 1) * 2 * SOPP + tid * 4);
         const float4 o1 = *reinterpret_cast<const float4*>(sop + (s & 1) * 2 * SOPP + SOPP + tid * 4);
-        const float dh_rec = sum_partials16(sdh + cb * J + cu, BC * J);
+        const float dh_rec = sum_slots<BSL_N>(sdh + cb * J + cu, BC * J);
         const float dout = o0.x + doutb;
         const float act[4] = {o0.y, o0.z, o0.w, o1.x};
         const float c = o1.y, cprev = o1.z, hprev = o1.y;
         const float dh = dout + dh_rec + dh_dir;
+        STAMP(7)
         if constexpr (CELL == CELL_LSTM) {
           const float ig = act[0], fg = act[1], gg = act[2], og = act[3];
           const float tc = ftanh(c);

@@ -200,6 +200,7 @@ class SepTrainer:
             raise ValueError("precision 'bf16s' runs the bf16 recurrence (rnn_precision bf16)")
         self.fast = precision in ("bf16", "bf16s") and self.rnn_precision == "bf16"
         self.dh_split = int(os.environ.get("DL4SS_DH_SPLIT", "3"))  # dH split-K (tuning knob, A/B runs)
+        self.dx_split = int(os.environ.get("DL4SS_DX_SPLIT", "1"))  # dX split-K (tuning knob, A/B runs)
         # Forward input projections x W_ih^T + b_ih formed inside the packed recurrence kernel
         # (dl4ss_birnn_fwd_xw) instead of a gemm_gl launch + a G buffer round trip; bitwise the same
         # G (tests/test_rnn_xw_gpu.py).  Each tile's projection of a block of 16 / BC steps is one
@@ -234,6 +235,7 @@ class SepTrainer:
             # gemm_gl split-K slabs (the largest split of _backward_fast)
             FE_ = F * net.E
             gl_need = max(_lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, FE_, max(1, self.dh_split), 1),
+                          _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, 2 * NGH, max(1, self.dx_split), 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", FE_, 2 * H, BT, 2, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", 2 * NGH, 2 * H, BT, 4, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", NGH, H, BT, 8, 2))
@@ -501,7 +503,7 @@ class SepTrainer:
                       _lib.ptr(self.status), st)
             if l > 0:  # the input gradient: all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
-                ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next)
+                ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk=self.dx_split, ws=self.gl_ws)
             if not grouped:
                 xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
                 ops.gemm_bf16_gl(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), beta=1.0, splitk=4,

@@ -65,9 +65,10 @@ def main():
         bw = stamps.view(240, 16).double().cpu() / T
     # slot i = cycles from the previous stamp to STAMP(i) (birnn.hip): forward cell waves
     # B2 -> gates (5) -> publish store issued (6) -> saved-state stores (4); BPTT cell waves
-    # B2 -> MFMA + transpose (4) -> granule publish (5) -> dG stores (6)
+    # B2 -> MFMA + transpose (4) -> granule publish (5) -> dG stores (6); BPTT cell phase B1 ->
+    # operand / partial-sum reads (7) -> math and the bf16 dgh image (2)
     names_f = ["gather", "bar1", "matvec", "bar2", "saves", "gates", "publish"]
-    names_b = ["gather", "bar1", "cell", "bar2", "matvec/mfma", "publish", "dg_stores"]
+    names_b = ["gather", "bar1", "cell_math", "bar2", "matvec/mfma", "publish", "dg_stores", "cell_reads"]
     print(f"precision {prec}")
     for title, st, names in (("fwd", fw, names_f), ("bwd", bw, names_b)):
         for role, off in (("thread0 (cell/publish)", 0), ("thread256 (gather)", 8)):
