@@ -28,6 +28,7 @@ SIGNATURES = {
     "dl4ss_f32_to_bf16": [P, P, LL, P],
     "dl4ss_f32_to_bf16_2d": [P, LL, I, I, P, LL, P],
     "dl4ss_f32_to_bf16_hilo": [P, LL, I, I, P, LL, I, I, U, P],
+    "dl4ss_birnn_bias_reduce": [I, I, I, I, P, P, P, P],
     "dl4ss_colsum_bf16": [P, LL, I, I, P, P],
     "dl4ss_colsum_bf16_part_bytes": [I, I],
     "dl4ss_colsum_bf16_det": [P, LL, I, I, P, P, LL, P],

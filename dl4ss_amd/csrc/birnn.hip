@@ -53,6 +53,7 @@ constexpr int HMAX = 320;    // largest hidden size of the training kernels (siz
 constexpr int HMAX_L = 640;  // largest hidden size of the forward-only (inference) instantiations: the
                              // H = 600 speaker classifier of EvalVer.py:305-326 / GRID.py:178-199
 constexpr int DL4SS_RNN_WS_ZEROED = 0x100;  // precision flag: workspace already zero (no memset)
+constexpr int DL4SS_RNN_DEFER_BIAS = 0x400;  // BPTT: leave the per-row bias partials for dl4ss_birnn_bias_reduce
 constexpr int DL4SS_RNN_DGH_PAD8 = 0x200;  // precision flag (bwd): dGh_bf16 direction stride padded to 8
 constexpr unsigned SPIN_LIMIT = 1u << 20;  // ~1 s of polling: a stuck hand-off exits, never hangs
 
@@ -2162,11 +2163,24 @@ DL4SS_API void dl4ss_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<uns
 #endif
 
 // dbi[i] += sum_b part[b][d][0][g], dbh[i] += sum_b part[b][d][1][g] for i = d * GH + g, rows
-// in order b = 0 .. B-1 (the BPTT kernel's per-row bias sums)
-__global__ __launch_bounds__(256) void bias_reduce_kernel(const float* __restrict__ part, int B, int GH,
-                                                          float* __restrict__ dbi, float* __restrict__ dbh) {
+// in order b = 0 .. B-1 (the BPTT kernel's per-row bias sums); blockIdx.y = the job (layer)
+constexpr int BIAS_JOBS_MAX = 8;
+struct BiasJobs {
+  int n, B, GH;
+  const float* part[BIAS_JOBS_MAX];
+  float* dbi[BIAS_JOBS_MAX];
+  float* dbh[BIAS_JOBS_MAX];
+};
+__global__ __launch_bounds__(256) void bias_reduce_kernel(BiasJobs j) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  const int B = j.B, GH = j.GH;
   if (i >= 2 * GH) return;
+  const float* part = j.part[0];
+  float* dbi = j.dbi[0];
+  float* dbh = j.dbh[0];
+#pragma unroll
+  for (int k = 1; k < BIAS_JOBS_MAX; ++k)
+    if (k == (int)blockIdx.y) { part = j.part[k]; dbi = j.dbi[k]; dbh = j.dbh[k]; }
   const int d = i / GH, g = i - d * GH;
   float si = 0.0f, sh = 0.0f;
   // rows in chunks of 8 with every load of a chunk issued before its adds (a row-by-row
@@ -2375,7 +2389,8 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
   const bool prezeroed = precision & DL4SS_RNN_WS_ZEROED;
   const bool dgh_pad8 = precision & DL4SS_RNN_DGH_PAD8;
-  precision &= ~(DL4SS_RNN_WS_ZEROED | DL4SS_RNN_DGH_PAD8);
+  const bool defer_bias = precision & DL4SS_RNN_DEFER_BIAS;
+  precision &= ~(DL4SS_RNN_WS_ZEROED | DL4SS_RNN_DGH_PAD8 | DL4SS_RNN_DEFER_BIAS);
   DL4SS_REQUIRE(precision == 0 || precision == 1);
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && workspace && status);
   DL4SS_REQUIRE(dG || dG_bf16);
@@ -2412,8 +2427,33 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   const size_t smem = pk ? p.smem_bwd_pk : mf ? p.smem_bwd_mf : p.smem_bwd;
   const int e = cell == CELL_LSTM ? dispatch<CELL_LSTM>(false, mf, pk, p.BC, a, grid, smem, st)
                                   : dispatch<CELL_GRU>(false, mf, pk, p.BC, a, grid, smem, st);
-  if (e || !bias) return e;
+  if (e || !bias || defer_bias) return e;
   const int GH = (cell == CELL_LSTM ? 4 : 3) * H;
-  hipLaunchKernelGGL(bias_reduce_kernel, dim3((2 * GH + 255) / 256), dim3(256), 0, st, a.dbpart, B, GH, db_ih, db_hh);
+  BiasJobs j{};
+  j.n = 1; j.B = B; j.GH = GH; j.part[0] = a.dbpart; j.dbi[0] = db_ih; j.dbh[0] = db_hh;
+  hipLaunchKernelGGL(bias_reduce_kernel, dim3((2 * GH + 255) / 256, 1), dim3(256), 0, st, j);
   return (int)hipGetLastError();
+}
+
+// The deferred form: the bias partials of n BPTT launches (DL4SS_RNN_DEFER_BIAS) reduced by ONE
+// launch after the last of them -- the per-layer reduce was a 5 us latency-bound launch between
+// each BPTT and the input-gradient GEMM that the next BPTT waits on.
+DL4SS_API int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
+                                      float* const* db_hh, void* stream) {
+  DL4SS_REQUIRE((cell == CELL_LSTM || cell == CELL_GRU) && B > 0 && H > 0 && n >= 1 && n <= BIAS_JOBS_MAX);
+  DL4SS_REQUIRE(workspaces && db_ih && db_hh);
+  Plan p;
+  if (!make_plan(cell, B, H, p, true)) return (int)hipErrorInvalidValue;  // the bf16 BPTT's plan
+  const int GH = (cell == CELL_LSTM ? 4 : 3) * H;
+  BiasJobs j{};
+  j.n = n; j.B = B; j.GH = GH;
+  for (int i = 0; i < n; ++i) {
+    DL4SS_REQUIRE(workspaces[i] && db_ih[i] && db_hh[i]);
+    j.part[i] = reinterpret_cast<const float*>(static_cast<const char*>(workspaces[i]) + handoff_bytes(p, H));
+    j.dbi[i] = db_ih[i];
+    j.dbh[i] = db_hh[i];
+  }
+  hipLaunchKernelGGL(bias_reduce_kernel, dim3((2 * GH + 255) / 256, n), dim3(256), 0, as_stream(stream), j);
+  DL4SS_CHECK_LAUNCH();
+  return 0;
 }

@@ -26,6 +26,7 @@ from . import _lib, ops
 CELLS = {"lstm": 0, "gru": 1}
 WS_ZEROED = 0x100  # DL4SS_RNN_WS_ZEROED (include/dl4ss_hip.h)
 DGH_PAD8 = 0x200  # DL4SS_RNN_DGH_PAD8
+DEFER_BIAS = 0x400  # DL4SS_RNN_DEFER_BIAS
 
 
 def _ngate(cell):
@@ -201,6 +202,8 @@ class SepTrainer:
         self.fast = precision in ("bf16", "bf16s") and self.rnn_precision == "bf16"
         self.dh_split = int(os.environ.get("DL4SS_DH_SPLIT", "3"))  # dH split-K (tuning knob, A/B runs)
         self.dx_split = int(os.environ.get("DL4SS_DX_SPLIT", "1"))  # dX split-K (tuning knob, A/B runs)
+        # BPTT bias partials reduced once after the last BPTT instead of after each (A/B knob)
+        self.defer_bias = os.environ.get("DL4SS_DEFER_BIAS", "1") != "0"
         # Forward input projections x W_ih^T + b_ih formed inside the packed recurrence kernel
         # (dl4ss_birnn_fwd_xw) instead of a gemm_gl launch + a G buffer round trip; bitwise the same
         # G (tests/test_rnn_xw_gpu.py).  Each tile's projection of a block of 16 / BC steps is one
@@ -494,7 +497,9 @@ class SepTrainer:
         for l in range(net.L - 1, -1, -1):
             dGb = self.dGb_l[l]
             dGhb = self.dGhb_l[l] if gru else dGb
-            _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED | (DGH_PAD8 if gru else 0), B, T, H, _lib.ptr(dH),
+            _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED | (DEFER_BIAS if self.defer_bias else 0) |
+                      (DGH_PAD8 if gru else 0), B, T, H,
+                      _lib.ptr(dH),
                       _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), None, None,
@@ -514,8 +519,21 @@ class SepTrainer:
                                  strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT, ws=self.gl_ws)
             if l > 0:
                 dH = dH_next
+        if self.defer_bias:
+            self._bias_reduce()
         if grouped:
             dwg.run()
+
+    def _bias_reduce(self):
+        """Every layer's BPTT bias partials (DL4SS_RNN_DEFER_BIAS) into db_ih / db_hh, one launch."""
+        net, g = self.net, self.net.grad
+        if not hasattr(self, "_bias_args"):
+            n = net.L
+            P = ctypes.c_void_p
+            self._bias_args = (n, (P * n)(*[self._ws_slot(l, True).data_ptr() for l in range(n)]),
+                               (P * n)(*[net.cat_view("bias_ih", l, g).data_ptr() for l in range(n)]),
+                               (P * n)(*[net.cat_view("bias_hh", l, g).data_ptr() for l in range(n)]))
+        _lib.call("dl4ss_birnn_bias_reduce", CELLS[net.cell], self.B, net.H, *self._bias_args, _lib.stream_ptr())
 
     def backward(self):
         net, B, T, H = self.net, self.B, self.T, self.net.H

@@ -146,6 +146,13 @@ enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
  * direction's columns start 16-B aligned (the GRU's 900 gate rows -> 904), so both directions'
  * dW_hh run as one LDS-DMA batched GEMM (gemm_gl).  The unpadded default is (B, T, 2, NGATE*H). */
 #define DL4SS_RNN_DGH_PAD8 0x200
+/* precision flag of dl4ss_birnn_bwd_ex (bf16 BPTT with fused bias gradients): leave the per-row
+ * bias partials in the workspace; dl4ss_birnn_bias_reduce adds those of n launches (n <= 8, their
+ * workspaces and bias gradient pointers as host arrays) into db_ih / db_hh in ONE launch, in the
+ * same fixed row order (bitwise the per-launch reduce). */
+#define DL4SS_RNN_DEFER_BIAS 0x400
+int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
+                            float* const* db_hh, void* stream);
 long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
 /* The persistent recurrence's plan under a co-residency budget: every workgroup of a launch
  * (2 directions x nchunk batch chunks x NG units groups) must be resident at once, so the
