@@ -562,6 +562,16 @@ constexpr int SXB = SXC * 8;
 // (slot stride XBUF + 16 BC bf16: the 16 columns' rows on distinct bank quads,
 // tools/lds_banks.py), DMA'd two blocks ahead of use.
 __host__ __device__ constexpr int xw_spb(int bc) { return 16 / bc; }
+// Packed forward's per-step input projections, one slab per step slot: [cell = b * J + u][4 gates],
+// read by each cell lane as ONE float4; slab stride BC * 128 + 4 floats (= 4 mod 8).  The fused
+// projection's block epilogue (xfinal) stores one gate of 16 (step, batch row) columns per
+// instruction: with [b * 32 + u][4] records in 512-float slabs all 16 hit ONE bank (a 16-way
+// conflict, ~150 conflict cycles per step and workgroup, SQ_LDS_BANK_CONFLICT / IDX_ACTIVE of the
+// fused kernels 0.32 / 0.35); dense rows and the odd quad in the slab stride spread them over 8
+// banks (tools/lds_banks.py: 600 -> 104 conflict cycles per block).  A gate-major layout (one
+// 16-B epilogue store per lane, conflict-free) measured slower: the cell lanes' 4 scalar reads
+// instead of one float4 cost the 600-wide layers 9-17 us per launch (round 4)
+__host__ __device__ constexpr int sin_slab(int bc) { return bc * 32 * 4 + 4; }
 __host__ __device__ constexpr int xw_nxq(int bc) { return (bc * SXC + 127) / 128; }
 __host__ __device__ constexpr int xw_slot(int bc) { return xw_nxq(bc) * 128 * 8 + 16 * bc; }  // bf16
 __host__ __device__ constexpr int xw_ring_bf16(int bc) { return 3 * xw_spb(bc) * xw_slot(bc); }
@@ -655,11 +665,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   unsigned short* shb = reinterpret_cast<unsigned short*>(smem);
   float* sgate = smem + 8 * SHB;                                                        // [BC][SGS]
   float* sgx = sgate + BC * SGS;  // tile 4's odd-k-step chain (wave 7) [BC][16]; the even one is in sgate
-  // per-step input projections [NSIN][BC*32][4]: double buffered, or with XW two blocks of SPB steps
+  // per-step input projections [NSIN][sin_slab]: double buffered, or with XW two blocks of SPB steps
   constexpr int SPB = xw_spb(BC);
   constexpr int NSIN = XW ? 2 * SPB : 2;
+  constexpr int SINS = sin_slab(BC);
   float* sin = sgx + BC * 16;
-  unsigned short* spub = reinterpret_cast<unsigned short*>(sin + NSIN * BC * 32 * 4);   // [BC][PKU]
+  unsigned short* spub = reinterpret_cast<unsigned short*>(sin + NSIN * SINS);   // [BC][PKU]
   // XW: the ring of 3 * SPB step slots of the layer-input rows ([BC][SXB] bf16 + the pad items of
   // the last DMA piece), 256-B aligned (the bank order of its rows)
   static_assert(!XW || FWD_NPW == 2, "the fused projection's DMA pieces assume two prefetch waves of 64 lanes");
@@ -778,7 +789,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     ld.p[q] = (on && ib < a.B && ij < H) ? a.G + ((long long)ib * T * 2 + d) * GH + gate * H + ij : nullptr;
     ld.stride[q] = 2 * GH;
     ld.shift[q] = 0;
-    ld.dst[q] = on ? ((cell / J) * 32 + iu) * 4 + gate : -1;
+    ld.dst[q] = on ? cell * 4 + gate : -1;
   }
   // XW: per-lane sources of this prefetch wave's DMA pieces (item i = q*128 + (wave-5)*64 + lane)
   const unsigned short* xsrc[NXQ];
@@ -858,14 +869,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   auto xfinal = [&](auto ntl, int kb) {
     constexpr int NTL = decltype(ntl)::value;
     const int n = lane & 15, o = n / BC, b = n % BC;
-    float* dst = sin + ((kb & 1) * SPB + o) * BC * 32 * 4;
+    float* dst = sin + ((kb & 1) * SPB + o) * SINS;
 #pragma unroll
     for (int i = 0; i < NTL; ++i) {
       if (xt[i] < 0) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int rr = xt[i] * 16 + 4 * (lane >> 4) + e;
-        if (rr < R) dst[(b * 32 + rr % J) * 4 + rr / J] = xacc[i][e] + bir[i][e];
+        if (rr < R) dst[(b * J + rr % J) * 4 + rr / J] = xacc[i][e] + bir[i][e];
       }
       xacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -1054,7 +1065,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       if (XW) xstart(ntl);
       for (int s = 0; s < T; ++s) {
         if (!XW) {
-          ld.commit(sin + (s & 1) * BC * 32 * 4);
+          ld.commit(sin + (s & 1) * SINS);
           if (s + 1 < T) ld.issue(d == 0 ? s + 1 : T - 2 - s, T);
         }
         STAMP(0)
@@ -1098,7 +1109,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       if (cval) {
         float hg[NGATE], gx[NGATE];
         const int sb = XW ? ((s / SPB) & 1) * SPB + s % SPB : (s & 1);
-        const float4 g4 = *reinterpret_cast<const float4*>(sin + sb * BC * 32 * 4 + tid * 4);  // one 16-B read
+        const float4 g4 = *reinterpret_cast<const float4*>(sin + sb * SINS + (cb * J + cu) * 4);  // one 16-B read
         const float gxa[4] = {g4.x, g4.y, g4.z, g4.w};
         // tile 4 (rows 64..79: with J = 20 only gate 3's units 4..19): even chain + odd chain, as the
         // whole-tile matvec's acc[0] + acc[1]; read unconditionally (a clamped address) and selected
@@ -1520,12 +1531,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 //        5-7 per-step operand prefetch.
 // --------------------------------------------------------------------------
 // BPTT per-step operand loads (prefetch waves): issued after B1, in the cell phase, not beside the
-// polling sweeps in the CU's memory queue (BWD_PF_LATE), as slot-major items (BWD_PF_SLOTMAJOR)
+// polling sweeps in the CU's memory queue (BWD_PF_LATE)
 #ifndef BWD_PF_LATE
 #define BWD_PF_LATE 1
-#endif
-#ifndef BWD_PF_SLOTMAJOR
-#define BWD_PF_SLOTMAJOR 1
 #endif
 // the cell lanes' dG / dGh stores of step s-1 issued after B1 of step s (before the cell update)
 // instead of right after the publish: measured slower, 7994 vs 8085 mixtures/s
@@ -1569,9 +1577,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   unsigned short* sdgb = reinterpret_cast<unsigned short*>(smem);  // [16][SDG] bf16 dgh B image
   float* sdh = smem + 8 * SDG;                                      // [16][BC][J] gathered partials (rows >= NG stay 0)
   float* wsc = sdh + ((16 * BC * J + 3) & ~3);                      // [4 waves][BC][WSP]
-  // per-step operands, [2 steps][2 planes][BC*32][4] with the planes 16 words apart in bank
-  // order: the prefetch commit (a cell's 8 operands on 8 consecutive lanes) and the cell's two
-  // 16-B reads are both conflict-free (a [cell][8] record was an 8-way commit conflict)
+  // per-step operands, [2 steps][2 planes][cell = b * J + u][4] (slots 0-3 in plane 0, 4-7 in
+  // plane 1): the cell lanes read their two 16-B quads conflict-free (16 lanes on 16 consecutive
+  // cells), and so is the prefetch commit (below)
   constexpr int SOPP = BC * 32 * 4 + 16;
   float* sop = wsc + 4 * BC * WSP;
   for (int i = tid; i < 8 * SDG + 16 * BC * J; i += NT) smem[i] = 0.0f;
@@ -1619,30 +1627,24 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   //   0 dOut, 1..4 act, 5 c (LSTM) / h_prev (GRU), 6 c_prev (LSTM), 7 unused
   constexpr int WPF = WPOLL + BWD_NPW;  // waves WPOLL .. WPF-1 poll
   constexpr int NPF = NT - WPF * 64;
-  // slot-major items (item = slot * BC*J + cell): a load instruction's lanes read consecutive
-  // units of one operand row -- a few cache lines per instruction instead of one per lane-octet;
-  // the slots in use only (LSTM 0-6, GRU 0-5: 3 instructions instead of 4).  With the issue after
-  // B1, cell-major items (8 operands of a cell on 8 lanes: conflict-free commits) held the
-  // prefetch waves ~650 cycles past the cell phase at B2 (stamps, profiles/r03_pfmap_stamps.txt);
-  // the commit's 8-way LDS conflict this order costs is off the critical path
-#if BWD_PF_SLOTMAJOR
+  // items by 64-lane blocks of 4 slots x 16 consecutive cells of one plane (slots in use only: LSTM
+  // 0-6, GRU 0-5), each 32-lane half 4 slots x 8 cells: a load instruction reads 16 consecutive units
+  // of each of 4 operand rows, and each half-wave of its commit covers the 32 banks of a ds_write_b32
+  // (4 * cell + slot % 4 over 8 cells x 4 slots).  Round 3's
+  // slot-major items (64 consecutive cells of one slot) wrote 16-B-strided words, a 4-way commit
+  // conflict (SQ_LDS_BANK_CONFLICT / IDX_ACTIVE 0.036 -> 0.157 -> 0.18); its cell-major items (a
+  // cell's 8 operands on 8 lanes) were conflict-free but touched one cache line per lane octet and
+  // held the prefetch waves ~650 cycles past the cell phase (profiles/r03_pfmap_stamps.txt)
   constexpr int NSL = CELL == CELL_LSTM ? 7 : 6;
-  constexpr int NQ = (BC * 20 * NSL + NPF - 1) / NPF;
-  const int ncell = BC * J;
-#else
-  constexpr int NQ = (BC * 20 * 8 + NPF - 1) / NPF;
-#endif
+  constexpr int NQ = (2 * ((BC * 20 + 15) / 16) * 64 + NPF - 1) / NPF;
+  const int ncell = BC * J, ncb = (ncell + 15) / 16;
   StepLoader<NQ> ld;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int i = tid - WPF * 64 + q * NPF;
-#if BWD_PF_SLOTMAJOR
-    const int slot = i / ncell, cell = i % ncell;
-    const bool on = wv >= WPF && i >= 0 && slot < NSL;
-#else
-    const int slot = i & 7, cell = i >> 3;
-    const bool on = wv >= WPF && cell < BC * J;
-#endif
+    const int pl = i / (ncb * 64), rem = i - pl * ncb * 64;
+    const int slot = 4 * pl + ((rem >> 3) & 3), cell = (rem >> 6) * 16 + ((rem >> 5) & 1) * 8 + (rem & 7);
+    const bool on = wv >= WPF && i >= 0 && pl < 2 && slot < NSL && cell < ncell;
     const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
     const bool valid = on && ib < a.B && ij < H;
     const float* p = nullptr;
@@ -1663,7 +1665,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.p[q] = p;
     ld.stride[q] = stride;
     ld.shift[q] = shift;
-    ld.dst[q] = on ? (slot >> 2) * SOPP + ((cell / J) * 32 + iu) * 4 + (slot & 3) : -1;
+    ld.dst[q] = on ? pl * SOPP + cell * 4 + (slot & 3) : -1;
   }
   if (wv >= WPF) ld.issue(d == 0 ? T - 1 : 0, T);
   __syncthreads();
@@ -1817,11 +1819,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 #pragma unroll
       for (int q = 0; q < NGATE; ++q) dgi[q] = dgh[q] = 0.0f;
       if (cval) {
-        // two 16-B reads per lane: the 8-float operand record read as scalars is an 8-way
-        // bank conflict (lanes 32 B apart); issued first, with the 16 partial reads behind
-        // them in the same LDS round trip (sdh is zero before the first gather)
-        const float4 o0 = *reinterpret_cast<const float4*>(sop + (s & 1) * 2 * SOPP + tid * 4);
-        const float4 o1 = *reinterpret_cast<const float4*>(sop + (s & 1) * 2 * SOPP + SOPP + tid * 4);
+        // two 16-B reads per lane (the record's two planes), issued first, with the slot
+        // partial reads behind them in the same LDS round trip (sdh is zero before the first gather)
+        const int rec = (s & 1) * 2 * SOPP + (cb * J + cu) * 4;
+        const float4 o0 = *reinterpret_cast<const float4*>(sop + rec);
+        const float4 o1 = *reinterpret_cast<const float4*>(sop + rec + SOPP);
         const float dh_rec = sum_slots<BSL_N>(sdh + cb * J + cu, BC * J);
         const float dout = o0.x + doutb;
         const float act[4] = {o0.y, o0.z, o0.w, o1.x};
@@ -2068,7 +2070,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) 
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
     p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((16 * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16 + 4) +
                                                     2 * 2 * (BC * 32 * 4 + 16));
-    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + BC * 16 + 2 * BC * 32 * 4) + 2 * BC * PKU;
+    p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + BC * 16 + 2 * sin_slab(BC)) + 2 * BC * PKU;
     return true;
   }
   return false;
@@ -2361,7 +2363,7 @@ DL4SS_API int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf
   const int grid = (int)(groups * p.NG);
   // + the per-step projections of two blocks instead of two steps, + 256: the ring starts at the
   // next 256-B boundary of the LDS address (bank order of its rows)
-  const size_t smem = p.smem_fwd_pk + sizeof(float) * (2 * xw_spb(p.BC) - 2) * p.BC * 32 * 4 + 256 +
+  const size_t smem = p.smem_fwd_pk + sizeof(float) * (2 * xw_spb(p.BC) - 2) * sin_slab(p.BC) + 256 +
                       (size_t)xw_ring_bf16(p.BC) * sizeof(unsigned short);
   return cell == CELL_LSTM ? dispatch<CELL_LSTM>(true, true, true, p.BC, a, grid, smem, st)
                            : dispatch<CELL_GRU>(true, true, true, p.BC, a, grid, smem, st);

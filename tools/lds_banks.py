@@ -8,7 +8,7 @@ For every access of a step: LDS-array cycles, the conflict-free minimum, and the
 same index formulas as the kernel, with the padding / swizzle knobs the kernel uses, so a
 layout change can be checked here before it goes to the GPU.
 
-  python tools/lds_banks.py [--old]      # --old: the round-2 layouts
+  python tools/lds_banks.py [--old]      # --old: the round-2 layouts (default: the shipped ones)
 """
 import argparse
 
@@ -95,7 +95,10 @@ def fwd_accesses(cell, old, XW=False, BC=4, J=20, NG=15, H=300):
         acc.append((f"F3 sgate store tile {tile}", "ds_write_b128", addr, 1))
     # F4 cell phase: sin float4 (waves 0-1), sgate scalar reads
     for w in range(BC * 32 // 64):
-        addr = [sin + 16 * (w * 64 + l) for l in range(64)]
+        if old:
+            addr = [sin + 16 * (w * 64 + l) for l in range(64)]
+        else:  # round 4: dense records, cell = b * J + u
+            addr = [sin + 16 * (((w * 64 + l) >> 5) * J + (l & 31)) if (l & 31) < J else None for l in range(64)]
         acc.append((f"F4 sin read wave {w}", "ds_read_b128", addr, 1))
         for q in range(ngate):
             addr = []
@@ -120,13 +123,13 @@ def fwd_accesses(cell, old, XW=False, BC=4, J=20, NG=15, H=300):
                     if gate >= ngate or c >= BC * J:
                         addr.append(None)
                         continue
-                    dst = ((c // J) * 32 + c % J) * 4 + gate
+                    dst = ((c // J) * 32 + c % J) * 4 + gate if old else c * 4 + gate
                     addr.append(sin + 4 * dst)
                 acc.append((f"F6 prefetch commit wave {wv} q={q}", "ds_write_b32", addr, 1))
     return acc
 
 
-def xw_accesses(old, BC=4, XK=20):
+def xw_accesses(old, BC=4, XK=20, J=20, R=80, xfinal_layout="r4"):
     SXB = 640 if old else 656  # bf16 row stride of the DMA'd input rows (new: 82 16-B chunks)
     NXQ = (BC * (SXB // 8) + 127) // 128
     sxb = 0
@@ -140,6 +143,24 @@ def xw_accesses(old, BC=4, XK=20):
             base = (sxb + 2 * row * SXB) if row < BC else sxz
             addr.append(base + 2 * (8 * (l >> 4) + ks * 32))
         acc.append((f"XW B read ks={ks}", "ds_read_b128", addr, 5))
+    # xfinal: the block epilogue writes G of SPB = 16 / BC steps once per block (x 1 / SPB per step):
+    # lane (o = n / BC, b = n % BC, h = lane >> 4) stores element e of rows t * 16 + 4 h + e into step
+    # slot o.  "r3": [b * 32 + u][4] records in 512-float slabs (16 lanes on one bank); "r4": dense
+    # records (cell = b * J + u), slab stride BC * 128 + 4
+    spb = 16 // BC
+    for t in range((R + 15) // 16):
+        for e in range(4):
+            addr = []
+            for l in range(64):
+                n, h = l & 15, l >> 4
+                o, b, rr = n // BC, n % BC, t * 16 + 4 * h + e
+                if rr >= R:
+                    addr.append(None)
+                elif xfinal_layout == "r3":
+                    addr.append(4 * (o * BC * 128 + (b * 32 + rr % J) * 4 + rr // J))
+                else:
+                    addr.append(4 * (o * (BC * 128 + 4) + (b * J + rr % J) * 4 + rr // J))
+            acc.append((f"XW xfinal store tile {t} e={e} (per block)", "ds_write_b32", addr, 1 / spb))
     return acc
 
 
@@ -149,6 +170,7 @@ def bwd_accesses(cell, old, BC=4, J=20, NG=15, H=300):
     SDG = KSRMAX * 32 + 8  # bf16
     WSPAN = 80
     wsp = WSPAN if old else WSPAN + 4
+    BSL_N = 6  # round 4: slot partials summed by the polling lanes (BSL_Q = 5 BC lanes per slot)
     sdgb = 0
     sdh = 2 * 8 * SDG
     wsc = sdh + 4 * ((16 * BC * J + 3) & ~3)
@@ -159,10 +181,13 @@ def bwd_accesses(cell, old, BC=4, J=20, NG=15, H=300):
         for half in range(2):
             if old:
                 addr = [sop + 4 * ((w * 64 + l) * 8 + 4 * half) for l in range(64)]
-            else:
-                addr = [sop + 4 * (half * (BC * 32 * 4 + 16) + (w * 64 + l) * 4) for l in range(64)]
+            else:  # round 4: dense cell index b * J + u
+                addr = []
+                for l in range(64):
+                    cb, cu = (w * 64 + l) >> 5, l & 31
+                    addr.append(sop + 4 * (half * (BC * 32 * 4 + 16) + (cb * J + cu) * 4) if cu < J else None)
             acc.append((f"B2 operand read {half} wave {w}", "ds_read_b128", addr, 1))
-        for i in range(16):
+        for i in range(16 if old else BSL_N):
             addr = []
             for l in range(64):
                 tid = w * 64 + l
@@ -200,7 +225,7 @@ def bwd_accesses(cell, old, BC=4, J=20, NG=15, H=300):
     JQ = J // 4
     n16 = NG * BC * JQ
     GLK = (80 * BC + 64 * 2 - 1) // (64 * 2)
-    for pw in range(2):
+    for pw in range(2 if old else 0):
         for g in range(GLK):
             addr = []
             for l in range(64):
@@ -211,21 +236,38 @@ def bwd_accesses(cell, old, BC=4, J=20, NG=15, H=300):
                 pb, qd = idx // JQ, idx % JQ
                 addr.append(sdh + 4 * (pb * J + 4 * qd))
             acc.append((f"B1 partial store wave {4 + pw} sweep {g}", "ds_write_b128", addr, 1))
+    if not old:  # round 4: one 16-B store per (slot, b, quad) lane, BSL_G = 3 slot groups per wave
+        for pw in range(2):
+            addr = []
+            for l in range(64):
+                gi, bq = l // (5 * BC), l % (5 * BC)
+                b, qd, sl = bq // 5, bq % 5, pw * 3 + gi
+                ok = gi < 3 and sl < BSL_N and qd < J // 4 and b < BC
+                addr.append(sdh + 4 * ((sl * BC + b) * J + 4 * qd) if ok else None)
+            acc.append((f"B1 slot partial store wave {4 + pw}", "ds_write_b128", addr, 1))
     # B8 prefetch commit into sop (waves 6-7), 8 slots
     NPF = 128
-    NQ = (BC * 20 * 8 + NPF - 1) // NPF
+    nsl = 7 if cell == "lstm" else 6
+    ncell, ncb = BC * J, (BC * J + 15) // 16
+    NQ = (BC * 20 * 8 + NPF - 1) // NPF if old else (2 * ncb * 64 + NPF - 1) // NPF
     for wv in (6, 7):
         for q in range(NQ):
             addr = []
             for l in range(64):
                 i = (wv - 6) * 64 + l + q * NPF
-                slot, c = (i // (BC * J), i % (BC * J)) if old else (i & 7, i >> 3)
-                if slot >= 8 or c >= BC * J:
-                    addr.append(None)
-                    continue
-                cellidx = (c // J) * 32 + c % J
-                # new: two planes [2][cell][4], the second 16 dwords off the first's banks
-                dst = cellidx * 8 + slot if old else (slot >> 2) * (BC * 32 * 4 + 16) + cellidx * 4 + (slot & 3)
+                if old:
+                    slot, c = i // (BC * J), i % (BC * J)
+                    if slot >= 8 or c >= BC * J:
+                        addr.append(None)
+                        continue
+                    dst = ((c // J) * 32 + c % J) * 8 + slot
+                else:  # round 4: 64-lane blocks of 4 slots x 16 cells of one plane, halves 4 x 8
+                    pl, rem = i // (ncb * 64), i % (ncb * 64)
+                    slot, c = 4 * pl + ((rem >> 3) & 3), (rem >> 6) * 16 + ((rem >> 5) & 1) * 8 + (rem & 7)
+                    if pl >= 2 or slot >= nsl or c >= ncell:
+                        addr.append(None)
+                        continue
+                    dst = pl * (BC * 32 * 4 + 16) + c * 4 + (slot & 3)
                 addr.append(sop + 4 * dst)
             acc.append((f"B8 prefetch commit wave {wv} q={q}", "ds_write_b32", addr, 1))
     return acc
@@ -238,8 +280,8 @@ def report(name, acc, verbose):
         tot += c * mult
         extra += (c - m) * mult
         if verbose and c > m:
-            print(f"  {what:48s} {ins:14s} x{mult}: {c} cycles (min {m})")
-    print(f"{name}: {tot} LDS-array cycles per step per workgroup, {extra} conflict cycles "
+            print(f"  {what:48s} {ins:14s} x{mult:g}: {c} cycles (min {m})")
+    print(f"{name}: {tot:g} LDS-array cycles per step per workgroup, {extra:g} conflict cycles "
           f"({extra / max(tot, 1):.2f})")
     return tot, extra
 
@@ -254,6 +296,8 @@ def main():
     report("fwd LSTM + fused projection (XK=20 B reads)", fwd_accesses("lstm", a.old, XW=True) + xw_accesses(a.old), v)
     report("fwd LSTM + fused projection (XK=5 B reads)", fwd_accesses("lstm", a.old, XW=True) + xw_accesses(a.old, XK=5),
            v)
+    report("fwd LSTM + fused projection, round-3 xfinal layout",
+           fwd_accesses("lstm", a.old, XW=True) + xw_accesses(a.old, xfinal_layout="r3"), v)
     report("bwd LSTM", bwd_accesses("lstm", a.old), v)
     report("fwd GRU", fwd_accesses("gru", a.old), v)
     report("bwd GRU", bwd_accesses("gru", a.old), v)
