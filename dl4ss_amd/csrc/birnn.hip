@@ -1627,24 +1627,26 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   //   0 dOut, 1..4 act, 5 c (LSTM) / h_prev (GRU), 6 c_prev (LSTM), 7 unused
   constexpr int WPF = WPOLL + BWD_NPW;  // waves WPOLL .. WPF-1 poll
   constexpr int NPF = NT - WPF * 64;
-  // items by 64-lane blocks of 4 slots x 16 consecutive cells of one plane (slots in use only: LSTM
-  // 0-6, GRU 0-5), each 32-lane half 4 slots x 8 cells: a load instruction reads 16 consecutive units
-  // of each of 4 operand rows, and each half-wave of its commit covers the 32 banks of a ds_write_b32
-  // (4 * cell + slot % 4 over 8 cells x 4 slots).  Round 3's
-  // slot-major items (64 consecutive cells of one slot) wrote 16-B-strided words, a 4-way commit
-  // conflict (SQ_LDS_BANK_CONFLICT / IDX_ACTIVE 0.036 -> 0.157 -> 0.18); its cell-major items (a
-  // cell's 8 operands on 8 lanes) were conflict-free but touched one cache line per lane octet and
-  // held the prefetch waves ~650 cycles past the cell phase (profiles/r03_pfmap_stamps.txt)
+  // (round 3 committed the raw operands straight into the cell lanes' record, slot-major: 16-B
+  // strided words, a 4-way conflict -- SQ_LDS_BANK_CONFLICT / IDX_ACTIVE 0.036 -> 0.157; cell-major
+  // items were conflict-free but touched one cache line per lane octet and held the prefetch waves
+  // ~650 cycles past the cell phase, profiles/r03_pfmap_stamps.txt)
   constexpr int NSL = CELL == CELL_LSTM ? 7 : 6;
-  constexpr int NQ = (2 * ((BC * 20 + 15) / 16) * 64 + NPF - 1) / NPF;
-  const int ncell = BC * J, ncb = (ncell + 15) / 16;
+  // each prefetch wave owns half of the cells (cpw of them) and stages their raw operands
+  // slot-major in a wave-private LDS block [NSL][CPWP] (a load instruction's lanes read consecutive
+  // units of one operand row; consecutive lanes commit consecutive words), then one lane per cell
+  // turns them into the cell's step factors (pf_factors)
+  static_assert(NPF == 128, "two prefetch waves");
+  constexpr int CPWP = (BC * 20 + 1) / 2;  // raw staging pitch: cells per prefetch wave at J <= 20
+  constexpr int NQ = (NSL * CPWP + 63) / 64;
+  const int ncell = BC * J, cpw = (ncell + 1) / 2, pwi = wv - WPF;
+  float* sraw = sop + 2 * 2 * SOPP + (wv >= WPF ? pwi : 0) * NSL * CPWP;
   StepLoader<NQ> ld;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int i = tid - WPF * 64 + q * NPF;
-    const int pl = i / (ncb * 64), rem = i - pl * ncb * 64;
-    const int slot = 4 * pl + ((rem >> 3) & 3), cell = (rem >> 6) * 16 + ((rem >> 5) & 1) * 8 + (rem & 7);
-    const bool on = wv >= WPF && i >= 0 && pl < 2 && slot < NSL && cell < ncell;
+    const int i = lane + 64 * q;
+    const int slot = i / cpw, c = i - slot * cpw, cell = pwi * cpw + c;
+    const bool on = wv >= WPF && slot < NSL && cell < ncell;
     const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
     const bool valid = on && ib < a.B && ij < H;
     const float* p = nullptr;
@@ -1665,7 +1667,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.p[q] = p;
     ld.stride[q] = stride;
     ld.shift[q] = shift;
-    ld.dst[q] = on ? pl * SOPP + cell * 4 + (slot & 3) : -1;
+    ld.dst[q] = on ? slot * CPWP + c : -1;
   }
   if (wv >= WPF) ld.issue(d == 0 ? T - 1 : 0, T);
   __syncthreads();
@@ -1760,8 +1762,39 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     return;
   }
   if (wv >= WPF) {
+    // the step factors of this wave's cells: everything of the cell backward that does not depend
+    // on the gathered dh, off the cell lanes' B1 -> B2 path (LSTM: tanh(c) and the gate
+    // derivatives; GRU: the z / n / r products), into the record the cell lanes read after B1:
+    //   LSTM {dOut, o (1 - tanh^2 c), g i (1 - i), c_prev f (1 - f)} {i (1 - g^2), tanh(c) o (1 - o), f, -}
+    //   GRU  {dOut, (1-z)(1-n^2) hn r (1-r), (h_prev - n) z (1-z), (1-z)(1-n^2)} {(1-z)(1-n^2) r, z, -, -}
+    auto pf_factors = [&](int s) {
+      ld.commit(sraw);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      const int cell = pwi * cpw + lane;
+      if (lane < cpw && cell < ncell) {
+        float v[NSL];
+#pragma unroll
+        for (int k = 0; k < NSL; ++k) v[k] = sraw[k * CPWP + lane];
+        float4 p0, p1;
+        if constexpr (CELL == CELL_LSTM) {
+          const float ig = v[1], fg = v[2], gg = v[3], og = v[4];
+          const float tc = ftanh(v[5]);
+          p0 = make_float4(v[0], og * (1.0f - tc * tc), gg * ig * (1.0f - ig), v[6] * fg * (1.0f - fg));
+          p1 = make_float4(ig * (1.0f - gg * gg), tc * og * (1.0f - og), fg, 0.0f);
+        } else {
+          const float rg = v[1], zg = v[2], ng = v[3], hn = v[4];
+          const float gn = (1.0f - zg) * (1.0f - ng * ng);
+          p0 = make_float4(v[0], gn * hn * rg * (1.0f - rg), (v[5] - ng) * zg * (1.0f - zg), gn);
+          p1 = make_float4(gn * rg, zg, 0.0f, 0.0f);
+        }
+        float* rec = sop + (s & 1) * 2 * SOPP + cell * 4;
+        *reinterpret_cast<float4*>(rec) = p0;
+        *reinterpret_cast<float4*>(rec + SOPP) = p1;
+      }
+    };
     for (int s = 0; s < T; ++s) {
-      ld.commit(sop + (s & 1) * 2 * SOPP);
+      pf_factors(s);
 #if BWD_PF_LATE
       // the next step's operand loads go out after B1, in the cell phase: not in the CU's memory
       // queue beside the polling sweeps (MI355X_MICROARCH.md handoff-1to1: the hand-off price sits
@@ -1826,34 +1859,25 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         const float4 o1 = *reinterpret_cast<const float4*>(sop + rec + SOPP);
         const float dh_rec = sum_slots<BSL_N>(sdh + cb * J + cu, BC * J);
         const float dout = o0.x + doutb;
-        const float act[4] = {o0.y, o0.z, o0.w, o1.x};
-        const float c = o1.y, cprev = o1.z, hprev = o1.y;
         const float dh = dout + dh_rec + dh_dir;
         STAMP(7)
         if constexpr (CELL == CELL_LSTM) {
-          const float ig = act[0], fg = act[1], gg = act[2], og = act[3];
-          const float tc = ftanh(c);
-          const float dc = dc_next + dh * og * (1.0f - tc * tc);
-          dgi[0] = dc * gg * ig * (1.0f - ig);
-          dgi[1] = dc * cprev * fg * (1.0f - fg);
-          dgi[2] = dc * ig * (1.0f - gg * gg);
-          dgi[3] = dh * tc * og * (1.0f - og);
-          dc_next = dc * fg;
+          const float dc = dc_next + dh * o0.y;
+          dgi[0] = dc * o0.z;
+          dgi[1] = dc * o0.w;
+          dgi[2] = dc * o1.x;
+          dgi[3] = dh * o1.y;
+          dc_next = dc * o1.z;
 #pragma unroll
           for (int q = 0; q < NGATE; ++q) dgh[q] = dgi[q];
         } else {
-          const float rg = act[0], zg = act[1], ng = act[2], hn = act[3];
-          const float dn = dh * (1.0f - zg);
-          const float dz = dh * (hprev - ng);
-          dh_dir = dh * zg;
-          const float dnp = dn * (1.0f - ng * ng);
-          const float dr = dnp * hn;
-          dgi[0] = dr * rg * (1.0f - rg);
-          dgi[1] = dz * zg * (1.0f - zg);
-          dgi[2] = dnp;
+          dgi[0] = dh * o0.y;
+          dgi[1] = dh * o0.z;
+          dgi[2] = dh * o0.w;
           dgh[0] = dgi[0];
           dgh[1] = dgi[1];
-          dgh[2] = dnp * rg;
+          dgh[2] = dh * o1.x;
+          dh_dir = dh * o1.y;
         }
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
@@ -2069,7 +2093,7 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) 
     p.fwd_pk = !p.big && J % 2 == 0 && H % 2 == 0 && J <= PKU && NG <= 16 && (R + 15) / 16 <= (FWD_NPW == 3 ? 5 : FWD_NPW == 2 ? 6 : 7);
     p.bwd_pk = !p.big && J % 4 == 0 && H % 4 == 0 && NG <= 16;
     p.smem_bwd_pk = 2 * 16 * SDG + sizeof(float) * (((16 * BC * J + 3) & ~3) + 4 * BC * ((HMAX / 16 + 3) / 4 * 16 + 4) +
-                                                    2 * 2 * (BC * 32 * 4 + 16));
+                                                    2 * 2 * (BC * 32 * 4 + 16) + 2 * 7 * ((BC * 20 + 1) / 2));
     p.smem_fwd_pk = 2 * 16 * SHB + sizeof(float) * (BC * (MT * 16 + 4) + BC * 16 + 2 * sin_slab(BC)) + 2 * BC * PKU;
     return true;
   }

@@ -245,31 +245,38 @@ def bwd_accesses(cell, old, BC=4, J=20, NG=15, H=300):
                 ok = gi < 3 and sl < BSL_N and qd < J // 4 and b < BC
                 addr.append(sdh + 4 * ((sl * BC + b) * J + 4 * qd) if ok else None)
             acc.append((f"B1 slot partial store wave {4 + pw}", "ds_write_b128", addr, 1))
-    # B8 prefetch commit into sop (waves 6-7), 8 slots
+    # B8 prefetch commit (waves 6-7): round 2 / 3 straight into the record; round 4 into a
+    # wave-private slot-major staging block, then one lane per cell writes its factor record (2 x 16 B)
     NPF = 128
     nsl = 7 if cell == "lstm" else 6
-    ncell, ncb = BC * J, (BC * J + 15) // 16
-    NQ = (BC * 20 * 8 + NPF - 1) // NPF if old else (2 * ncb * 64 + NPF - 1) // NPF
+    ncell = BC * J
+    cpw, cpwp = (ncell + 1) // 2, (BC * 20 + 1) // 2
+    NQ = (BC * 20 * 8 + NPF - 1) // NPF if old else (nsl * cpwp + 63) // 64
     for wv in (6, 7):
         for q in range(NQ):
             addr = []
             for l in range(64):
-                i = (wv - 6) * 64 + l + q * NPF
                 if old:
+                    i = (wv - 6) * 64 + l + q * NPF
                     slot, c = i // (BC * J), i % (BC * J)
-                    if slot >= 8 or c >= BC * J:
-                        addr.append(None)
-                        continue
+                    ok = slot < 8 and c < BC * J
                     dst = ((c // J) * 32 + c % J) * 8 + slot
-                else:  # round 4: 64-lane blocks of 4 slots x 16 cells of one plane, halves 4 x 8
-                    pl, rem = i // (ncb * 64), i % (ncb * 64)
-                    slot, c = 4 * pl + ((rem >> 3) & 3), (rem >> 6) * 16 + ((rem >> 5) & 1) * 8 + (rem & 7)
-                    if pl >= 2 or slot >= nsl or c >= ncell:
-                        addr.append(None)
-                        continue
-                    dst = pl * (BC * 32 * 4 + 16) + c * 4 + (slot & 3)
-                addr.append(sop + 4 * dst)
+                else:
+                    i = l + 64 * q
+                    slot, c = i // cpw, i % cpw
+                    ok = slot < nsl and (wv - 6) * cpw + c < ncell
+                    dst = 2 * 2 * (BC * 32 * 4 + 16) + (wv - 6) * nsl * cpwp + slot * cpwp + c
+                addr.append(sop + 4 * dst if ok else None)
             acc.append((f"B8 prefetch commit wave {wv} q={q}", "ds_write_b32", addr, 1))
+        if not old:
+            for k in range(nsl):
+                addr = [sop + 4 * (2 * 2 * (BC * 32 * 4 + 16) + (wv - 6) * nsl * cpwp + k * cpwp + l)
+                        if l < cpw else None for l in range(64)]
+                acc.append((f"B9 staging read {k} wave {wv}", "ds_read_b32", addr, 1))
+            for pl in range(2):
+                addr = [sop + 4 * (pl * (BC * 32 * 4 + 16) + ((wv - 6) * cpw + l) * 4) if l < cpw else None
+                        for l in range(64)]
+                acc.append((f"B9 factor record store {pl} wave {wv}", "ds_write_b128", addr, 1))
     return acc
 
 
