@@ -91,7 +91,9 @@ def stft_grid_threads(n_sig, T):
 
 
 def stft_grids(B, K, T):
-    return [stft_grid_threads(B, T), stft_grid_threads(B * K, T)]
+    """The in-step magnitude STFT: ONE launch over the B mixtures + B K sources (the trainer's
+    shared signal buffer, SepTrainer._stfts)."""
+    return [stft_grid_threads(B + B * K, T)]
 
 
 def pmc_traffic(kernel, grids):
@@ -436,15 +438,13 @@ def standin_main(args, world, rank):
 
 
 def stft_instep_graph(tr, B, K, N, reps=10):
-    """The in-step STFT pair (mixtures, then sources; magnitude only) as the step runs it: both
-    launches captured `reps` times into one HIP graph and replayed between two events on the
-    stream the graph runs on, so the per-pair time is kernel time plus in-graph gaps, not the
-    host launch path of eager re-launches."""
-    from dl4ss_amd import ops
+    """The in-step STFT (mixtures and sources, magnitude only: one launch over the trainer's
+    shared signal buffer) as the step runs it: captured `reps` times into one HIP graph and
+    replayed between two events on the stream the graph runs on, so the per-step time is kernel
+    time plus in-graph gaps, not the host launch path of eager re-launches."""
 
     def pair():
-        ops.stft(tr.mix, complex_out=False, mag_out=True, out_mag=tr.mag_mix)
-        ops.stft(tr.src.view(B * K, N), complex_out=False, mag_out=True, out_mag=tr.mag_src.view(B * K, tr.T, tr.F))
+        tr._stfts()
 
     pair()
     torch.cuda.synchronize()
@@ -632,7 +632,7 @@ def train_main(args, cfg, dev, world, rank, pg):
         out.update({
             "loss": loss_v,
             "roofline": sa,
-            "roofline_instep": {"bound": "hbm", "kernel": f"stft_fwd in-step (2 launches/step: {B} mixtures + "
+            "roofline_instep": {"bound": "hbm", "kernel": f"stft_fwd in-step (1 launch/step: {B} mixtures + "
                                                          f"{B * K} sources, magnitude; timed as a replayed graph)",
                                 "achieved": stft_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": stft_gbs / HBM_PEAK_GBS,

@@ -134,16 +134,21 @@ class SepTrainer:
         NGH = _ngate(net.cell) * H
         BT = B * T
         f32 = dict(device=dev, dtype=torch.float32)
-        self.src = torch.empty(B, K, N, **f32)
-        self.mix = torch.empty(B, N, **f32)
+        # mixtures and scaled sources in ONE signal buffer [B + B K, N] (magnitude modes: one STFT
+        # launch over both, their magnitudes likewise adjacent)
+        self._sig = torch.empty(B + B * K, N, **f32)
+        self.mix = self._sig[:B]
+        self.src = self._sig[B:].view(B, K, N)
         self.stats = torch.empty(32 * B * K, **f32)  # mixing partials (dl4ss_mix_sources)
-        self.mag_mix = torch.empty(B, T, F, **f32)
         if mode == "crm":
+            self.mag_mix = torch.empty(B, T, F, **f32)
             self.Xc_mix = torch.empty(B, T, F, 2, **f32)
             self.Xc_src = torch.empty(B, K, T, F, 2, **f32)
         else:
             self.Xc_mix = None
-            self.mag_src = torch.empty(B, K, T, F, **f32)
+            self._mag = torch.empty(B + B * K, T, F, **f32)
+            self.mag_mix = self._mag[:B]
+            self.mag_src = self._mag[B:].view(B, K, T, F)
         self.out = [torch.empty(B, T, 2 * H, **f32) for _ in range(net.L)]
         self.hprev = [torch.empty(B, T, 2 * H, **f32) for _ in range(net.L)]
         self.act = [torch.empty(B, T, 2, 4 * H, **f32) for _ in range(net.L)]
@@ -262,15 +267,19 @@ class SepTrainer:
     # ------------------------------------------------------------------ features
     def features(self, raw, gains):
         ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
+        self._stfts()
+
+    def _stfts(self):
+        """The step's STFTs: cRM, the mixtures' complex + magnitude and the sources' complex
+        spectra (two launches); magnitude modes, mixtures and sources in one launch over the
+        shared signal buffer."""
         B, K, N = self.B, self.K, self.N
         if self.mode == "crm":
             ops.stft(self.mix, complex_out=True, mag_out=True, out_c=self.Xc_mix, out_mag=self.mag_mix)
             ops.stft(self.src.view(B * K, N), complex_out=True, mag_out=False, out_c=self.Xc_src.view(B * K, self.T,
                                                                                                      self.F, 2))
         else:
-            ops.stft(self.mix, complex_out=False, mag_out=True, out_mag=self.mag_mix)
-            ops.stft(self.src.view(B * K, N), complex_out=False, mag_out=True,
-                     out_mag=self.mag_src.view(B * K, self.T, self.F))
+            ops.stft(self._sig, complex_out=False, mag_out=True, out_mag=self._mag)
 
     # ------------------------------------------------------------------ forward
     def _to_bf16_rows(self, x, out):
@@ -631,15 +640,7 @@ class SepTrainer:
         """The launch sequence recorded into the step graph: STFT features of the mixed
         batch, forward, loss + its gradient, backward (everything between the mixing
         kernel and the all-reduce; no host synchronisation inside)."""
-        B, K, N = self.B, self.K, self.N
-        if self.mode == "crm":
-            ops.stft(self.mix, complex_out=True, mag_out=True, out_c=self.Xc_mix, out_mag=self.mag_mix)
-            ops.stft(self.src.view(B * K, N), complex_out=True, mag_out=False,
-                     out_c=self.Xc_src.view(B * K, self.T, self.F, 2))
-        else:
-            ops.stft(self.mix, complex_out=False, mag_out=True, out_mag=self.mag_mix)
-            ops.stft(self.src.view(B * K, N), complex_out=False, mag_out=True,
-                     out_mag=self.mag_src.view(B * K, self.T, self.F))
+        self._stfts()
         self.forward()
         return self.loss_and_grad()
 
