@@ -122,3 +122,24 @@ def test_mix_sources_matches_oracle(dev):
         s, m = dsp.mix_sources(srcs, g[b])
         np.testing.assert_allclose(osrc[b], s, atol=1e-5)
         np.testing.assert_allclose(omix[b], m, atol=2e-5)
+
+
+def test_step_stft_one_launch_equals_two(dev):
+    """The trainer's magnitude-mode features: mixtures and scaled sources share one signal buffer
+    and ONE STFT launch covers both (SepTrainer._stfts); bitwise the two separate launches."""
+    from dl4ss_amd import engine
+
+    B, K, N = 4, 3, 8000
+    net = engine.SepNet(cell="gru", num_layers=2, device=dev, seed=3)
+    tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+    assert tr.mix.data_ptr() == tr._sig.data_ptr() and tr.src.data_ptr() == tr._sig[B:].data_ptr()
+    src, _, u = synth.SyntheticMixtures(n_samples=N, k=K, seed=4).batch(B)
+    raw = torch.from_numpy(src.astype(np.float32)).to(dev)
+    gains = torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev)
+    tr.features(raw, gains)
+    torch.cuda.synchronize()
+    _, m_mix = ops.stft(tr.mix.clone(), complex_out=False, mag_out=True)
+    _, m_src = ops.stft(tr.src.reshape(B * K, N).clone(), complex_out=False, mag_out=True)
+    torch.cuda.synchronize()
+    assert torch.equal(tr.mag_mix, m_mix)
+    assert torch.equal(tr.mag_src.reshape(B * K, tr.T, tr.F), m_src)
