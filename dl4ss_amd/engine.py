@@ -459,8 +459,10 @@ class SepTrainer:
         ldgh = self.ngh_p8 if gru else NGH
         # split-K factors of the grouped launch (C2 bench, 20 steps, r03_dwg: dW_lin / dW_ih / dW_hh
         # 2/4/8 -> 4.434 ms per step, 2/4/4 4.424, 2/3/6 4.420, 1/2/4 4.405, 2/2/4 4.400): fewer, longer
-        # k-ranges than the single launches wanted, and smaller slabs for the combine
-        s_lin, s_ih, s_hh = 2, 2, 4
+        # k-ranges than the single launches wanted, and smaller slabs for the combine.  Round 4 (n-fastest
+        # tiles per XCD, alternating A/B runs, profiles/r04_dw_splits.jsonl): 2/1/4 3.856 ms vs 2/2/4 3.869, 2/1/3
+        # 3.858, 1/2/4 3.855-3.860, 2/2/8 3.867-3.877, 2/2/2 3.880, 1/1/4 3.888 -- dW_ih unsplit
+        s_lin, s_ih, s_hh = (int(v) for v in os.environ.get("DL4SS_DW_SPLITS", "2,1,4").split(","))  # A/B knob
         probs = [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
                       transA=True, transB=False, beta=1.0, splitk=s_lin)]
         # longest k-ranges first (dW_lin 63 k-tiles per workgroup, dW_ih 32, dW_hh 16): the short
