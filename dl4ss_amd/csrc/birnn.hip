@@ -1636,17 +1636,33 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   // slot-major in a wave-private LDS block [NSL][CPWP] (a load instruction's lanes read consecutive
   // units of one operand row; consecutive lanes commit consecutive words), then one lane per cell
   // turns them into the cell's step factors (pf_factors)
+  // (BC >= 4 only.  At BC <= 2 the raw operands go straight into the record as slot-major items --
+  // 64 consecutive cells of one slot per load instruction, a 4-way commit conflict: there the
+  // step is short and the loads' spread decides; 4 slots x 8 cells per half-wave (conflict-free,
+  // twice the cache lines per instruction) took the BiGRU C3 BPTT from 325 to 407 us per launch)
   static_assert(NPF == 128, "two prefetch waves");
+  constexpr bool PFF = BC >= 4;
   constexpr int CPWP = (BC * 20 + 1) / 2;  // raw staging pitch: cells per prefetch wave at J <= 20
-  constexpr int NQ = (NSL * CPWP + 63) / 64;
+  constexpr int NQ = PFF ? (NSL * CPWP + 63) / 64 : (BC * 20 * NSL + NPF - 1) / NPF;
   const int ncell = BC * J, cpw = (ncell + 1) / 2, pwi = wv - WPF;
   float* sraw = sop + 2 * 2 * SOPP + (wv >= WPF ? pwi : 0) * NSL * CPWP;
   StepLoader<NQ> ld;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int i = lane + 64 * q;
-    const int slot = i / cpw, c = i - slot * cpw, cell = pwi * cpw + c;
-    const bool on = wv >= WPF && slot < NSL && cell < ncell;
+    int slot, c = 0, cell;
+    bool on;
+    if constexpr (PFF) {
+      const int i = lane + 64 * q;
+      slot = i / cpw;
+      c = i - slot * cpw;
+      cell = pwi * cpw + c;
+      on = wv >= WPF && slot < NSL && cell < ncell;
+    } else {
+      const int i = tid - WPF * 64 + q * NPF;
+      slot = i / ncell;
+      cell = i - slot * ncell;
+      on = wv >= WPF && i >= 0 && slot < NSL;
+    }
     const int ib = b0 + cell / J, iu = cell % J, ij = j0 + iu;
     const bool valid = on && ib < a.B && ij < H;
     const float* p = nullptr;
@@ -1667,7 +1683,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.p[q] = p;
     ld.stride[q] = stride;
     ld.shift[q] = shift;
-    ld.dst[q] = on ? slot * CPWP + c : -1;
+    ld.dst[q] = !on ? -1 : PFF ? slot * CPWP + c : (slot >> 2) * SOPP + cell * 4 + (slot & 3);
   }
   if (wv >= WPF) ld.issue(d == 0 ? T - 1 : 0, T);
   __syncthreads();
@@ -1794,7 +1810,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       }
     };
     for (int s = 0; s < T; ++s) {
-      pf_factors(s);
+      if constexpr (PFF)
+        pf_factors(s);
+      else
+        ld.commit(sop + (s & 1) * 2 * SOPP);
 #if BWD_PF_LATE
       // the next step's operand loads go out after B1, in the cell phase: not in the CU's memory
       // queue beside the polling sweeps (MI355X_MICROARCH.md handoff-1to1: the hand-off price sits
@@ -1861,7 +1880,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         const float dout = o0.x + doutb;
         const float dh = dout + dh_rec + dh_dir;
         STAMP(7)
-        if constexpr (CELL == CELL_LSTM) {
+        if constexpr (PFF && CELL == CELL_LSTM) {  // the record holds the step factors (pf_factors)
           const float dc = dc_next + dh * o0.y;
           dgi[0] = dc * o0.z;
           dgi[1] = dc * o0.w;
@@ -1870,7 +1889,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           dc_next = dc * o1.z;
 #pragma unroll
           for (int q = 0; q < NGATE; ++q) dgh[q] = dgi[q];
-        } else {
+        } else if constexpr (PFF) {
           dgi[0] = dh * o0.y;
           dgi[1] = dh * o0.z;
           dgi[2] = dh * o0.w;
@@ -1878,6 +1897,30 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
           dgh[1] = dgi[1];
           dgh[2] = dh * o1.x;
           dh_dir = dh * o1.y;
+        } else if constexpr (CELL == CELL_LSTM) {  // raw operands {dOut, i, f, g} {o, c, c_prev, -}
+          const float ig = o0.y, fg = o0.z, gg = o0.w, og = o1.x;
+          const float tc = ftanh(o1.y);
+          const float dc = dc_next + dh * og * (1.0f - tc * tc);
+          dgi[0] = dc * gg * ig * (1.0f - ig);
+          dgi[1] = dc * o1.z * fg * (1.0f - fg);
+          dgi[2] = dc * ig * (1.0f - gg * gg);
+          dgi[3] = dh * tc * og * (1.0f - og);
+          dc_next = dc * fg;
+#pragma unroll
+          for (int q = 0; q < NGATE; ++q) dgh[q] = dgi[q];
+        } else {  // raw operands {dOut, r, z, n} {hn, h_prev, -, -}
+          const float rg = o0.y, zg = o0.z, ng = o0.w, hn = o1.x;
+          const float dn = dh * (1.0f - zg);
+          const float dz = dh * (o1.y - ng);
+          dh_dir = dh * zg;
+          const float dnp = dn * (1.0f - ng * ng);
+          const float dr = dnp * hn;
+          dgi[0] = dr * rg * (1.0f - rg);
+          dgi[1] = dz * zg * (1.0f - zg);
+          dgi[2] = dnp;
+          dgh[0] = dgi[0];
+          dgh[1] = dgi[1];
+          dgh[2] = dnp * rg;
         }
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
