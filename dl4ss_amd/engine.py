@@ -460,9 +460,21 @@ class SepTrainer:
         # split-K factors of the grouped launch (C2 bench, 20 steps, r03_dwg: dW_lin / dW_ih / dW_hh
         # 2/4/8 -> 4.434 ms per step, 2/4/4 4.424, 2/3/6 4.420, 1/2/4 4.405, 2/2/4 4.400): fewer, longer
         # k-ranges than the single launches wanted, and smaller slabs for the combine.  Round 4 (n-fastest
-        # tiles per XCD, alternating A/B runs, profiles/r04_dw_splits.jsonl): 2/1/4 3.856 ms vs 2/2/4 3.869, 2/1/3
-        # 3.858, 1/2/4 3.855-3.860, 2/2/8 3.867-3.877, 2/2/2 3.880, 1/1/4 3.888 -- dW_ih unsplit
-        s_lin, s_ih, s_hh = (int(v) for v in os.environ.get("DL4SS_DW_SPLITS", "2,1,4").split(","))  # A/B knob
+        # tiles per XCD, alternating A/B runs, profiles/r04_dw_splits.jsonl): at C2 2/1/4 3.856 ms vs
+        # 2/2/4 3.869, 2/1/3 3.858, 1/2/4 3.855-3.860, 2/2/8 3.867-3.877, 2/2/2 3.880, 1/1/4 3.888; the
+        # 2-layer BiGRU configs want dW_ih split (C4 2.52 vs 2.59 ms, C3 2.13 vs 2.17 ms with 2/2/4).  So
+        # dW_ih goes unsplit when the group fills >= 3 waves of the 512 workgroup slots without it
+        # (C2: 1793 workgroups; the BiGRU-2L nets: 999)
+        def tiles(m, n):
+            return ((m + 127) // 128) * ((n + 127) // 128)
+
+        s_lin, s_hh = 2, 4
+        wg1 = s_lin * tiles(FE, 2 * H) + sum(tiles(NGH * 2, self.F if l == 0 else 2 * H) for l in range(net.L)) + \
+            s_hh * 2 * net.L * tiles(NGH, H)
+        s_ih = 1 if wg1 >= 3 * 512 else 2
+        if os.environ.get("DL4SS_DW_SPLITS"):  # A/B knob: "lin,ih,hh"
+            s_lin, s_ih, s_hh = (int(v) for v in os.environ["DL4SS_DW_SPLITS"].split(","))
+        self.dw_splits = (s_lin, s_ih, s_hh)
         probs = [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
                       transA=True, transB=False, beta=1.0, splitk=s_lin)]
         # longest k-ranges first (dW_lin 63 k-tiles per workgroup, dW_ih 32, dW_hh 16): the short
