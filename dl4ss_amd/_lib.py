@@ -75,13 +75,14 @@ SIGNATURES = {
     "dl4ss_birnn_plan_info": [I, I, I, I, I, P],
     "dl4ss_debug_set_spin_limit": [ctypes.c_uint],
     "dl4ss_debug_set_place_force": [ctypes.c_int],
+    "dl4ss_debug_set_rnn_max_wg": [ctypes.c_int],
 }
 # entry points that return a value rather than a hipError_t
 RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_colsum_bf16_part_bytes": ctypes.c_longlong,
             "dl4ss_gemm_bf16_gl_ws_bytes": ctypes.c_longlong,
             "dl4ss_gemm_bf16_gl_grouped_ws_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
             "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None,
-            "dl4ss_debug_set_place_force": None}
+            "dl4ss_debug_set_place_force": None, "dl4ss_debug_set_rnn_max_wg": None}
 
 _lib = None
 

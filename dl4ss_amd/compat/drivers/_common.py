@@ -8,6 +8,21 @@ import torch
 MSE = torch.nn.MSELoss()
 
 
+def require_torch_multi_loader_runs(cfg, driver):
+    """Fail once, when a driver on the Torch_multi loaders (predata_multiAims_dB / _3dB) starts, if
+    ``cfg.AUGMENT_DATA`` is set: those loaders' augmentation line ``signal[s:] + signal[:s]``
+    (Torch_multi/predata_multiAims_dB.py:164-166) is a numpy broadcast error for almost every shift,
+    so the reference stops at its first source (compat._data.torch_multi_augment restates it) --
+    and config_WSJ0_dB.py:112 sets the flag.  Raising here instead of inside the first batch tells
+    the user what to change before any model is built."""
+    if getattr(cfg, "AUGMENT_DATA", False):
+        raise RuntimeError(
+            f"{driver}: config_WSJ0_dB.AUGMENT_DATA is True, but the Torch_multi loader this driver uses "
+            "cannot augment (predata_multiAims_dB.py:166 raises ValueError on its first source, as in the "
+            "reference); set config_WSJ0_dB.AUGMENT_DATA = False to run it.  The TDAA_beta list loaders "
+            "(predata_fromList, predata_fromList_cRM_123) do rotate with the flag on.")
+
+
 def dev():
     return torch.device("cuda")
 

@@ -80,6 +80,7 @@ def train_step(m, optimizer, train_data, dict_spk2idx, dict_idx2spk, num_labels)
 
 
 def main(max_epoch=None, max_batches=None, log=print, loader="dB"):
+    C.require_torch_multi_loader_runs(config, "main_run_multi_selfSS_dB")
     np.random.seed(1)
     torch.manual_seed(1)
     random.seed(1)

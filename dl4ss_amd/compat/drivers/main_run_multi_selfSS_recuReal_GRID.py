@@ -28,6 +28,7 @@ import librosa  # noqa: E402,F401
 import soundfile as sf  # noqa: E402,F401
 
 from dl4ss_amd import checkpoint, engine, infer  # noqa: E402
+from dl4ss_amd.compat.drivers import _common as C  # noqa: E402
 
 
 def build(num_labels=101, B=1, T=None, precision=None):
@@ -63,6 +64,7 @@ def extract(ext, train_data, dict_idx2spk):
 
 
 def main(max_batches=2, log=print):
+    C.require_torch_multi_loader_runs(config, "main_run_multi_selfSS_recuReal_GRID")
     np.random.seed(1)
     torch.manual_seed(1)
     random.seed(1)

@@ -1787,11 +1787,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       ld.commit(sraw);
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
-      const int cell = pwi * cpw + lane;
-      if (lane < cpw && cell < ncell) {
+      // one lane per cell, in passes of 64: cpw = ceil(BC J / 2) is 80 at BC = 8, J = 20
+      for (int c = lane; c < cpw; c += 64) {
+        const int cell = pwi * cpw + c;
+        if (cell >= ncell) break;
         float v[NSL];
 #pragma unroll
-        for (int k = 0; k < NSL; ++k) v[k] = sraw[k * CPWP + lane];
+        for (int k = 0; k < NSL; ++k) v[k] = sraw[k * CPWP + c];
         float4 p0, p1;
         if constexpr (CELL == CELL_LSTM) {
           const float ig = v[1], fg = v[2], gg = v[3], og = v[4];
@@ -2081,7 +2083,9 @@ struct Plan {
 // workgroup must be resident at once, so the plan keeps 2 * nchunk * NG within the device's
 // CU count minus 1/16 of it (240 of 256 on a full MI355X; 30 on a 32-CU CPX partition),
 // leaving room for concurrent kernels (RCCL).  DL4SS_RNN_MAX_WG overrides it (experiments).
+int g_max_wg = 0;  // dl4ss_debug_set_rnn_max_wg (tests force the wider batch chunks)
 int wg_limit() {
+  if (g_max_wg > 0) return g_max_wg;
   static const int env = std::getenv("DL4SS_RNN_MAX_WG") ? std::atoi(std::getenv("DL4SS_RNN_MAX_WG")) : 0;
   if (env > 0) return env;
   const int cu = device_cu_count();
@@ -2305,6 +2309,11 @@ DL4SS_API void dl4ss_debug_set_spin_limit(unsigned limit) { g_spin_limit = limit
 // 1: the packed kernels write every granule through (`sc1`) as if the group spanned XCDs (test
 // hook for the cross-XCD form); 0: plain stores wherever the group was found on one XCD.
 DL4SS_API void dl4ss_debug_set_place_force(int force) { g_place_force = force == 1 ? 1 : 0; }
+
+// > 0: the co-residency budget of every later plan (max_wg of dl4ss_birnn_plan_info, in
+// workgroups) instead of the device's; 0 restores the default.  Test hook: a budget of 120 makes
+// the B = 32, H = 300 nets plan batch chunks of 8 (the plan a B >= 33 batch gets on a full part).
+DL4SS_API void dl4ss_debug_set_rnn_max_wg(int max_wg) { g_max_wg = max_wg > 0 ? max_wg : 0; }
 
 // The recurrence plan for (cell, B, H) under a co-residency budget of max_wg workgroups
 // (<= 0: the current device's, see wg_limit): info = {BC, NG, J, nchunk, grid}.  Host-only

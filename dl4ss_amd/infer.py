@@ -49,10 +49,13 @@ class _BiRNNStack:
         self.ws = torch.empty((wsn + 7) // 8, dtype=torch.int64, device=device)
         self.status = torch.zeros(1, dtype=torch.int32, device=device)
 
-    def run(self, x2d, cat_view, precision):
+    def run(self, x2d, cat_view, precision, rnn_precision=None):
         """x2d (B*T, D0) fp32 -> (B, T, 2H); cat_view(kind, l) gives the [fwd; reverse]
-        parameter of layer l (``weight_ih`` / ``weight_hh`` / ``bias_ih`` / ``bias_hh``)."""
+        parameter of layer l (``weight_ih`` / ``weight_hh`` / ``bias_ih`` / ``bias_hh``).
+        ``precision``: the input-projection GEMMs; ``rnn_precision`` (default: the same) the
+        recurrent matvec."""
         B, T, H = self.B, self.T, self.H
+        rnn_precision = rnn_precision or precision
         st = _lib.stream_ptr()
         x = x2d
         out = None
@@ -60,7 +63,7 @@ class _BiRNNStack:
             ops.gemm(x, cat_view("weight_ih", l), transB=True, bias=cat_view("bias_ih", l), out=self.G,
                      precision=precision)
             out = self.out[l % 2]
-            _lib.call("dl4ss_birnn_fwd", CELLS[self.cell], ops.PREC[precision], B, T, H, _lib.ptr(self.G),
+            _lib.call("dl4ss_birnn_fwd", CELLS[self.cell], ops.PREC[rnn_precision], B, T, H, _lib.ptr(self.G),
                       _lib.ptr(cat_view("weight_hh", l)), _lib.ptr(cat_view("bias_hh", l)), _lib.ptr(out),
                       _lib.ptr(self.hprev), _lib.ptr(self.act), _lib.ptr(self.cs) if self.cs is not None else None,
                       _lib.ptr(self.ws), self.wsn, _lib.ptr(self.status), st)
@@ -158,16 +161,18 @@ class ClassifierForward:
 
 
 class MaskNetForward:
-    """MIX_SPEECH forward on a SepNet: V (B*T, F*E) = tanh(Linear(BiRNN(X)))."""
+    """MIX_SPEECH forward on a SepNet: V (B*T, F*E) = tanh(Linear(BiRNN(X))).  ``precision``: the
+    GEMMs (input projections, Linear); ``rnn_precision`` (default: the same): the recurrence."""
 
-    def __init__(self, net, B, T, precision="fp32"):
+    def __init__(self, net, B, T, precision="fp32", rnn_precision=None):
         self.net, self.B, self.T, self.precision = net, B, T, precision
+        self.rnn_precision = rnn_precision or precision
         self.stack = _BiRNNStack(net.cell, net.H, net.L, B, T, net.device)
         self.h = None
 
     def __call__(self, feats, out):
         B, T, net = self.B, self.T, self.net
-        self.h = self.stack.run(feats.reshape(B * T, -1), net.cat_view, self.precision)
+        self.h = self.stack.run(feats.reshape(B * T, -1), net.cat_view, self.precision, self.rnn_precision)
         ops.gemm(self.h.view(B * T, 2 * net.H), net.view("mix.Linear.weight"), transB=True,
                  bias=net.view("mix.Linear.bias"), epilogue=ops.EPI_TANH, out=out, precision=self.precision)
         return out
@@ -189,18 +194,33 @@ def select_speakers(classifier, feats, alpha=-0.5, top_k=2):
 class RecursiveExtractor:
     """The recursive extraction loop of GRID.py:383-475 for a batch of B independent rows
     (the reference runs B = 1).  ``net``: the GRID mask net (SepNet, BiGRU-2L,
-    no ADJUST; its ``emb.layer.weight`` is the speaker embedding); ``cnet``: ClassifierNet."""
+    no ADJUST; its ``emb.layer.weight`` is the speaker embedding); ``cnet``: ClassifierNet.
+
+    ``precision``: "fp32" (exact GEMMs and recurrences), "bf16" (bf16 operands everywhere, fp32
+    accumulate and state) or "mixed" -- the mask net's GEMMs (input projections, Linear -> V) in
+    fp32 with its recurrence on bf16 operands, the classifier in bf16.  The masks are sigmoids of
+    V . emb with N(0,1) speaker embeddings and no ADDJUST: every bf16 GEMM operand of the mask net
+    costs ~1e-3 of masked-magnitude error (tools/bf16_budget.py on the same BiGRU-2L net), the
+    recurrence ~0.3e-3, so "mixed" is the mode within the north-star 1e-3 (C5 in DESIGN.md
+    section 6).  The classifier only decides the speaker ids (its bf16 probabilities are within
+    ~1e-4 of fp32)."""
+
+    MODES = {"fp32": ("fp32", "fp32", "fp32"), "bf16": ("bf16", "bf16", "bf16"), "mixed": ("fp32", "bf16", "bf16")}
 
     def __init__(self, net, cnet, B, T, precision="fp32", alpha=-0.3, top_k=3, max_steps=2):
         if net.E != 50 or net.crm:
             raise ValueError("the recursive path is the magnitude-mask 'dot' attention with E = 50")
+        if precision not in self.MODES:
+            raise ValueError(f"precision {precision!r}: expected one of {sorted(self.MODES)}")
+        mask_gemm, mask_rnn, cls_prec = self.MODES[precision]
+        self.precision = precision
         self.net, self.cnet, self.B, self.T = net, cnet, B, T
         self.alpha, self.top_k, self.S = alpha, top_k, max_steps
         dev = net.device
         F, E = net.F, net.E
         f32 = dict(device=dev, dtype=torch.float32)
-        self.mask_net = MaskNetForward(net, B, T, precision)
-        self.classifier = ClassifierForward(cnet, B, T, precision)
+        self.mask_net = MaskNetForward(net, B, T, mask_gemm, mask_rnn)
+        self.classifier = ClassifierForward(cnet, B, T, cls_prec)
         self.V0 = torch.empty(B * T, F * E, **f32)
         self.V = torch.empty(B * T, F * E, **f32)
         self.feats = [torch.empty(B, T, F, **f32) for _ in range(2)]

@@ -218,11 +218,11 @@ class GroupedGemm:
 
     def __init__(self, problems, device):
         import ctypes
-        n = len(problems)
-        if not 1 <= n <= 16:
+        if not 1 <= len(problems) <= 16:
             raise RuntimeError("GroupedGemm: 1..16 problems")
         ta, tb = int(problems[0]["transA"]), int(problems[0]["transB"])
-        dims, self._keep = [], []
+        dims, self._keep, kept = [], [], []
+        self._k0 = []  # K = 0 problems with beta != 1: C = beta C, applied by run()
         for p in problems:
             A, B, out = p["A"], p["B"], p["out"]
             _mat_bf16(A, "GroupedGemm(A)")
@@ -241,12 +241,26 @@ class GroupedGemm:
                     raise RuntimeError(f"GroupedGemm: out shape {tuple(out.shape)} != {(M, N)}")
             # explicit M / N / K: the kernel and its combine must stay inside every view
             # (the argument arrays are frozen here, so a wrong view would be written past silently)
-            if not (0 < M <= shapeA[0] and 0 < K <= shapeA[1] and K <= shapeB[0] and 0 < N <= shapeB[1]):
+            if not (0 <= M <= shapeA[0] and 0 <= K <= shapeA[1] and K <= shapeB[0] and 0 <= N <= shapeB[1]):
                 raise RuntimeError(f"GroupedGemm: M, N, K = {(M, N, K)} exceed the operand views")
-            if not (out.shape[0] >= M and out.shape[1] >= N and out.stride(0) >= N):
+            if not (out.shape[0] >= M and out.shape[1] >= N and (N == 0 or out.stride(0) >= N)):
                 raise RuntimeError(f"GroupedGemm: out view {tuple(out.shape)} (ldc {out.stride(0)}) < {(M, N)}")
+            # empty problems (an empty batch: M or N = 0, or K = 0) launch nothing: no output, or
+            # C = beta C with an empty sum
+            if M == 0 or N == 0:
+                continue
+            if K == 0:
+                if float(p.get("beta", 0.0)) != 1.0:
+                    self._k0.append((out[:M, :N], float(p.get("beta", 0.0))))
+                continue
             dims.append((M, N, K))
+            kept.append(p)
             self._keep += [A, B, out]
+        problems = kept
+        n = len(problems)
+        self.n = n
+        if n == 0:
+            return
         Iv = lambda xs: (ctypes.c_int * n)(*xs)
         Lv = lambda xs: (ctypes.c_longlong * n)(*xs)
         Pv = lambda xs: (ctypes.c_void_p * n)(*xs)
@@ -266,6 +280,10 @@ class GroupedGemm:
         self.ws = torch.empty(max(int(nb), 1), device=device, dtype=torch.uint8)
 
     def run(self):
+        for c, beta in self._k0:
+            c.mul_(beta)
+        if self.n == 0:
+            return
         _lib.call("dl4ss_gemm_bf16_gl_grouped", self.n, self.ta, self.tb, self.M, self.N, self.K, self.A, self.lda,
                   self.B, self.ldb, self.C, self.ldc, self.beta, self.splitk, _lib.ptr(self.ws), self.ws.numel(),
                   _lib.stream_ptr())

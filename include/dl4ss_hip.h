@@ -168,6 +168,10 @@ void dl4ss_debug_set_spin_limit(unsigned limit);
 /* Test hook: 1 = the packed (bf16) recurrence kernels write every hand-off granule through
  * (`sc1`), as for a group whose workgroups span XCDs; 0 = by the placement found at launch. */
 void dl4ss_debug_set_place_force(int force);
+/* Test hook: > 0 replaces the device's co-residency budget (workgroups per persistent launch) in
+ * every later recurrence plan -- e.g. 120 gives the B = 32, H = 300 nets batch chunks of 8, the
+ * plan of B >= 33 on a full MI355X; 0 restores the default. */
+void dl4ss_debug_set_rnn_max_wg(int max_wg);
 /* One layer, both directions: G (B,T,2,NG*H) = X W_ih^T + b_ih (NG = 4 LSTM / 3 GRU),
  * W_hh (2, NG*H, H), b_hh (2, NG*H) -> out (B,T,2H) [fwd | reverse], hprev (B,T,2H)
  * (h_{t-1} per step), act (B,T,2,4H) gate activations, cs (B,T,2,H) LSTM cells.

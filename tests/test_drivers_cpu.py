@@ -108,3 +108,17 @@ def test_inception_v3_constructs_with_reference_names():
     assert list(sd) == list(fx["names"])
     assert [",".join(map(str, v.shape)) for v in sd.values()] == list(fx["shapes"])
     assert net.transform_input
+
+
+@pytest.mark.parametrize("driver", ["main_run_multi_selfSS_dB", "main_run_multi_selfSS_recuReal_GRID"])
+def test_torch_multi_drivers_refuse_augment_at_start(driver):
+    """config_WSJ0_dB.py:112 sets AUGMENT_DATA, which the Torch_multi loaders cannot run
+    (predata_multiAims_dB.py:166 raises on the first source): the drivers on those loaders fail
+    once, at start, with the fix in the message -- not inside their first batch."""
+    compat.install(drivers=True)
+    import config_WSJ0_dB as cfg
+
+    m = importlib.import_module(driver)
+    assert cfg.AUGMENT_DATA is True
+    with pytest.raises(RuntimeError, match="AUGMENT_DATA = False"):
+        m.main(log=lambda *a: None)

@@ -91,3 +91,26 @@ def test_grouped_rejects_views_it_would_write_past(dev):
         ops.GroupedGemm([dict(ok, out=torch.zeros(80, 32, device=dev), M=80)], dev)
     with pytest.raises(RuntimeError, match="out view"):
         ops.GroupedGemm([dict(ok, out=torch.zeros(64, 16, device=dev), N=32)], dev)
+
+
+def test_grouped_empty_problems_are_no_ops(dev):
+    """an empty dimension (an empty batch) is a no-op problem, not an error: M or N = 0
+    writes nothing, K = 0 leaves C = beta C; the other problems of the group still run."""
+    g = torch.Generator().manual_seed(3)
+    A = _bf(g, dev, 96, 64)
+    B = _bf(g, dev, 96, 32)
+    out = torch.zeros(64, 32, device=dev)
+    c_k0 = torch.ones(64, 32, device=dev)
+    c_k0b = torch.ones(64, 32, device=dev)
+    empty_a = torch.zeros(0, 64, device=dev, dtype=torch.bfloat16)
+    empty_b = torch.zeros(0, 32, device=dev, dtype=torch.bfloat16)
+    probs = [dict(A=A, B=B, out=out, transA=True, transB=False, beta=0.0),
+             dict(A=A[:, :0], B=B, out=torch.zeros(0, 32, device=dev), transA=True, transB=False),  # M = 0
+             dict(A=empty_a, B=empty_b, out=c_k0, transA=True, transB=False, beta=0.5),  # K = 0
+             dict(A=empty_a, B=empty_b, out=c_k0b, transA=True, transB=False, beta=1.0)]
+    ops.GroupedGemm(probs, dev).run()
+    torch.cuda.synchronize()
+    ref = A.double().cpu().t() @ B.double().cpu()
+    assert (out.double().cpu() - ref).abs().max() <= 1e-5 * ref.abs().max()
+    assert bool((c_k0 == 0.5).all()) and bool((c_k0b == 1.0).all())
+    ops.GroupedGemm([probs[1]], dev).run()  # nothing left to launch

@@ -1,4 +1,6 @@
 """GPU parity of the dense / recurrent kernels against torch-CPU (fp64) references."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -280,3 +282,23 @@ def test_birnn_fwd_large_hidden(dev, cell, B, T, prec):
             _lib.call("dl4ss_birnn_bwd", cellid, prec, B, T, H, _lib.ptr(o), None, _lib.ptr(whd), _lib.ptr(act),
                       _lib.ptr(cs), _lib.ptr(hp), _lib.ptr(dG), _lib.ptr(dG), _lib.ptr(wsb), ws, _lib.ptr(st),
                       _lib.stream_ptr())
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+@pytest.mark.parametrize("B,T", [(32, 12), (29, 7)])
+def test_birnn_batch_chunk_8(dev, cell, B, T):
+    """The plan a B >= 33 batch gets on a full MI355X (or B = 32 under a smaller co-residency
+    budget, or a CPX partition): batch chunks of BC = 8, 160 cells per group -- 80 per BPTT
+    prefetch wave, more than its 64 lanes (the step factors are formed in passes of 64 lanes,
+    round-5 fix).  Forced here with a 120-workgroup budget; bf16 and fp32 recurrences against
+    the fp64 references of test_birnn_bwd_dG_per_step."""
+    lib = _lib.lib()
+    info = (ctypes.c_int * 5)()
+    lib.dl4ss_debug_set_rnn_max_wg(120)
+    try:
+        _lib.call("dl4ss_birnn_plan_info", 0 if cell == "lstm" else 1, B, 300, 1, 0, info)
+        assert info[0] == 8 and info[4] <= 120, list(info)
+        for prec in (1, 0):
+            test_birnn_bwd_dG_per_step(dev, cell, B, T, 300, prec)
+    finally:
+        lib.dl4ss_debug_set_rnn_max_wg(0)

@@ -169,3 +169,37 @@ def test_dh_split_above_three_fits_the_workspace(dev, monkeypatch):
     loss = tr.step(*_batch(dev, B, K, N, 6))
     tr.check()
     assert np.isfinite(float(loss[0].item()))
+
+
+def test_captured_trainer_freed_by_refcount(dev):
+    """A trainer that has run eager and graph steps (its CUDAGraph, grouped-GEMM argument arrays,
+    workspaces) is freed by reference counting alone once dropped: with the collector off, nothing
+    of it can be left for a collection inside a later capture (the round-4 abort;
+    tests/test_lifetime_cpu.py pins the same on freshly built trainers)."""
+    import gc
+    import weakref
+
+    B, K, N = 2, 2, 4000
+    batch = _batch(dev, B, K, N, 3)
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=3)
+        tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+        tr.step(*batch)
+        tr.step_graph(*batch)
+        tr.check()
+        refs = [weakref.ref(tr), weakref.ref(tr.graph), weakref.ref(tr._dw_group)]
+        del tr
+        torch.cuda.synchronize()
+        assert all(r() is None for r in refs), [r() is None for r in refs]
+        # and the next trainer captures normally
+        tr2 = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+        tr2.step(*batch)
+        loss = tr2.step_graph(*batch)
+        tr2.check()
+        assert torch.isfinite(loss[:1]).all()
+    finally:
+        if was:
+            gc.enable()
