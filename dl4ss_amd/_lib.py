@@ -37,6 +37,7 @@ SIGNATURES = {
     "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
     "dl4ss_gemm_bf16_gl_grouped_ws_bytes": [I, P, P, P, P],
     "dl4ss_gemm_bf16_gl_grouped": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P],
+    "dl4ss_gemm_bf16_gl_grouped_ex": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, I, I, I, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_fwd_xw": [I, I, I, I, P, I, LL, P, LL, P, P, P, P, P, P, P, P, P, P, LL, P, P, I],
     "dl4ss_birnn_fwd_xw_supported": [I, I, I, I, I],
@@ -71,6 +72,7 @@ SIGNATURES = {
     "dl4ss_bss_gram": [P, I, I, I, I, P, P, P, P],
     "dl4ss_adam_guarded": [P, P, P, P, LL, F, F, F, F, I, P, P, P],
     "dl4ss_adam_guarded_dp": [P, P, P, P, LL, F, F, F, F, I, P, P, P, P],
+    "dl4ss_adam_guarded_dp_scaled": [P, P, P, P, LL, F, F, F, F, I, P, P, F, P, P],
     "dl4ss_status_flag": [P, P, P],
     "dl4ss_birnn_plan_info": [I, I, I, I, I, P],
     "dl4ss_debug_set_spin_limit": [ctypes.c_uint],

@@ -1158,20 +1158,23 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       }
       STAMP(6)
       if (tid == 0) TRACE(0, s);
+#ifndef FWD_EXP_SKIP
+#define FWD_EXP_SKIP 0  // timing experiments only (results wrong): skip saved-state stores, bits 1 act, 2 cs, 4 out, 8 outb, 16 hprevb
+#endif
       if (cval) {
         const long long bt = (long long)bg * T + t;
         float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
-        actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
-        if constexpr (CELL == CELL_LSTM) a.cs[(bt * 2 + d) * H + cj] = cst;
+        if (!(FWD_EXP_SKIP & 1)) { actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3]; }
+        if constexpr (CELL == CELL_LSTM) if (!(FWD_EXP_SKIP & 2)) a.cs[(bt * 2 + d) * H + cj] = cst;
         const long long ho = bt * 2 * H + d * H + cj;
         if (a.hprev) a.hprev[ho] = hst;
-        a.out[ho] = hn;
+        if (!(FWD_EXP_SKIP & 4)) a.out[ho] = hn;
         // bf16 copies, 16-B aligned rows for the GEMMs: out_bf16 (B*T, pad8(2H)) with the
         // directions adjacent (the next layer's K), hprev_bf16 (B*T, 2 pad8(H)) with each
         // direction's block 16-B aligned (the per-direction dW_hh operand)
         const int hp8 = (H + 7) & ~7, op8 = (2 * H + 7) & ~7;
-        if (a.outb) a.outb[bt * op8 + d * H + cj] = bf16_rne(hn);
-        if (a.hprevb) a.hprevb[bt * 2 * hp8 + d * hp8 + cj] = bf16_rne(hst);
+        if (a.outb && !(FWD_EXP_SKIP & 8)) a.outb[bt * op8 + d * H + cj] = bf16_rne(hn);
+        if (a.hprevb && !(FWD_EXP_SKIP & 16)) a.hprevb[bt * 2 * hp8 + d * hp8 + cj] = bf16_rne(hst);
       }
       hst = hn;
     }
@@ -1994,7 +1997,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     STAMP(5)
     // this step's dG / dGh, after the publish (off the critical path; issued after B1 of the next
     // step instead they measured slower, 7994 vs 8085 mixtures/s, round 3)
+#ifndef BWD_EXP_NO_DG  // timing experiments only (results wrong): the BPTT without its dG stores
     store_dg();
+#endif
     STAMP(6)
   }
   // fused bias gradients: this cell's sums over t, one plain store per (row, gate) into the
@@ -2156,8 +2161,17 @@ int launch_resident(K kernel, int grid, size_t smem, hipStream_t st, const RnnAr
   return (int)hipLaunchKernel(reinterpret_cast<const void*>(kernel), dim3(grid), dim3(NT), args, smem, st);
 }
 
+// RNN_EXP_MINIMAL (experiment variant libraries only, tools/variant_lib.py --minimal): only the packed
+// bf16 kernels at BC = 4 are instantiated -- the C2 / C4 training step at B = 32 -- so a variant of
+// this file compiles in a fraction of the full build's time; every other plan fails its launch.
 template <int CELL, int BC>
 int launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
+#ifdef RNN_EXP_MINIMAL
+  if (BC != 4 || !mf || !pk) return (int)hipErrorNotSupported;
+  if (a.Xb && a.Kin <= 5 * 32) return launch_resident(rnn_fwd_pk_kernel<CELL, 4, 5>, grid, smem, st, a);
+  if (a.Xb) return launch_resident(rnn_fwd_pk_kernel<CELL, 4, XKMAX>, grid, smem, st, a);
+  return launch_resident(rnn_fwd_pk_kernel<CELL, 4>, grid, smem, st, a);
+#else
   if (a.H > HMAX) {  // forward-only large-H instantiations (the H = 600 classifier)
     if (mf)
       return launch_resident(rnn_fwd_kernel<CELL, BC, 0, true, HMAX_L>, grid, smem, st, a);
@@ -2179,11 +2193,16 @@ int launch_fwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStr
     return launch_resident(rnn_fwd_kernel<CELL, BC, 40, false>, grid, smem, st, a);
   else
     return launch_resident(rnn_fwd_kernel<CELL, BC, 0, false>, grid, smem, st, a);
+#endif
 }
 template <int CELL, int BC>
 int launch_bwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStream_t st) {
   int rpln, kgln;
   bwd_dims(a.RPL, a.KGL, rpln, kgln);
+#ifdef RNN_EXP_MINIMAL
+  if (BC != 4 || !mf || !pk) return (int)hipErrorNotSupported;
+  return launch_resident(rnn_bwd_pk_kernel<CELL, 4>, grid, smem, st, a);
+#else
   if (mf && pk)
     return launch_resident(rnn_bwd_pk_kernel<CELL, BC>, grid, smem, st, a);
   else if (mf)
@@ -2194,6 +2213,7 @@ int launch_bwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStr
     return launch_resident(rnn_bwd_kernel<CELL, BC, 20, 2, false>, grid, smem, st, a);
   else
     return launch_resident(rnn_bwd_kernel<CELL, BC, 0, 0, false>, grid, smem, st, a);
+#endif
 }
 
 template <int CELL>

@@ -654,13 +654,7 @@ struct GlGroup {
 };
 
 template <bool A_KC, bool B_KC, class CF>
-__global__ __launch_bounds__(CF::NT, 2) void gemm_gl_grouped_kernel(GlGroup g) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
-  // problems by DISPATCH order (so every problem's workgroups are dealt over all 8 XCDs: an
-  // XCD-contiguous remap of the whole grid handed one XCD nearly all of dW_lin's long k-ranges,
-  // 616 vs ~330 us), then the XCD-major remap inside the problem (L0 = its first dispatch index;
-  // L - L0 with equal residues mod 8 share an XCD, whatever L0 % 8 is)
-  const int L = blockIdx.x;
+__device__ __forceinline__ void grouped_tile(const GlGroup& g, int L, unsigned short* smem) {
   int pi = 0;
 #pragma unroll
   for (int k = 1; k < GMAXP; ++k)
@@ -691,6 +685,21 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_gl_grouped_kernel(GlGroup g) {
   else
     gl_tile<A_KC, B_KC, EPI_NONE, false, CF>(smem, p.M, p.N, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, nullptr, p.beta, m0,
                                              n0, kbeg, kend - kbeg, nullptr);
+}
+
+template <bool A_KC, bool B_KC, class CF>
+__global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) void gemm_gl_grouped_kernel(GlGroup g) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
+  // problems by DISPATCH order (so every problem's workgroups are dealt over all 8 XCDs: an
+  // XCD-contiguous remap of the whole grid handed one XCD nearly all of dW_lin's long k-ranges,
+  // 616 vs ~330 us), then the XCD-major remap inside the problem (L0 = its first dispatch index;
+  // L - L0 with equal residues mod 8 share an XCD, whatever L0 % 8 is).  A grid smaller than the
+  // tile count (the persistent form, dl4ss_gemm_bf16_gl_grouped_ex) walks the tiles in steps of
+  // gridDim.x.
+  for (int L = blockIdx.x; L < g.total_wg; L += gridDim.x) {
+    if (L != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue is done with the LDS
+    grouped_tile<A_KC, B_KC, CF>(g, L, smem);
+  }
 }
 
 // The split-K combine of every split problem of a group, one launch: unit u of problem p is four
@@ -920,17 +929,13 @@ DL4SS_API long long dl4ss_gemm_bf16_gl_grouped_ws_bytes(int n, const int* M, con
   return tot;
 }
 
-// Grouped C_i = op(A_i) op(B_i) + beta_i C_i for i < n (n <= 16) in ONE launch (+ one split-K combine
-// launch): the backward's weight gradients.  Every problem has the layout rules of
-// dl4ss_gemm_bf16_gl with the SAME transA / transB, no bias, EPI_NONE; splitk[i] as there (the
-// same slabs and fixed-order sums, so each C_i is bitwise the single launch's).
-DL4SS_API int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const int* M, const int* N, const int* K,
-                                         const void* const* A, const long long* lda, const void* const* B,
-                                         const long long* ldb, float* const* C, const long long* ldc,
-                                         const float* beta, const int* splitk, void* ws, long long ws_bytes,
-                                         void* stream) {
-  DL4SS_REQUIRE(n >= 1 && n <= GMAXP && M && N && K && A && lda && B && ldb && C && ldc && beta && splitk);
-  const bool a_kc = !transA, b_kc = transB;
+namespace {
+// the grouped launch in tile configuration CF over `grid` workgroups (<= 0: one per tile)
+template <class CF>
+int grouped_launch(int n, bool a_kc, bool b_kc, const int* M, const int* N, const int* K, const void* const* A,
+                   const long long* lda, const void* const* B, const long long* ldb, float* const* C,
+                   const long long* ldc, const float* beta, const int* splitk, void* ws, long long ws_bytes, int grid,
+                   size_t dyn_lds, hipStream_t st) {
   GlGroup g{};
   long long off = 0;
   int wg = 0, units = 0;
@@ -950,7 +955,7 @@ DL4SS_API int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const in
     p.lda = lda[i]; p.ldb = ldb[i]; p.ldc = ldc[i];
     p.beta = beta[i];
     p.M = M[i]; p.N = N[i]; p.K = K[i];
-    p.gm = (M[i] + C128::BM - 1) / C128::BM;
+    p.gm = (M[i] + CF::BM - 1) / CF::BM;
     p.gn = (N[i] + BN - 1) / BN;
     int sk = splitk[i] < 1 ? 1 : splitk[i];
     int kps = (K[i] + sk - 1) / sk;
@@ -975,15 +980,54 @@ DL4SS_API int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const in
   g.n = n;
   g.total_wg = wg;
   g.total_units = units;
-  hipStream_t st = as_stream(stream);
-  if (a_kc && b_kc) hipLaunchKernelGGL((gemm_gl_grouped_kernel<true, true, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
-  else if (a_kc) hipLaunchKernelGGL((gemm_gl_grouped_kernel<true, false, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
-  else if (b_kc) hipLaunchKernelGGL((gemm_gl_grouped_kernel<false, true, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
-  else hipLaunchKernelGGL((gemm_gl_grouped_kernel<false, false, C128>), dim3(wg), dim3(C128::NT), 0, st, g);
+  const int nwg = grid > 0 && grid < wg ? grid : wg;
+#define GGR(AK, BKC) \
+  hipLaunchKernelGGL((gemm_gl_grouped_kernel<AK, BKC, CF>), dim3(nwg), dim3(CF::NT), dyn_lds, st, g)
+  if (a_kc && b_kc) GGR(true, true);
+  else if (a_kc) GGR(true, false);
+  else if (b_kc) GGR(false, true);
+  else GGR(false, false);
+#undef GGR
   DL4SS_CHECK_LAUNCH();
   if (units > 0) {
     hipLaunchKernelGGL(gemm_gl_grouped_reduce_kernel, dim3(cdiv(units, 256)), dim3(256), 0, st, g);
     DL4SS_CHECK_LAUNCH();
   }
   return 0;
+}
+}  // namespace
+
+// Grouped C_i = op(A_i) op(B_i) + beta_i C_i for i < n (n <= 16) in ONE launch (+ one split-K combine
+// launch): the backward's weight gradients.  Every problem has the layout rules of
+// dl4ss_gemm_bf16_gl with the SAME transA / transB, no bias, EPI_NONE; splitk[i] as there (the
+// same slabs and fixed-order sums, so each C_i is bitwise the single launch's).
+DL4SS_API int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const int* M, const int* N, const int* K,
+                                         const void* const* A, const long long* lda, const void* const* B,
+                                         const long long* ldb, float* const* C, const long long* ldc,
+                                         const float* beta, const int* splitk, void* ws, long long ws_bytes,
+                                         void* stream) {
+  DL4SS_REQUIRE(n >= 1 && n <= GMAXP && M && N && K && A && lda && B && ldb && C && ldc && beta && splitk);
+  return grouped_launch<C128>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes, 0, 0,
+                              as_stream(stream));
+}
+
+// The persistent form: `grid` workgroups walk the group's tiles (grid <= 0: one per tile, as
+// dl4ss_gemm_bf16_gl_grouped), in tile configuration cfg (1 = 128 x 128 double buffer; 2 = 256 x
+// 128, three stages, 144 KB LDS: one workgroup per CU); one_per_cu pads cfg 1's LDS so that one
+// workgroup fills a CU.  For a side stream beside the persistent recurrence, which leaves the CUs
+// above its co-residency budget free (dl4ss_birnn_plan_info).
+DL4SS_API int dl4ss_gemm_bf16_gl_grouped_ex(int n, int transA, int transB, const int* M, const int* N, const int* K,
+                                            const void* const* A, const long long* lda, const void* const* B,
+                                            const long long* ldb, float* const* C, const long long* ldc,
+                                            const float* beta, const int* splitk, void* ws, long long ws_bytes,
+                                            int grid, int cfg, int one_per_cu, void* stream) {
+  DL4SS_REQUIRE(n >= 1 && n <= GMAXP && M && N && K && A && lda && B && ldb && C && ldc && beta && splitk);
+  DL4SS_REQUIRE(cfg == 1 || cfg == 2);
+  hipStream_t st = as_stream(stream);
+  if (cfg == 2)
+    return grouped_launch<C256>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes, grid,
+                                0, st);
+  // C128 holds 64 KB: 20 KB more dynamic LDS leaves room for only one workgroup per CU
+  return grouped_launch<C128>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes, grid,
+                              one_per_cu ? 20 * 1024 : 0, st);
 }

@@ -243,7 +243,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2s,
                                                    const int* __restrict__ status, int* __restrict__ refused,
-                                                   const float* __restrict__ dp_flag, float* __restrict__ loss) {
+                                                   const float* __restrict__ dp_flag, float gscale,
+                                                   float* __restrict__ loss) {
   // refuse the update when a recurrence hand-off of this step timed out on this rank
   // (status[0]) or on any data-parallel peer (dp_flag: the all-reduced status flag)
   if ((status && status[0]) || (dp_flag && dp_flag[0] != 0.f)) {
@@ -258,7 +259,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
        i += (long long)gridDim.x * blockDim.x * 4) {
     if (i + 3 < n) {
       float4 pp = *reinterpret_cast<float4*>(p + i);
-      const float4 gg = *reinterpret_cast<const float4*>(g + i);
+      float4 gg = *reinterpret_cast<const float4*>(g + i);
+      gg.x *= gscale; gg.y *= gscale; gg.z *= gscale; gg.w *= gscale;  // 1 / world (DP SUM); 1: exact
       float4 mm = *reinterpret_cast<float4*>(m + i);
       float4 vv = *reinterpret_cast<float4*>(v + i);
 #define ADAM1(c)                                              \
@@ -272,8 +274,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
       *reinterpret_cast<float4*>(v + i) = vv;
     } else {
       for (long long j = i; j < n; ++j) {
-        m[j] = m[j] + (1.f - b1) * (g[j] - m[j]);
-        v[j] = b2 * v[j] + (1.f - b2) * g[j] * g[j];
+        const float gj = g[j] * gscale;
+        m[j] = m[j] + (1.f - b1) * (gj - m[j]);
+        v[j] = b2 * v[j] + (1.f - b2) * gj * gj;
         p[j] -= step * (m[j] / (sqrtf(v[j]) / bc2s + eps));
       }
     }
@@ -341,8 +344,8 @@ DL4SS_API int dl4ss_colsum(const float* A, long long lda, int M, int N, float* o
 
 namespace {
 int adam_launch(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
-                float eps, int step, const int* status, int* refused, const float* dp_flag, float* loss,
-                void* stream) {
+                float eps, int step, const int* status, int* refused, const float* dp_flag, float gscale,
+                float* loss, void* stream) {
   DL4SS_REQUIRE(p && g && m && v && n >= 0 && step >= 1);
   if (n == 0) return 0;
   // bias corrections in double on the host, as torch computes them in Python floats
@@ -350,7 +353,7 @@ int adam_launch(float* p, const float* g, float* m, float* v, long long n, float
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   const unsigned grid = (unsigned)min(8192LL, (n / 4 + 255) / 256 + 1);
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr, beta1, beta2, eps,
-                     bc1, bc2s, status, refused, dp_flag, loss);
+                     bc1, bc2s, status, refused, dp_flag, gscale, loss);
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
@@ -358,21 +361,29 @@ int adam_launch(float* p, const float* g, float* m, float* v, long long n, float
 
 DL4SS_API int dl4ss_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                          float beta2, float eps, int step, void* stream) {
-  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, nullptr, nullptr, nullptr, stream);
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, nullptr, nullptr, 1.0f, nullptr, stream);
 }
 
 // status: ONE int (the hand-off word), read only; a refusal shows as loss[0] = NaN
 DL4SS_API int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                                  float beta2, float eps, int step, int* status, float* loss, void* stream) {
-  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, nullptr, nullptr, loss, stream);
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, nullptr, nullptr, 1.0f, loss, stream);
 }
 
 // status: 2 ints {hand-off word, refused-update count}; the count is incremented per refusal
 DL4SS_API int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                                     float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
                                     void* stream) {
-  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, status ? status + 1 : nullptr, dp_flag, loss,
-                     stream);
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, status ? status + 1 : nullptr, dp_flag, 1.0f,
+                     loss, stream);
+}
+
+// the DP form on the SUM-reduced gradient: g * gscale (gscale = 1 / world) inside the update
+DL4SS_API int dl4ss_adam_guarded_dp_scaled(float* p, const float* g, float* m, float* v, long long n, float lr,
+                                           float beta1, float beta2, float eps, int step, int* status,
+                                           const float* dp_flag, float gscale, float* loss, void* stream) {
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, status ? status + 1 : nullptr, dp_flag, gscale,
+                     loss, stream);
 }
 
 __global__ void status_flag_kernel(const int* __restrict__ status, float* __restrict__ flag) {

@@ -33,6 +33,28 @@ def allreduce_mean_(flat, pg=None):
     return flat
 
 
+def allreduce_sum_async(t, pg=None):
+    """Start the SUM all-reduce of t over ranks; returns the work handle (None without a process
+    group).  On RCCL the collective runs on the group's own stream, ordered after the work
+    enqueued on the current stream so far, so the caller can go on enqueueing (the next graph
+    replay) and make the current stream wait later with ``work.wait()``.  The trainer applies the
+    1 / world of the mean inside Adam (dl4ss_adam_guarded_dp_scaled), not as a pass over t."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg, async_op=True)
+
+
+def allreduce_buckets_(ext, split, pg=None):
+    """The bucketed form of one SUM all-reduce of ``ext``: [split, end) first, then [0, split), both
+    asynchronous, then waited for -- elementwise the same sums as the flat all-reduce
+    (tests/test_dp_cpu.py)."""
+    works = [allreduce_sum_async(ext[split:], pg), allreduce_sum_async(ext[:split], pg)]
+    for w in works:
+        if w is not None:
+            w.wait()
+    return ext
+
+
 def max_over_ranks(value, device, pg=None):
     """Max of a host float over ranks (bench timing: the slowest rank's time)."""
     if world(pg) == 1:

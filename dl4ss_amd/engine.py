@@ -63,12 +63,14 @@ class SepNet:
         self.numel = off
         self.device = torch.device(device)
         self.flat = torch.zeros(off, device=self.device, dtype=torch.float32)
-        # the flat gradient plus one 16-B slot behind it: slot 0 carries each rank's hand-off
-        # status flag through the gradient all-reduce (SepTrainer.allreduce), so every rank's
-        # guarded Adam refuses the same steps
+        # the flat gradient behind one 16-B slot: slot 0 carries each rank's hand-off status flag
+        # through the gradient all-reduce (SepTrainer.allreduce), so every rank's guarded Adam
+        # refuses the same steps.  Layout [flag | layers | Linear, emb, adj]: the data-parallel
+        # step's two buckets are the contiguous ranges in front of and behind the Linear weight
+        # (bucket_split)
         self.grad_ext = torch.zeros(off + 4, device=self.device, dtype=torch.float32)
-        self.grad = self.grad_ext[:off]
-        self.dp_flag = self.grad_ext[off:off + 1]
+        self.grad = self.grad_ext[4:]
+        self.dp_flag = self.grad_ext[0:1]
         self.reset_parameters(seed)
 
     def view(self, name, buf=None):
@@ -82,6 +84,12 @@ class SepNet:
         n = a.numel()
         base = self.flat if buf is None else buf
         return base[off:off + 2 * n].view(2 * a.shape[0], *a.shape[1:]) if a.dim() == 2 else base[off:off + 2 * n]
+
+    def bucket_split(self):
+        """Index into grad_ext between the data-parallel buckets: [0, split) = the status flag and
+        every recurrent layer (complete after the last BPTT), [split, end) = the Linear, the speaker
+        embedding and ADDJUST (complete before the first BPTT)."""
+        return 4 + self.offsets["mix.Linear.weight"][0]
 
     def named_parameters(self):
         return {name: self.view(name) for name, _ in self.specs}
@@ -127,6 +135,10 @@ class SepTrainer:
         self.rnn_precision = rnn_precision or precision
         self.lr, self.betas, self.eps = lr, betas, eps
         self.pg = process_group
+        from . import dp
+
+        # data parallel: the gradient is all-reduced with SUM and Adam applies 1 / world
+        self.world = dp.world(process_group) if process_group is not None else 1
         self.T = ops.n_frames(n_samples)
         self.F = net.F
         dev = net.device
@@ -220,6 +232,24 @@ class SepTrainer:
             raise ValueError(f"DL4SS_RNN_XW={xw}: expected 0, 1 or l0")
         self.xw = self.fast and xw != "0" and not self.split
         self.xw_kmax = 160 if xw == "l0" else 640
+        # data parallel, bf16 step: the gradient leaves in two buckets ("can
+        # overlap with BPTT of the lower layers").  The Linear / embedding / ADDJUST gradients are
+        # complete before the first BPTT (dW_lin then runs on its own, not in the grouped launch) and
+        # their all-reduce runs beside the BPTT chain; the recurrent layers' bucket follows the last
+        # BPTT.  DL4SS_DP_BUCKETS=0: one flat all-reduce after the step's backward.
+        self.buckets = (process_group is not None and self.fast and net.L <= 5
+                        and os.environ.get("DL4SS_DP_BUCKETS", "1") != "0")
+        self._works = []
+        # DL4SS_SIDE_DWLIN="grid,cfg,split[,one_per_cu]" (experiment knob): dW_lin leaves the grouped
+        # launch and runs on a side stream as a persistent grouped launch of `grid` workgroups, beside
+        # the BPTT chain, on the CUs above the recurrence's co-residency budget
+        side = os.environ.get("DL4SS_SIDE_DWLIN", "")
+        self.side = None
+        if side and self.fast and net.L <= 5 and not self.buckets:
+            v = [int(x) for x in side.split(",")]
+            self.side = (v[0], v[1], v[2], bool(v[3]) if len(v) > 3 else True)
+        self._side_stream = None
+        self._side_gemm = None
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
             p8 = lambda n: (n + 7) // 8 * 8
@@ -475,8 +505,9 @@ class SepTrainer:
         if os.environ.get("DL4SS_DW_SPLITS"):  # A/B knob: "lin,ih,hh"
             s_lin, s_ih, s_hh = (int(v) for v in os.environ["DL4SS_DW_SPLITS"].split(","))
         self.dw_splits = (s_lin, s_ih, s_hh)
-        probs = [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
-                      transA=True, transB=False, beta=1.0, splitk=s_lin)]
+        probs = [] if (self.buckets or self.side) else [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H],
+                                              out=net.view("mix.Linear.weight", g), transA=True, transB=False,
+                                              beta=1.0, splitk=s_lin)]
         # longest k-ranges first (dW_lin 63 k-tiles per workgroup, dW_ih 32, dW_hh 16): the short
         # ones fill the tail
         for l in range(net.L - 1, -1, -1):
@@ -492,29 +523,52 @@ class SepTrainer:
         self._dw_group = ops.GroupedGemm(probs, net.device)
         return self._dw_group
 
+    def _backward_fast_early(self):
+        """The bf16 backward up to the first BPTT: the Linear's input gradient dH (all the BPTT chain
+        waits on), its bias gradient, and -- ungrouped or data-parallel bucketed -- its weight
+        gradient."""
+        net, B, T, H = self.net, self.B, self.T, self.net.H
+        BT = B * T
+        FE = self.F * net.E
+        g = net.grad
+        dPreb = self.dPreb[:, :FE]
+        st = _lib.stream_ptr()
+        grouped = net.L <= 5  # <= 16 problems per grouped launch
+        # gemm_gl split-K factors, measured per shape at C2 (tools/gemm_gl_bench.py --sweep): dH
+        # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
+        # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
+        ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], splitk=self.dh_split, ws=self.gl_ws)
+        if (not grouped or self.buckets) and not self.side:  # (bitwise the grouped launch's dW_lin at the same split)
+            ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
+                             beta=1.0, splitk=2, ws=self.gl_ws)
+        _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+                  _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part), self.colsum_part.numel() * 4, st)
+        if self.side:
+            grid, cfg, split, one = self.side
+            if self._side_stream is None:
+                self._side_stream = torch.cuda.Stream(device=net.device)
+                self._side_gemm = ops.GroupedGemm(
+                    [dict(A=dPreb, B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g), transA=True,
+                          transB=False, beta=1.0, splitk=split)], net.device, grid=grid, cfg=cfg, one_per_cu=one)
+            side = self._side_stream
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                self._side_gemm.run()
+
     def _backward_fast(self):
+        """The bf16 backward from the first BPTT on: the BPTT / dX chain down the layers, the bias
+        reduce and the grouped weight-gradient launch."""
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         NGH = _ngate(net.cell) * H
-        FE = self.F * net.E
         g = net.grad
         cell = CELLS[net.cell]
-        dPreb = self.dPreb[:, :FE]
         st = _lib.stream_ptr()
         gru = self.dGhb_l is not None
         grouped = net.L <= 5  # <= 16 problems per grouped launch
         dwg = self._weight_grad_group() if grouped else None
         self.rnn_ws_all[1].zero_()  # every layer's BPTT hand-off workspace, one fill
-        # gemm_gl split-K factors, measured per shape at C2 (tools/gemm_gl_bench.py --sweep): dH
-        # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
-        # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
         dH = self.dH[0]
-        ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=dH, splitk=self.dh_split, ws=self.gl_ws)  # input gradient first
-        if not grouped:
-            ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
-                             beta=1.0, splitk=2, ws=self.gl_ws)
-        _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
-                  _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part), self.colsum_part.numel() * 4, st)
         hp8 = self.p8(H)
         ldgh = self.ngh_p8 if gru else NGH  # dW_hh operand: direction d at column d * ldgh
         for l in range(net.L - 1, -1, -1):
@@ -544,6 +598,8 @@ class SepTrainer:
                 dH = dH_next
         if self.defer_bias:
             self._bias_reduce()
+        if self.side:  # dW_lin's side stream joins before the grouped launch
+            torch.cuda.current_stream().wait_stream(self._side_stream)
         if grouped:
             dwg.run()
 
@@ -559,12 +615,17 @@ class SepTrainer:
         _lib.call("dl4ss_birnn_bias_reduce", CELLS[net.cell], self.B, net.H, *self._bias_args, _lib.stream_ptr())
 
     def backward(self):
+        self.backward_early()
+        self.backward_late()
+
+    def backward_early(self):
+        """The backward up to the first BPTT: the query / embedding / ADDJUST gradients and the
+        Linear's.  Every gradient of the data-parallel early bucket (the flat range from
+        SepNet.bucket_split on) is complete when this returns (in stream order)."""
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
-        NGH = _ngate(net.cell) * H
         g = net.grad
         st = _lib.stream_ptr()
-        cell = CELLS[net.cell]
         g.zero_()
         wadj = net.view("adj.layer.weight") if net.adjust else None
         _lib.call("dl4ss_query_bwd", _lib.ptr(self.dq), B, T, 2 * H, _lib.ptr(self.spk),
@@ -573,8 +634,7 @@ class SepTrainer:
                   _lib.ptr(net.view("adj.layer.weight", g)) if net.adjust else None,
                   _lib.ptr(self.dh_bcast) if net.adjust else None, st)
         if self.fast:
-            self._backward_fast()
-            self._status_flag()
+            self._backward_fast_early()
             return
         dPre = self.V
         hL = self.out[-1].view(BT, 2 * H)
@@ -582,8 +642,21 @@ class SepTrainer:
         ops.gemm(dPre, hL, transA=True, out=net.view("mix.Linear.weight", g), beta=1.0, splitk="auto",
                  precision=self.precision)
         ops.colsum(dPre, net.view("mix.Linear.bias", g))
+        ops.gemm(dPre, net.view("mix.Linear.weight"), out=self.dH[0], splitk="auto", precision=self.precision)
+
+    def backward_late(self):
+        """The BPTT chain and the recurrent layers' weight / bias gradients, then the status flag."""
+        net, B, T, H = self.net, self.B, self.T, self.net.H
+        BT = B * T
+        NGH = _ngate(net.cell) * H
+        g = net.grad
+        st = _lib.stream_ptr()
+        cell = CELLS[net.cell]
+        if self.fast:
+            self._backward_fast()
+            self._status_flag()
+            return
         dH = self.dH[0]
-        ops.gemm(dPre, net.view("mix.Linear.weight"), out=dH, splitk="auto", precision=self.precision)
         for l in range(net.L - 1, -1, -1):
             dG = self.G
             dGh = self.dGh if self.dGh is not None else dG
@@ -617,26 +690,50 @@ class SepTrainer:
             _lib.call("dl4ss_status_flag", _lib.ptr(self.status), _lib.ptr(self.net.dp_flag), _lib.stream_ptr())
 
     def allreduce(self):
-        """One RCCL all-reduce of the flat gradient buffer (mean over ranks).  The slot behind
-        the gradient carries this rank's hand-off status flag (dl4ss_status_flag, written at the
-        end of backward()): after the mean it is non-zero on every rank iff a hand-off timed out
-        on any rank, and the guarded Adam reads it (a timed-out rank's incomplete
-        gradient must not reach the healthy ranks' weights either)."""
+        """The RCCL all-reduce (SUM) of the whole flat gradient; Adam applies the 1 / world of the
+        mean (no separate pass over the buffer).  The slot in front of the gradient carries this
+        rank's hand-off status flag (dl4ss_status_flag, written at the end of backward()): after
+        the sum it is non-zero on every rank iff a hand-off timed out on any rank, and the guarded
+        Adam reads it (a timed-out rank's incomplete gradient must not reach the healthy
+        ranks' weights either).  Bucketed steps (self.buckets) use allreduce_early / _late."""
         if self.pg is None:
             return
         from . import dp
 
-        dp.allreduce_mean_(self.net.grad_ext, self.pg)
+        self._works.append(dp.allreduce_sum_async(self.net.grad_ext, self.pg))
+
+    def allreduce_early(self):
+        """Start the SUM all-reduce of the early bucket (Linear, embedding, ADDJUST gradients):
+        asynchronous, on the process group's stream after the work enqueued so far, beside the
+        BPTT chain that follows."""
+        from . import dp
+
+        self._works.append(dp.allreduce_sum_async(self.net.grad_ext[self.net.bucket_split():], self.pg))
+
+    def allreduce_late(self):
+        """Start the SUM all-reduce of the late bucket (the status flag and every recurrent layer)."""
+        from . import dp
+
+        self._works.append(dp.allreduce_sum_async(self.net.grad_ext[:self.net.bucket_split()], self.pg))
+
+    def _wait_allreduce(self):
+        """The current stream waits for every all-reduce started this step (before Adam)."""
+        for w in self._works:
+            if w is not None:
+                w.wait()
+        self._works = []
 
     def optimizer_step(self):
         """Adam on device; refused (parameters untouched, loss[0] = NaN) when a recurrence
         hand-off of this step timed out on this rank or (data parallel) on any rank -- a
         timed-out step never reaches the weights.  A refused step is counted on device
         (status[1]); check() takes the refused steps back out of step_count, so the bias
-        corrections follow the updates actually applied, as torch.optim.Adam's do."""
+        corrections follow the updates actually applied, as torch.optim.Adam's do.  Data
+        parallel: the gradient is the SUM over ranks, scaled by 1 / world inside the update."""
+        self._wait_allreduce()
         self.step_count += 1
         ops.adam_(self.net.flat, self.net.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps,
-                  status=self.status, loss=self.loss, dp_flag=self.net.dp_flag)
+                  status=self.status, loss=self.loss, dp_flag=self.net.dp_flag, gscale=1.0 / self.world)
 
     def step(self, raw, gains, spk_idx):
         """One full training step on device-resident inputs; returns the loss tensor (not synced)."""
@@ -644,8 +741,14 @@ class SepTrainer:
         self.features(raw, gains)
         self.forward()
         loss = self.loss_and_grad()
-        self.backward()
-        self.allreduce()
+        if self.buckets:
+            self.backward_early()
+            self.allreduce_early()
+            self.backward_late()
+            self.allreduce_late()
+        else:
+            self.backward()
+            self.allreduce()
         self.optimizer_step()
         return loss
 
@@ -669,12 +772,14 @@ class SepTrainer:
         kernels, gemm_gl GEMMs, attention, small kernels) as one HIP graph, replayed by
         step_graph().  The mixing kernel (its input pointer changes per batch), the RCCL
         all-reduce and Adam (its bias correction is a per-step host scalar) stay eager launches
-        around the replay.  Call after at least one eager step(), so every workspace exists
-        before the capture."""
+        around the replay.  Bucketed data parallel: two graphs, split where the early bucket's
+        all-reduce starts (after backward_early).  Call after at least one eager step(), so every
+        workspace exists before the capture."""
         import gc
 
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        g2 = torch.cuda.CUDAGraph() if self.buckets else None
         # no garbage collection while the stream is being captured: a collection that frees another
         # object's device memory mid-capture aborted the process (round 4, a dropped trainer's buffers)
         gc.collect()
@@ -683,22 +788,34 @@ class SepTrainer:
         try:
             with torch.cuda.graph(g):
                 self._graph_loss = self._graph_body()
-                self.backward()
+                if g2 is None:
+                    self.backward()
+                else:
+                    self.backward_early()
+            if g2 is not None:
+                with torch.cuda.graph(g2, pool=g.pool()):
+                    self.backward_late()
         finally:
             if was_enabled:
                 gc.enable()
         torch.cuda.synchronize()
-        self.graph = g
+        self.graph, self.graph_late = g, g2
         return g
 
     def step_graph(self, raw, gains, spk_idx):
-        """step() with the captured graph: mixing, graph replay, all-reduce, Adam."""
+        """step() with the captured graph: mixing, graph replay, all-reduce, Adam (bucketed: the
+        early bucket's all-reduce between the two replays)."""
         if getattr(self, "graph", None) is None:
             self.capture()
         self.spk.copy_(spk_idx)
         ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
         self.graph.replay()
-        self.allreduce()
+        if self.graph_late is not None:
+            self.allreduce_early()
+            self.graph_late.replay()
+            self.allreduce_late()
+        else:
+            self.allreduce()
         self.optimizer_step()
         return self._graph_loss
 

@@ -216,8 +216,12 @@ class GroupedGemm:
     optionally M, N, K (else from the shapes).  The argument arrays are built once: the tensors
     must stay alive (and at the same addresses) for as long as run() is called."""
 
-    def __init__(self, problems, device):
+    def __init__(self, problems, device, grid=0, cfg=1, one_per_cu=False):
+        """grid > 0: the persistent form (dl4ss_gemm_bf16_gl_grouped_ex): ``grid`` workgroups walk the
+        tiles, in tile configuration ``cfg`` (1: 128 x 128, 2: 256 x 128 one per CU); one_per_cu pads
+        cfg 1 to one workgroup per CU."""
         import ctypes
+        self.grid, self.cfg, self.one_per_cu = int(grid), int(cfg), int(bool(one_per_cu))
         if not 1 <= len(problems) <= 16:
             raise RuntimeError("GroupedGemm: 1..16 problems")
         ta, tb = int(problems[0]["transA"]), int(problems[0]["transB"])
@@ -284,6 +288,11 @@ class GroupedGemm:
             c.mul_(beta)
         if self.n == 0:
             return
+        if self.grid > 0 or self.cfg != 1:
+            _lib.call("dl4ss_gemm_bf16_gl_grouped_ex", self.n, self.ta, self.tb, self.M, self.N, self.K, self.A, self.lda,
+                      self.B, self.ldb, self.C, self.ldc, self.beta, self.splitk, _lib.ptr(self.ws), self.ws.numel(),
+                      self.grid, self.cfg, self.one_per_cu, _lib.stream_ptr())
+            return
         _lib.call("dl4ss_gemm_bf16_gl_grouped", self.n, self.ta, self.tb, self.M, self.N, self.K, self.A, self.lda,
                   self.B, self.ldb, self.C, self.ldc, self.beta, self.splitk, _lib.ptr(self.ws), self.ws.numel(),
                   _lib.stream_ptr())
@@ -307,19 +316,20 @@ def colsum(A, out):
     return out
 
 
-def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, loss=None, dp_flag=None):
+def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, loss=None, dp_flag=None, gscale=1.0):
     """torch Adam step on flat buffers; with ``status`` (the recurrence hand-off status word,
     2 ints: {timed out, refused-update count}) the update is refused on device when a hand-off
     of this step timed out, loss[0] is set to NaN and status[1] counts the refusal
     (dl4ss_adam_guarded_dp's 2-int status form); with ``dp_flag`` (the all-reduced status flag
-    behind the flat gradient) also when a data-parallel peer's hand-off timed out."""
+    behind the flat gradient) also when a data-parallel peer's hand-off timed out.  ``gscale``: the
+    update uses g * gscale (1 / world_size on a SUM-reduced gradient; 1 is bitwise the unscaled step)."""
     for t in (p, g, m, v):
         _f32c(t, "adam")
     if status is not None and status.numel() < 2:
         raise ValueError("adam_: the status word needs 2 ints (timed out, refused-update count)")
-    _lib.call("dl4ss_adam_guarded_dp", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(), float(lr),
-              float(betas[0]), float(betas[1]), float(eps), int(step), _lib.ptr(status), _lib.ptr(dp_flag),
-              _lib.ptr(loss), _lib.stream_ptr())
+    _lib.call("dl4ss_adam_guarded_dp_scaled", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(),
+              float(lr), float(betas[0]), float(betas[1]), float(eps), int(step), _lib.ptr(status), _lib.ptr(dp_flag),
+              float(gscale), _lib.ptr(loss), _lib.stream_ptr())
 
 
 def birnn_plan(cell, B, H, precision="bf16", max_wg=0):

@@ -112,6 +112,15 @@ int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const int* M, cons
                                const void* const* A, const long long* lda, const void* const* B, const long long* ldb,
                                float* const* C, const long long* ldc, const float* beta, const int* splitk, void* ws,
                                long long ws_bytes, void* stream);
+/* The grouped launch in its persistent form: `grid` workgroups walk the tiles (grid <= 0: one per
+ * tile); cfg 1 = 128 x 128 double buffer, 2 = 256 x 128 three stages (one workgroup per CU);
+ * one_per_cu pads cfg 1's LDS to one workgroup per CU.  For a side stream on the CUs the persistent
+ * recurrence leaves free (its co-residency budget, dl4ss_birnn_plan_info). */
+int dl4ss_gemm_bf16_gl_grouped_ex(int n, int transA, int transB, const int* M, const int* N, const int* K,
+                                  const void* const* A, const long long* lda, const void* const* B,
+                                  const long long* ldb, float* const* C, const long long* ldc, const float* beta,
+                                  const int* splitk, void* ws, long long ws_bytes, int grid, int cfg, int one_per_cu,
+                                  void* stream);
 /* Split-precision operand image: x = hi + lo (hi = bf16(x), lo = bf16(x - hi)); segment s of each
  * row of y (width segw >= cols, zero-padded; s < nseg <= 8) holds hi, or lo when bit s of pattern
  * is set; zeros up to ldy.  [x_hi | x_lo | x_hi] against weights [w_hi | w_hi | w_lo] makes one bf16
@@ -289,7 +298,13 @@ int dl4ss_adam_guarded(float* p, const float* g, float* m, float* v, long long n
 int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                           float beta2, float eps, int step, int* status, const float* dp_flag, float* loss,
                           void* stream);
-/* flag[0] = status[0] != 0 ? 1 : 0 (one float, written behind the flat gradient before its all-reduce). */
+/* dl4ss_adam_guarded_dp on g * gscale: the data-parallel step takes the gradient all-reduced with
+ * SUM and applies the 1 / world_size of the mean here (no separate pass over the buffer; gscale =
+ * 1 is bitwise the unscaled step).  Replaces optimizer.step() at EvalVer.py:673-675 under DP. */
+int dl4ss_adam_guarded_dp_scaled(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
+                                 float beta2, float eps, int step, int* status, const float* dp_flag, float gscale,
+                                 float* loss, void* stream);
+/* flag[0] = status[0] != 0 ? 1 : 0 (one float, written in front of the flat gradient before its all-reduce). */
 int dl4ss_status_flag(const int* status, float* flag, void* stream);
 
 /* ---- kernels behind the reference-API nn.Modules (dl4ss_amd/compat/myNet.py) ---- */

@@ -141,3 +141,45 @@ def test_dp_status_flag_reaches_every_rank():
         assert g0 == g1 == g2 == 2.0  # the gradient mean is unaffected by the flag slot
         assert f0 == 0.0  # clean step: every rank's guarded Adam applies it
         assert f1 > 0.0 and f2 > 0.0  # a timeout on any one rank: every rank refuses the step
+
+
+def _bucket_worker(rank, world, port, out):
+    """The bucketed all-reduce of the trainer's extended gradient [flag | layers | Linear, emb, adj]
+    (SepTrainer.allreduce_early / allreduce_late: two async SUMs split at SepNet.bucket_split) against
+    one flat SUM (SepTrainer.allreduce), on the layout of the C2 net."""
+    from dl4ss_amd import engine
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    net = engine.SepNet(cell="lstm", num_layers=4, device="cpu")
+    g = torch.Generator().manual_seed(100 + rank)
+    ext = torch.randn(net.grad_ext.numel(), generator=g) * (1 + rank)
+    ext[0] = 1.0 if rank == 1 else 0.0  # rank 1's hand-off timed out (dl4ss_status_flag)
+    flat = ext.clone()
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    buck = dp.allreduce_buckets_(ext.clone(), net.bucket_split())
+    mean = dp.allreduce_mean_(ext.clone())
+    out[rank] = (flat, buck, mean)
+    dist.destroy_process_group()
+
+
+def test_dp_bucketed_allreduce_equals_flat():
+    from dl4ss_amd import engine
+
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    net = engine.SepNet(cell="lstm", num_layers=4, device="cpu")
+    split = net.bucket_split()
+    # the buckets are the contiguous ranges the backward completes at different times
+    early = {n for n, (off, _) in net.offsets.items() if off + 4 >= split}
+    assert early == {"mix.Linear.weight", "mix.Linear.bias", "emb.layer.weight", "adj.layer.weight"}
+    assert net.dp_flag.data_ptr() == net.grad_ext.data_ptr()  # the flag travels with the late bucket
+    for r in range(world):
+        flat, buck, mean = out[r]
+        assert torch.equal(flat, buck)  # bitwise: the same elementwise sums
+        assert torch.equal(flat, out[0][0])  # every rank holds the same sums
+        assert flat[0] == 1.0  # one rank's timeout reaches every rank through the late bucket
+        # Adam's 1 / world scale on the SUM (dl4ss_adam_guarded_dp_scaled) is the mean's arithmetic
+        assert torch.equal(flat[4:] * (1.0 / world), mean[4:])

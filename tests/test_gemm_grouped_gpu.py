@@ -114,3 +114,24 @@ def test_grouped_empty_problems_are_no_ops(dev):
     assert (out.double().cpu() - ref).abs().max() <= 1e-5 * ref.abs().max()
     assert bool((c_k0 == 0.5).all()) and bool((c_k0b == 1.0).all())
     ops.GroupedGemm([probs[1]], dev).run()  # nothing left to launch
+
+
+@pytest.mark.parametrize("grid,cfg,one", [(16, 1, True), (7, 1, False), (16, 2, False)])
+def test_grouped_persistent_form_matches(dev, grid, cfg, one):
+    """dl4ss_gemm_bf16_gl_grouped_ex: `grid` workgroups walk the tiles (the side-stream form beside
+    the recurrence).  Each tile's k-loop and epilogue are the one-tile-per-workgroup launch's, so the
+    128 x 128 form is bitwise the grouped launch; the 256 x 128 three-stage tiles sum every output in
+    the same k order, bitwise too."""
+    g = torch.Generator().manual_seed(11)
+    probs, probs_p = [], []
+    for (M, N, K, sk) in [(900, 300, 1000, 3), (130, 257, 700, 1), (2400, 600, 1024, 1), (17, 9, 130, 5)]:
+        A = _bf(g, dev, K, (M + 7) // 8 * 8)[:, :M]
+        B = _bf(g, dev, K, (N + 7) // 8 * 8)[:, :N]
+        C0 = torch.randn(M, N, generator=g).to(dev)
+        probs.append(dict(A=A, B=B, out=C0.clone(), transA=True, transB=False, beta=1.0, splitk=sk))
+        probs_p.append(dict(A=A, B=B, out=C0.clone(), transA=True, transB=False, beta=1.0, splitk=sk))
+    ops.GroupedGemm(probs, dev).run()
+    ops.GroupedGemm(probs_p, dev, grid=grid, cfg=cfg, one_per_cu=one).run()
+    torch.cuda.synchronize()
+    for p, q in zip(probs, probs_p):
+        assert torch.equal(p["out"], q["out"])

@@ -121,7 +121,9 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5", "c5x32"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16", "bf16s"])
+    ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16", "bf16s", "mixed"],
+                    help="c1/c3/c4: fp32, bf16, bf16s; c5: fp32, bf16, mixed (infer.RecursiveExtractor)")
+    ap.add_argument("--c5-precision", default=None, help="precision of the c5 configs (default: --precision)")
     ap.add_argument("--rnn-precision", default=None, choices=["fp32", "bf16"],
                     help="recurrent matvec precision (default: --precision)")
     a = ap.parse_args()
@@ -139,9 +141,9 @@ def main():
             r = train_config("C4: 3-spk mixed SNR BiGRU-2L (no ADDJUST), B=32, N=32000", "gru", 2, 32, 3, 32000,
                              "label", a.precision, a.steps, a.warmup, adjust=False, **rp)
         elif c == "c5":  # the reference's replica: one mixture at a time
-            r = recursive_config(a.precision, a.steps, a.warmup)
+            r = recursive_config(a.c5_precision or a.precision, a.steps, a.warmup)
         elif c == "c5x32":  # 32 independent extractions (rows) per launch: the same latency-bound chain
-            r = recursive_config(a.precision, a.steps, a.warmup, B=32)
+            r = recursive_config(a.c5_precision or a.precision, a.steps, a.warmup, B=32)
         else:
             raise SystemExit(f"unknown config {c}")
         print(json.dumps(r), flush=True)

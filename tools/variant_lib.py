@@ -13,11 +13,19 @@ from dl4ss_amd import build as B  # noqa: E402
 
 
 def main(tag, defs):
+    """--minimal: recompile only birnn.hip, with -DRNN_EXP_MINIMAL (the packed BC = 4 kernels of the
+    C2 / C4 step at B = 32 only), and link it with the shipped build's other objects (python -m
+    dl4ss_amd.build first): a recurrence variant in well under a minute."""
     od = f"/tmp/variant_obj_{tag}"
     os.makedirs(od, exist_ok=True)
     srcs = sorted(f for f in os.listdir(B.CSRC) if f.endswith(".hip"))
+    minimal = "--minimal" in defs
+    if minimal:
+        defs = [d for d in defs if d != "--minimal"] + ["-DRNN_EXP_MINIMAL"]
 
     def comp(f):
+        if minimal and f != "birnn.hip":
+            return os.path.join(B.OBJ, f[:-4] + ".o")
         o = f"{od}/{f[:-4]}.o"
         subprocess.run([B.HIPCC, *B.FLAGS, *B.FILE_FLAGS.get(f, []), *defs, "-I", B.CSRC, "-c",
                         os.path.join(B.CSRC, f), "-o", o], check=True)
