@@ -37,7 +37,7 @@ SIGNATURES = {
     "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
     "dl4ss_gemm_bf16_gl_grouped_ws_bytes": [I, P, P, P, P],
     "dl4ss_gemm_bf16_gl_grouped": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P],
-    "dl4ss_gemm_bf16_gl_grouped_ex": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, I, I, I, P],
+    "dl4ss_gemm_bf16_gl_grouped_ex": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, I, I, I, P, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_fwd_xw": [I, I, I, I, P, I, LL, P, LL, P, P, P, P, P, P, P, P, P, P, LL, P, P, I],
     "dl4ss_birnn_fwd_xw_supported": [I, I, I, I, I],

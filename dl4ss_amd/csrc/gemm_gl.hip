@@ -128,15 +128,25 @@ __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int k
 // One BM x 128 output tile of C (or of split-K slab `slab`, SPLIT) over k in [kbeg, kbeg + kspan):
 // the k-loop and the epilogue of gemm_gl_kernel and gemm_gl_grouped_kernel.  smem: the kernel's
 // one LDS array (CF::STG * CF::STAGE bf16).
-template <bool A_KC, bool B_KC, int EPI, bool SPLIT, class CF>
+// RS (row sums, the grouped side-stream dW_lin): the tiles of column block 0 also form
+// rsum[m] = beta rsum[m] + sum_k A(m, k) -- the Linear's bias gradient, sum over rows of dPre, off the
+// same A fragments: the waves of columns 0..63 run one more MFMA per A fragment against an all-ones B
+// (bf16 products exact, fp32 accumulation, fixed k order).
+template <bool A_KC, bool B_KC, int EPI, bool SPLIT, class CF, bool RS = false>
 __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, const unsigned short* __restrict__ A,
                                         long long lda, const unsigned short* __restrict__ B, long long ldb,
                                         float* __restrict__ C, long long ldc, const float* __restrict__ bias,
-                                        float beta, int m0, int n0, int kbeg, int kspan, float* __restrict__ slab) {
+                                        float beta, int m0, int n0, int kbeg, int kspan, float* __restrict__ slab,
+                                        float* __restrict__ rsum = nullptr) {
   constexpr int STG = CF::STG, IMG_A = CF::IMG_A, STAGE = CF::STAGE;
   const int nk = (kspan + BK - 1) / BK;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const bool rs = RS && rsum != nullptr && n0 == 0 && wn == 0;  // wave-uniform
+  f32x4 accr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
 
   Stager<A_KC, CF::CPW_A> sa_;
   Stager<B_KC, CF::CPW_B> sb_;
@@ -163,6 +173,12 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if constexpr (RS) {
+        if (rs) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) accr[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accr[i], 0, 0, 0);
+        }
+      }
 #else
 #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" :: "v"(af[i]), "v"(bfr[i]));
@@ -203,6 +219,18 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
     __syncthreads();  // every wave is done with the stages before the epilogue reuses LDS
   }
 
+  if constexpr (RS) {
+    // accr[i][e] = rsum of row wm + 16 i + 4 (lane >> 4) + e in every column; column 0's lanes store
+    if (rs && (lane & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
+          if (row < M) rsum[row] = beta != 0.0f ? accr[i][e] + beta * rsum[row] : accr[i][e];
+        }
+    }
+  }
   // epilogue: acc[i][j][e] = C(wm + 16 i + 4 (lane >> 4) + e, wn + 16 j + (lane & 15)).  Each
   // wave stages 32 rows (i = 2h, 2h + 1) of its 64 x 64 sub-tile at a time in LDS (free
   // after the last barrier; 32 x 68 fp32 per wave) and writes rows back as 16-B stores.
@@ -647,22 +675,17 @@ struct GlProb {
   int wg0;  // first workgroup (in the XCD-remapped order) of this problem
   int u0;   // first reduce unit (gemm_gl_grouped_reduce_kernel)
   int vec;  // reduce with 16-B accesses (N % 4 == 0, ldc % 4 == 0, C 16-B aligned)
+  float* rsum;  // row sums of op(A) (+= beta rsum), formed by column block 0 (unsplit problems, RS kernels)
 };
 struct GlGroup {
   int n, total_wg, total_units;
   GlProb p[GMAXP];
 };
 
-template <bool A_KC, bool B_KC, class CF>
-__device__ __forceinline__ void grouped_tile(const GlGroup& g, int L, unsigned short* smem) {
-  int pi = 0;
-#pragma unroll
-  for (int k = 1; k < GMAXP; ++k)
-    if (k < g.n && L >= g.p[k].wg0) pi = k;
-  GlProb p = g.p[0];
-#pragma unroll
-  for (int k = 1; k < GMAXP; ++k)
-    if (k == pi) p = g.p[k];
+// tile L (dispatch order) of the group: p is its problem (selected by the kernel from the kernel
+// argument with compile-time indices: a reference to the argument struct put it in scratch)
+template <bool A_KC, bool B_KC, class CF, bool RS>
+__device__ __forceinline__ void grouped_tile(const GlProb p, int L, unsigned short* smem) {
   const int ntot = p.gm * p.gn * p.nsplit;
   const int Ll = L - p.wg0;
   const int xcd = Ll % 8, q8 = ntot / 8, r8 = ntot % 8;
@@ -683,11 +706,11 @@ __device__ __forceinline__ void grouped_tile(const GlGroup& g, int L, unsigned s
     gl_tile<A_KC, B_KC, EPI_NONE, true, CF>(smem, p.M, p.N, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, nullptr, 0.0f, m0, n0,
                                             kbeg, kend - kbeg, p.part + (long long)zsplit * p.M * p.N);
   else
-    gl_tile<A_KC, B_KC, EPI_NONE, false, CF>(smem, p.M, p.N, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, nullptr, p.beta, m0,
-                                             n0, kbeg, kend - kbeg, nullptr);
+    gl_tile<A_KC, B_KC, EPI_NONE, false, CF, RS>(smem, p.M, p.N, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, nullptr, p.beta,
+                                                 m0, n0, kbeg, kend - kbeg, nullptr, p.rsum);
 }
 
-template <bool A_KC, bool B_KC, class CF>
+template <bool A_KC, bool B_KC, class CF, bool RS = false>
 __global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) void gemm_gl_grouped_kernel(GlGroup g) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
   // problems by DISPATCH order (so every problem's workgroups are dealt over all 8 XCDs: an
@@ -698,7 +721,15 @@ __global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) vo
   // gridDim.x.
   for (int L = blockIdx.x; L < g.total_wg; L += gridDim.x) {
     if (L != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue is done with the LDS
-    grouped_tile<A_KC, B_KC, CF>(g, L, smem);
+    int pi = 0;
+#pragma unroll
+    for (int k = 1; k < GMAXP; ++k)
+      if (k < g.n && L >= g.p[k].wg0) pi = k;
+    GlProb p = g.p[0];
+#pragma unroll
+    for (int k = 1; k < GMAXP; ++k)
+      if (k == pi) p = g.p[k];
+    grouped_tile<A_KC, B_KC, CF, RS>(p, L, smem);
   }
 }
 
@@ -935,8 +966,9 @@ template <class CF>
 int grouped_launch(int n, bool a_kc, bool b_kc, const int* M, const int* N, const int* K, const void* const* A,
                    const long long* lda, const void* const* B, const long long* ldb, float* const* C,
                    const long long* ldc, const float* beta, const int* splitk, void* ws, long long ws_bytes, int grid,
-                   size_t dyn_lds, hipStream_t st) {
+                   size_t dyn_lds, float* const* rsum, hipStream_t st) {
   GlGroup g{};
+  bool any_rs = false;
   long long off = 0;
   int wg = 0, units = 0;
   char* w = reinterpret_cast<char*>(ws);
@@ -967,6 +999,9 @@ int grouped_launch(int n, bool a_kc, bool b_kc, const int* M, const int* N, cons
     wg += p.gm * p.gn * sk;
     p.part = nullptr;
     p.vec = (N[i] % 4 == 0 && ldc[i] % 4 == 0 && ((uintptr_t)C[i] & 15) == 0) ? 1 : 0;
+    p.rsum = rsum ? rsum[i] : nullptr;
+    DL4SS_REQUIRE(!p.rsum || sk == 1);  // row sums are formed by unsplit tiles only
+    any_rs = any_rs || p.rsum != nullptr;
     p.u0 = units;
     if (sk > 1) {
       const long long b = (long long)sk * M[i] * N[i] * 4;
@@ -983,7 +1018,10 @@ int grouped_launch(int n, bool a_kc, bool b_kc, const int* M, const int* N, cons
   const int nwg = grid > 0 && grid < wg ? grid : wg;
 #define GGR(AK, BKC) \
   hipLaunchKernelGGL((gemm_gl_grouped_kernel<AK, BKC, CF>), dim3(nwg), dim3(CF::NT), dyn_lds, st, g)
-  if (a_kc && b_kc) GGR(true, true);
+  if (any_rs) {  // the side-stream dW_lin: A k-major (dPre^T), B k-major (h)
+    DL4SS_REQUIRE(!a_kc && !b_kc);
+    hipLaunchKernelGGL((gemm_gl_grouped_kernel<false, false, CF, true>), dim3(nwg), dim3(CF::NT), dyn_lds, st, g);
+  } else if (a_kc && b_kc) GGR(true, true);
   else if (a_kc) GGR(true, false);
   else if (b_kc) GGR(false, true);
   else GGR(false, false);
@@ -1008,26 +1046,28 @@ DL4SS_API int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const in
                                          void* stream) {
   DL4SS_REQUIRE(n >= 1 && n <= GMAXP && M && N && K && A && lda && B && ldb && C && ldc && beta && splitk);
   return grouped_launch<C128>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes, 0, 0,
-                              as_stream(stream));
+                              nullptr, as_stream(stream));
 }
 
 // The persistent form: `grid` workgroups walk the group's tiles (grid <= 0: one per tile, as
 // dl4ss_gemm_bf16_gl_grouped), in tile configuration cfg (1 = 128 x 128 double buffer; 2 = 256 x
 // 128, three stages, 144 KB LDS: one workgroup per CU); one_per_cu pads cfg 1's LDS so that one
-// workgroup fills a CU.  For a side stream beside the persistent recurrence, which leaves the CUs
+// workgroup fills a CU.  rowsum (NULL, or n pointers, each NULL or M_i floats): rowsum_i[m] =
+// beta_i rowsum_i[m] + sum_k op(A_i)(m, k) for unsplit problems with both operands k-major (the
+// Linear's bias gradient beside its weight gradient).  For a side stream beside the persistent recurrence, which leaves the CUs
 // above its co-residency budget free (dl4ss_birnn_plan_info).
 DL4SS_API int dl4ss_gemm_bf16_gl_grouped_ex(int n, int transA, int transB, const int* M, const int* N, const int* K,
                                             const void* const* A, const long long* lda, const void* const* B,
                                             const long long* ldb, float* const* C, const long long* ldc,
                                             const float* beta, const int* splitk, void* ws, long long ws_bytes,
-                                            int grid, int cfg, int one_per_cu, void* stream) {
+                                            int grid, int cfg, int one_per_cu, float* const* rowsum, void* stream) {
   DL4SS_REQUIRE(n >= 1 && n <= GMAXP && M && N && K && A && lda && B && ldb && C && ldc && beta && splitk);
   DL4SS_REQUIRE(cfg == 1 || cfg == 2);
   hipStream_t st = as_stream(stream);
   if (cfg == 2)
     return grouped_launch<C256>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes, grid,
-                                0, st);
+                                0, rowsum, st);
   // C128 holds 64 KB: 20 KB more dynamic LDS leaves room for only one workgroup per CU
   return grouped_launch<C128>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes, grid,
-                              one_per_cu ? 20 * 1024 : 0, st);
+                              one_per_cu ? 20 * 1024 : 0, rowsum, st);
 }

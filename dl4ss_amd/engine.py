@@ -240,16 +240,30 @@ class SepTrainer:
         self.buckets = (process_group is not None and self.fast and net.L <= 5
                         and os.environ.get("DL4SS_DP_BUCKETS", "1") != "0")
         self._works = []
-        # DL4SS_SIDE_DWLIN="grid,cfg,split[,one_per_cu]" (experiment knob): dW_lin leaves the grouped
-        # launch and runs on a side stream as a persistent grouped launch of `grid` workgroups, beside
-        # the BPTT chain, on the CUs above the recurrence's co-residency budget
-        side = os.environ.get("DL4SS_SIDE_DWLIN", "")
+        # The Linear's weight and bias gradients on a SIDE STREAM beside the BPTT chain (round 5): the
+        # persistent recurrence keeps its grid within the CUs minus 1/16 (dl4ss_birnn_plan_info), so
+        # `free` CUs idle through the chain.  dW_lin (and the bias gradient as the row sums of the same
+        # dPre fragments, dl4ss_gemm_bf16_gl_grouped_ex rowsum) runs there as a persistent launch of one
+        # 256 x 128 three-stage workgroup per free CU, from the end of the dH GEMM to the grouped
+        # launch, which it joins.  C2 (rocprofv3 r05e): the side launch takes 1.41 ms of the 1.78 ms
+        # chain, the BPTTs are unchanged (406 / 399 / 396 / 397 vs 408 / 398 / 398 / 398 us), and the
+        # grouped launch + combine go 336 -> 230 us.  On by a cost model (the side launch must fit in
+        # the chain: dW_lin's FLOPs at ~2.75 TFLOP/s per free CU vs ~1.75 us per dependent step and
+        # layer); DL4SS_SIDE_DWLIN = "0" off, "1" on, or "grid,cfg,split[,one_per_cu]" to force a shape.
         self.side = None
-        if side and self.fast and net.L <= 5 and not self.buckets:
-            v = [int(x) for x in side.split(",")]
-            self.side = (v[0], v[1], v[2], bool(v[3]) if len(v) > 3 else True)
         self._side_stream = None
         self._side_gemm = None
+        side = os.environ.get("DL4SS_SIDE_DWLIN", "")
+        if self.fast and net.L <= 5 and not self.buckets and side != "0" and dev.type == "cuda":
+            if side and side != "1":
+                v = [int(x) for x in side.split(",")]
+                self.side = (v[0], v[1], v[2], bool(v[3]) if len(v) > 3 else True)
+            else:
+                plan = ops.birnn_plan(net.cell, B, H)
+                free = torch.cuda.get_device_properties(dev).multi_processor_count - (plan["grid"] if plan else 1 << 30)
+                flops = 2.0 * (F * net.E) * (2 * H) * BT
+                if free >= 8 and (flops / (free * 2.75e12) < net.L * T * 1.75e-6 * 0.85 or side == "1"):
+                    self.side = (free, 2, 1, False)
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
             p8 = lambda n: (n + 7) // 8 * 8
@@ -349,7 +363,7 @@ class SepTrainer:
         st = _lib.stream_ptr()
         cell = CELLS[net.cell]
         A_SPLIT, W_SPLIT = 0b010, 0b100  # [hi | lo | hi] and [hi | hi | lo]
-        self.rnn_ws_all[0].zero_()
+        self.rnn_ws_all.zero_()  # every layer's forward AND BPTT hand-off workspaces, one fill per step
         self._weights_to_bf16()
         for l in range(net.L):
             self._hilo(net.cat_view("weight_ih", l), self.ws_ih[l], self.seg[l], W_SPLIT)
@@ -373,7 +387,7 @@ class SepTrainer:
         BT = B * T
         st = _lib.stream_ptr()
         cell = CELLS[net.cell]
-        self.rnn_ws_all[0].zero_()  # every layer's forward hand-off workspace, one fill
+        self.rnn_ws_all.zero_()  # every layer's forward AND BPTT hand-off workspaces, one fill per step
         self._weights_to_bf16()
         self._to_bf16_rows(x, self.xb0)
         xb = self.xb0[:, :x.shape[1]]
@@ -541,15 +555,23 @@ class SepTrainer:
         if (not grouped or self.buckets) and not self.side:  # (bitwise the grouped launch's dW_lin at the same split)
             ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
                              beta=1.0, splitk=2, ws=self.gl_ws)
-        _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
-                  _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part), self.colsum_part.numel() * 4, st)
-        if self.side:
+        if not self.side:
+            _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+                      _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
+                      self.colsum_part.numel() * 4, st)
+        else:
             grid, cfg, split, one = self.side
             if self._side_stream is None:
                 self._side_stream = torch.cuda.Stream(device=net.device)
                 self._side_gemm = ops.GroupedGemm(
                     [dict(A=dPreb, B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g), transA=True,
-                          transB=False, beta=1.0, splitk=split)], net.device, grid=grid, cfg=cfg, one_per_cu=one)
+                          transB=False, beta=1.0, splitk=split,
+                          rowsum=net.view("mix.Linear.bias", g) if split == 1 else None)],
+                    net.device, grid=grid, cfg=cfg, one_per_cu=one)
+            if split != 1:
+                _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+                          _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
+                          self.colsum_part.numel() * 4, st)
             side = self._side_stream
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
@@ -567,7 +589,7 @@ class SepTrainer:
         gru = self.dGhb_l is not None
         grouped = net.L <= 5  # <= 16 problems per grouped launch
         dwg = self._weight_grad_group() if grouped else None
-        self.rnn_ws_all[1].zero_()  # every layer's BPTT hand-off workspace, one fill
+        # (the BPTT hand-off workspaces were zeroed with the forward's, in the step's one fill)
         dH = self.dH[0]
         hp8 = self.p8(H)
         ldgh = self.ngh_p8 if gru else NGH  # dW_hh operand: direction d at column d * ldgh

@@ -278,6 +278,16 @@ class GroupedGemm:
         self.ldc = Lv([p["out"].stride(0) for p in problems])
         self.beta = (ctypes.c_float * n)(*[float(p.get("beta", 0.0)) for p in problems])
         self.splitk = Iv([int(p.get("splitk", 1)) for p in problems])
+        # optional per-problem row sums of op(A) ("rowsum": an M-float view; persistent form only)
+        rs = [p.get("rowsum") for p in problems]
+        for r, (M, _, _), p in zip(rs, dims, problems):
+            if r is not None:
+                _f32c(r, "GroupedGemm(rowsum)")
+                if r.numel() < M or int(p.get("splitk", 1)) != 1 or not (p["transA"] and not p["transB"]):
+                    raise RuntimeError("GroupedGemm: rowsum needs M floats, an unsplit problem, transA and not transB")
+                self._keep.append(r)
+        self.rowsum = Pv([r.data_ptr() if r is not None else None for r in rs]) if any(r is not None for r in rs) \
+            else None
         nb = _lib.query("dl4ss_gemm_bf16_gl_grouped_ws_bytes", n, self.M, self.N, self.K, self.splitk)
         if nb < 0:
             raise RuntimeError("GroupedGemm: bad problem list")
@@ -288,10 +298,10 @@ class GroupedGemm:
             c.mul_(beta)
         if self.n == 0:
             return
-        if self.grid > 0 or self.cfg != 1:
+        if self.grid > 0 or self.cfg != 1 or self.rowsum is not None:
             _lib.call("dl4ss_gemm_bf16_gl_grouped_ex", self.n, self.ta, self.tb, self.M, self.N, self.K, self.A, self.lda,
                       self.B, self.ldb, self.C, self.ldc, self.beta, self.splitk, _lib.ptr(self.ws), self.ws.numel(),
-                      self.grid, self.cfg, self.one_per_cu, _lib.stream_ptr())
+                      self.grid, self.cfg, self.one_per_cu, self.rowsum, _lib.stream_ptr())
             return
         _lib.call("dl4ss_gemm_bf16_gl_grouped", self.n, self.ta, self.tb, self.M, self.N, self.K, self.A, self.lda,
                   self.B, self.ldb, self.C, self.ldc, self.beta, self.splitk, _lib.ptr(self.ws), self.ws.numel(),

@@ -115,12 +115,15 @@ int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const int* M, cons
 /* The grouped launch in its persistent form: `grid` workgroups walk the tiles (grid <= 0: one per
  * tile); cfg 1 = 128 x 128 double buffer, 2 = 256 x 128 three stages (one workgroup per CU);
  * one_per_cu pads cfg 1's LDS to one workgroup per CU.  For a side stream on the CUs the persistent
- * recurrence leaves free (its co-residency budget, dl4ss_birnn_plan_info). */
+ * recurrence leaves free (its co-residency budget, dl4ss_birnn_plan_info).  rowsum (NULL or n
+ * entries, each NULL or M_i floats): rowsum_i[m] = beta_i rowsum_i[m] + sum_k op(A_i)(m, k), for
+ * unsplit problems whose operands are both k-major (transA, !transB) -- the Linear's bias gradient
+ * sum_rows dPre (EvalVer.py:290, loss.backward() at :673) beside dW_lin. */
 int dl4ss_gemm_bf16_gl_grouped_ex(int n, int transA, int transB, const int* M, const int* N, const int* K,
                                   const void* const* A, const long long* lda, const void* const* B,
                                   const long long* ldb, float* const* C, const long long* ldc, const float* beta,
                                   const int* splitk, void* ws, long long ws_bytes, int grid, int cfg, int one_per_cu,
-                                  void* stream);
+                                  float* const* rowsum, void* stream);
 /* Split-precision operand image: x = hi + lo (hi = bf16(x), lo = bf16(x - hi)); segment s of each
  * row of y (width segw >= cols, zero-padded; s < nseg <= 8) holds hi, or lo when bit s of pattern
  * is set; zeros up to ldy.  [x_hi | x_lo | x_hi] against weights [w_hi | w_hi | w_lo] makes one bf16

@@ -135,3 +135,28 @@ def test_grouped_persistent_form_matches(dev, grid, cfg, one):
     torch.cuda.synchronize()
     for p, q in zip(probs, probs_p):
         assert torch.equal(p["out"], q["out"])
+
+
+@pytest.mark.parametrize("cfg", [2, 1])
+def test_grouped_rowsum_is_the_bias_gradient(dev, cfg):
+    """The side-stream dW_lin (engine.SepTrainer.side): the persistent grouped launch also forms
+    rowsum[m] = beta rowsum[m] + sum_k op(A)(m, k) -- the Linear's bias gradient, the column sums of
+    dPre -- from the tiles of column block 0.  Against fp64 (bf16 operands exact, fp32 sums), with
+    the weight gradient bitwise the launch without row sums; ragged M, N and K."""
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 6450 // 5 + 3, 600 // 4 + 6, 8032 // 8 + 5
+    A = _bf(g, dev, K, (M + 7) // 8 * 8)[:, :M]  # dPre (K rows of M) -> op(A) = A^T
+    B = _bf(g, dev, K, (N + 7) // 8 * 8)[:, :N]
+    r0 = torch.randn(M, generator=g).to(dev)
+    rs = r0.clone()
+    out = torch.zeros(M, N, device=dev)
+    out_ref = torch.zeros(M, N, device=dev)
+    ops.GroupedGemm([dict(A=A, B=B, out=out, transA=True, transB=False, beta=1.0, splitk=1, rowsum=rs)], dev,
+                    grid=16, cfg=cfg).run()
+    ops.GroupedGemm([dict(A=A, B=B, out=out_ref, transA=True, transB=False, beta=1.0, splitk=1)], dev,
+                    grid=16, cfg=cfg).run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_ref)
+    ref = r0.double().cpu() + A.double().cpu().sum(0)
+    mag = r0.double().cpu().abs() + A.double().cpu().abs().sum(0)
+    assert bool(((rs.double().cpu() - ref).abs() <= 2e-6 * mag).all())
