@@ -254,7 +254,7 @@ class SepTrainer:
         self._side_stream = None
         self._side_gemm = None
         side = os.environ.get("DL4SS_SIDE_DWLIN", "")
-        if self.fast and net.L <= 5 and not self.buckets and side != "0" and dev.type == "cuda":
+        if self.fast and net.L <= 5 and side != "0" and dev.type == "cuda":
             if side and side != "1":
                 v = [int(x) for x in side.split(",")]
                 self.side = (v[0], v[1], v[2], bool(v[3]) if len(v) > 3 else True)
@@ -560,22 +560,34 @@ class SepTrainer:
                       _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
                       self.colsum_part.numel() * 4, st)
         else:
-            grid, cfg, split, one = self.side
-            if self._side_stream is None:
-                self._side_stream = torch.cuda.Stream(device=net.device)
-                self._side_gemm = ops.GroupedGemm(
-                    [dict(A=dPreb, B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g), transA=True,
-                          transB=False, beta=1.0, splitk=split,
-                          rowsum=net.view("mix.Linear.bias", g) if split == 1 else None)],
-                    net.device, grid=grid, cfg=cfg, one_per_cu=one)
-            if split != 1:
+            if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
                 _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                           _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
                           self.colsum_part.numel() * 4, st)
-            side = self._side_stream
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                self._side_gemm.run()
+            if not self.buckets:  # (bucketed: step() / step_graph() launch it, with the early all-reduce)
+                self._side_launch()
+
+    def _side_launch(self):
+        """Fork: the side stream waits for the work enqueued so far on the current stream, then runs
+        the persistent dW_lin (+ bias row sums) launch beside what the current stream does next."""
+        net, H = self.net, self.net.H
+        g = net.grad
+        if self._side_stream is None:
+            grid, cfg, split, one = self.side
+            FE = self.F * net.E
+            self._side_stream = torch.cuda.Stream(device=net.device)
+            self._side_gemm = ops.GroupedGemm(
+                [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
+                      transA=True, transB=False, beta=1.0, splitk=split,
+                      rowsum=net.view("mix.Linear.bias", g) if split == 1 else None)],
+                net.device, grid=grid, cfg=cfg, one_per_cu=one)
+        self._side_stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._side_stream):
+            self._side_gemm.run()
+
+    def _side_join(self):
+        """Join: the current stream waits for the side stream's work."""
+        torch.cuda.current_stream().wait_stream(self._side_stream)
 
     def _backward_fast(self):
         """The bf16 backward from the first BPTT on: the BPTT / dX chain down the layers, the bias
@@ -620,10 +632,10 @@ class SepTrainer:
                 dH = dH_next
         if self.defer_bias:
             self._bias_reduce()
-        if self.side:  # dW_lin's side stream joins before the grouped launch
-            torch.cuda.current_stream().wait_stream(self._side_stream)
         if grouped:
             dwg.run()
+        if self.side and not self.buckets:  # dW_lin's side stream joins at the end of the backward
+            self._side_join()
 
     def _bias_reduce(self):
         """Every layer's BPTT bias partials (DL4SS_RNN_DEFER_BIAS) into db_ih / db_hh, one launch."""
@@ -732,6 +744,16 @@ class SepTrainer:
 
         self._works.append(dp.allreduce_sum_async(self.net.grad_ext[self.net.bucket_split():], self.pg))
 
+    def _early_bucket(self):
+        """Bucketed data parallel: the side stream's dW_lin (when on) and then, behind it on the same
+        stream, the early bucket's all-reduce -- both beside the BPTT chain that follows."""
+        if self.side:
+            self._side_launch()
+            with torch.cuda.stream(self._side_stream):
+                self.allreduce_early()
+        else:
+            self.allreduce_early()
+
     def allreduce_late(self):
         """Start the SUM all-reduce of the late bucket (the status flag and every recurrent layer)."""
         from . import dp
@@ -765,9 +787,11 @@ class SepTrainer:
         loss = self.loss_and_grad()
         if self.buckets:
             self.backward_early()
-            self.allreduce_early()
+            self._early_bucket()
             self.backward_late()
             self.allreduce_late()
+            if self.side:
+                self._side_join()
         else:
             self.backward()
             self.allreduce()
@@ -833,9 +857,11 @@ class SepTrainer:
         ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
         self.graph.replay()
         if self.graph_late is not None:
-            self.allreduce_early()
+            self._early_bucket()
             self.graph_late.replay()
             self.allreduce_late()
+            if self.side:
+                self._side_join()
         else:
             self.allreduce()
         self.optimizer_step()

@@ -60,14 +60,19 @@ def _trainer(dev, cfg, B, K, N, pg):
     return engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16", process_group=pg)
 
 
-@pytest.mark.parametrize("name", ["C2", "C4"])
-def test_rccl_world1_graph_step_bitwise_equal_to_single_gpu(dev, pg, name):
+@pytest.mark.parametrize("name,buckets", [("C2", "1"), ("C4", "1"), ("C2", "0")])
+def test_rccl_world1_graph_step_bitwise_equal_to_single_gpu(dev, pg, name, buckets, monkeypatch):
+    """buckets "1" (default): the early bucket (Linear, embedding, ADDJUST) all-reduced behind the
+    side-stream dW_lin beside the BPTT chain, the late one after it, two graph replays; "0": one flat
+    all-reduce after one replay.  Both SUM, with the 1 / world inside Adam."""
+    monkeypatch.setenv("DL4SS_DP_BUCKETS", buckets)
     cfg = CFGS[name]
     B, K, N = 32, cfg["K"], 32000
     pool = _pool(dev, B, K, N)
     runs = {}
     for tag, group in (("single", None), ("rccl", pg)):
         tr = _trainer(dev, cfg, B, K, N, group)
+        assert tr.buckets == (group is not None and buckets == "1")
         tr.step(*pool[0])  # eager warm-up before the capture
         losses = [float(tr.step_graph(*b)[0].item()) for b in pool]
         tr.check()
