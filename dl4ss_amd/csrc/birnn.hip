@@ -212,6 +212,10 @@ struct RnnArgs {
   const float* bih;            // (2, NGATE*H)
   int Kin;
   long long ldx, ldw;
+  // act layout: 0 gate-major (B,T,2,4H); 1 cell-major (B,T,2,H,4) -- the packed kernels at BC >= 4
+  // (act_cell_major): the forward stores a cell's four gates as one 16-B store, the BPTT loads them
+  // as one 16-B item
+  int act_cm;
 };
 
 __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& group, int& w) {
@@ -1163,8 +1167,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #endif
       if (cval) {
         const long long bt = (long long)bg * T + t;
-        float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
-        if (!(FWD_EXP_SKIP & 1)) { actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3]; }
+        if (FWD_EXP_SKIP & 1) {
+        } else if (a.act_cm) {
+          *reinterpret_cast<float4*>(a.act + ((bt * 2 + d) * H + cj) * 4) = make_float4(st[0], st[1], st[2], st[3]);
+        } else {
+          float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
+          actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
+        }
         if constexpr (CELL == CELL_LSTM) if (!(FWD_EXP_SKIP & 2)) a.cs[(bt * 2 + d) * H + cj] = cst;
         const long long ho = bt * 2 * H + d * H + cj;
         if (a.hprev) a.hprev[ho] = hst;
@@ -1646,20 +1655,54 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   static_assert(NPF == 128, "two prefetch waves");
   constexpr bool PFF = BC >= 4;
   constexpr int CPWP = (BC * 20 + 1) / 2;  // raw staging pitch: cells per prefetch wave at J <= 20
-  constexpr int NQ = PFF ? (NSL * CPWP + 63) / 64 : (BC * 20 * NSL + NPF - 1) / NPF;
+  // PFF: the act slots 1-4 arrive as ONE 16-B item per cell (the cell-major act of the packed
+  // forward, a.act_cm, required at BC >= 4 by the launcher): the scalar loader carries the other
+  // slots (dOut, c, c_prev / dOut, h_prev), slot index = sl_of[scalar slot]
+  constexpr int NSLS = NSL - 4;
+  constexpr int NQ = PFF ? (NSLS * CPWP + 63) / 64 : (BC * 20 * NSL + NPF - 1) / NPF;
+  constexpr int NQA = PFF ? (CPWP + 63) / 64 : 1;
   const int ncell = BC * J, cpw = (ncell + 1) / 2, pwi = wv - WPF;
   float* sraw = sop + 2 * 2 * SOPP + (wv >= WPF ? pwi : 0) * NSL * CPWP;
   StepLoader<NQ> ld;
+  const float4* ap[NQA];
+  float4 av[NQA];
+  int ac[NQA];
+#pragma unroll
+  for (int q = 0; q < NQA; ++q) {
+    const int c = lane + 64 * q, cell = pwi * cpw + c;
+    const int ib = b0 + cell / J, ij = j0 + cell % J;
+    const bool ok = PFF && wv >= WPF && c < cpw && cell < ncell;
+    ap[q] = (ok && ib < a.B && ij < H) ? reinterpret_cast<const float4*>(a.act) + ((long long)ib * T * 2 + d) * H + ij
+                                       : nullptr;
+    ac[q] = ok ? c : -1;
+    av[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  auto act_issue = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < NQA; ++q)
+      av[q] = ap[q] != nullptr ? ap[q][(long long)t * 2 * H] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto act_commit = [&]() {
+#pragma unroll
+    for (int q = 0; q < NQA; ++q)
+      if (ac[q] >= 0) {
+        sraw[1 * CPWP + ac[q]] = av[q].x;
+        sraw[2 * CPWP + ac[q]] = av[q].y;
+        sraw[3 * CPWP + ac[q]] = av[q].z;
+        sraw[4 * CPWP + ac[q]] = av[q].w;
+      }
+  };
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     int slot, c = 0, cell;
     bool on;
     if constexpr (PFF) {
       const int i = lane + 64 * q;
-      slot = i / cpw;
-      c = i - slot * cpw;
+      const int ss = i / cpw;  // scalar slot 0, 1, 2 -> slot 0, 5, 6
+      slot = ss == 0 ? 0 : ss + 4;
+      c = i - ss * cpw;
       cell = pwi * cpw + c;
-      on = wv >= WPF && slot < NSL && cell < ncell;
+      on = wv >= WPF && ss < NSLS && cell < ncell;
     } else {
       const int i = tid - WPF * 64 + q * NPF;
       slot = i / ncell;
@@ -1688,7 +1731,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.shift[q] = shift;
     ld.dst[q] = !on ? -1 : PFF ? slot * CPWP + c : (slot >> 2) * SOPP + cell * 4 + (slot & 3);
   }
-  if (wv >= WPF) ld.issue(d == 0 ? T - 1 : 0, T);
+  if (wv >= WPF) {
+    ld.issue(d == 0 ? T - 1 : 0, T);
+    if constexpr (PFF) act_issue(d == 0 ? T - 1 : 0);
+  }
   __syncthreads();
   const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
   STAMP_DECL
@@ -1788,6 +1834,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     //   GRU  {dOut, (1-z)(1-n^2) hn r (1-r), (h_prev - n) z (1-z), (1-z)(1-n^2)} {(1-z)(1-n^2) r, z, -, -}
     auto pf_factors = [&](int s) {
       ld.commit(sraw);
+      act_commit();
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       // one lane per cell, in passes of 64: cpw = ceil(BC J / 2) is 80 at BC = 8, J = 20
@@ -1824,10 +1871,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       // queue beside the polling sweeps (MI355X_MICROARCH.md handoff-1to1: the hand-off price sits
       // in the consumer CU's queue); they still have the cell phase and the next poll window to land
       __syncthreads();  // B1
-      if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+      if (s + 1 < T) {
+        ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+        if constexpr (PFF) act_issue(d == 0 ? T - 2 - s : s + 1);
+      }
       __syncthreads();  // B2
 #else
-      if (s + 1 < T) ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+      if (s + 1 < T) {
+        ld.issue(d == 0 ? T - 2 - s : s + 1, T);
+        if constexpr (PFF) act_issue(d == 0 ? T - 2 - s : s + 1);
+      }
       __syncthreads();  // B1
       __syncthreads();  // B2
 #endif
@@ -2152,6 +2205,10 @@ bool make_plan(int cell, int B, int H, Plan& p, bool mf = true, int max_wg = 0) 
   return false;
 }
 
+// act layout of a plan: cell-major (B,T,2,H,4) when both packed kernels run it at BC >= 4 (the
+// forward's one 16-B store per cell, the BPTT's one 16-B load; RnnArgs::act_cm), else gate-major
+bool act_cell_major(const Plan& p) { return p.fwd_pk && p.bwd_pk && p.BC >= 4; }
+
 // every persistent recurrence launch goes through the co-residency guard
 template <typename K>
 int launch_resident(K kernel, int grid, size_t smem, hipStream_t st, const RnnArgs& a) {
@@ -2387,6 +2444,7 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
   const long long groups = 2LL * p.nchunk;
   const bool mf = precision == 1;
   const bool pk = mf && p.fwd_pk && T < 65535;
+  const bool act_cm = pk && act_cell_major(p);
   if (!prezeroed) {
     hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.BC * p.NG * 8 * 8 : groups * 2 * p.BC * H * 8, st);
     if (e != hipSuccess) return (int)e;
@@ -2397,6 +2455,7 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
   RnnArgs a{};
   fill_args(a, p, B, T, H);
   a.G = G; a.Whh = W_hh; a.bhh = b_hh; a.out = out; a.hprev = hprev; a.act = act; a.cs = cs;
+  a.act_cm = act_cm ? 1 : 0;
   a.outb = reinterpret_cast<unsigned short*>(out_bf16);
   a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
@@ -2448,6 +2507,7 @@ DL4SS_API int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf
   RnnArgs a{};
   fill_args(a, p, B, T, H);
   a.G = nullptr; a.Whh = W_hh; a.bhh = b_hh; a.out = out; a.hprev = hprev; a.act = act; a.cs = cs;
+  a.act_cm = act_cell_major(p) ? 1 : 0;
   a.outb = reinterpret_cast<unsigned short*>(out_bf16);
   a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
@@ -2500,7 +2560,8 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   hipStream_t st = as_stream(stream);
   const long long groups = 2LL * p.nchunk;
   const bool mf = precision == 1;
-  const bool pk = mf && p.bwd_pk && T < 65535;
+  // the packed BPTT at BC >= 4 reads the cell-major act that only the packed forward writes
+  const bool pk = mf && p.bwd_pk && T < 65535 && (p.BC < 4 || act_cell_major(p));
   const long long HG = ((H + 1) / 2 + 1) & ~1;
   if (!prezeroed) {
     hipError_t e =

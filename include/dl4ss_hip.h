@@ -186,7 +186,10 @@ void dl4ss_debug_set_place_force(int force);
 void dl4ss_debug_set_rnn_max_wg(int max_wg);
 /* One layer, both directions: G (B,T,2,NG*H) = X W_ih^T + b_ih (NG = 4 LSTM / 3 GRU),
  * W_hh (2, NG*H, H), b_hh (2, NG*H) -> out (B,T,2H) [fwd | reverse], hprev (B,T,2H)
- * (h_{t-1} per step), act (B,T,2,4H) gate activations, cs (B,T,2,H) LSTM cells.
+ * (h_{t-1} per step), act (B,T,2,4H) gate activations, cs (B,T,2,H) LSTM cells.  act is
+ * gate-major (B,T,2,4H) except where both packed bf16 kernels run the plan at batch chunks >= 4
+ * (every C2 / C4 step at B = 32): there it is cell-major (B,T,2,H,4), one 16-B record per cell,
+ * written by the forward and read by dl4ss_birnn_bwd[_ex] of the same precision and shape.
  * precision 0: exact fp32 recurrent matvec (VALU); 1: bf16 operands on MFMA with fp32
  * accumulate (cell state, gates and all outputs stay fp32).
  * *status != 0 after the call means a hand-off timed out (results invalid).
