@@ -216,6 +216,7 @@ struct RnnArgs {
   // (act_cell_major): the forward stores a cell's four gates as one 16-B store, the BPTT loads them
   // as one 16-B item
   int act_cm;
+  float* hmean;  // fwd (packed): (B, 2H) mean over t of h, summed by each cell lane in step order (or null)
 };
 
 __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& group, int& w) {
@@ -584,6 +585,9 @@ constexpr int WPOLL = 4;    // the polling wave (BPTT: the first of BWD_NPW)
 #define BWD_NPW 2  // BPTT polling waves
 #endif
 constexpr int FWD_MV_CHAINS = 2;  // forward bf16 matvec: accumulator chains per MFMA tile (4: 367 vs 363 us per pass)
+#ifndef FWD_XDMA_EARLY
+#define FWD_XDMA_EARLY 0  // 1: the fused forward's input-row DMA issued after B1 instead of after B2 (C2: 3.540 vs 3.498 ms per step, A/B x3, round 5: slower)
+#endif
 #ifndef FWD_NPW
 #define FWD_NPW 2  // forward polling waves: 4, and 7 when >= 2, and 6 when 3 (their MFMA tile indices must be >= MT)
 #endif
@@ -761,7 +765,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   float bh[NGATE];
 #pragma unroll
   for (int q = 0; q < NGATE; ++q) bh[q] = cval ? a.bhh[(long long)d * GH + q * H + cj] : 0.0f;
-  float hst = 0.0f, cst = 0.0f;
+  float hst = 0.0f, cst = 0.0f, hsum = 0.0f;
 
   // granules of this group: [2 slots][hand-off, spare][BC][NG][8] x 8 B; the spare copy of
   // slot 1 holds the placement granules
@@ -818,7 +822,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   };
   // wait until at most `n` steps' pieces (the latest issued) are still in flight (n <= SPB)
   auto xwait = [&](int n) {
-    static_assert(!XW || SPB * NXQ <= 63, "vmcnt range");
+    static_assert(!XW || (SPB + FWD_XDMA_EARLY) * NXQ <= 63, "vmcnt range");
 #define XW_WAIT(k) \
   case k:          \
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((k) * NXQ <= 63 ? (k) * NXQ : 63) : "memory"); break;
@@ -1075,17 +1079,26 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         STAMP(0)
         __syncthreads();  // B1
         STAMP(1)
+#if FWD_XDMA_EARLY
+        // step s + 3 SPB's rows into slot s % NSLOT, issued right after B1: that slot held step s's
+        // rows, last read by the chain of block s / SPB, which ended before B1(s).  Here, not after B2,
+        // the pieces travel during the matvec and the gate phase instead of sitting in the CU's memory
+        // queue beside the next hand-off's polls (the BPTT's BWD_PF_LATE argument)
+        if (XW && s + NSLOT < T) xdma(s + NSLOT);
+#endif
         if constexpr (MV) matvec();
         // XW: at a block start the rows of the next block (consumed from this step on) landed
-        // before B2; the block after it may stay in flight
-        if (XW && s % SPB == 0) xwait(max(0, min(SPB, T - (s / SPB + 2) * SPB)));
+        // before B2; the block after it may stay in flight (and, issued early, this step's too)
+        if (XW && s % SPB == 0) xwait(max(0, min(SPB + FWD_XDMA_EARLY, T - (s / SPB + 2) * SPB)));
         STAMP(2)
         __syncthreads();  // B2
         STAMP(3)
         if (XW) xstep(ntl, s);
+#if !FWD_XDMA_EARLY
         // step s + 3 SPB's rows into slot s % NSLOT, issued after B2 (off the matvec -> B2 path); that
         // slot held step s's rows, last read by the chain of block s / SPB, which ended before B1(s)
         if (XW && s + NSLOT < T) xdma(s + NSLOT);
+#endif
         STAMP(4)
       }
     };
@@ -1177,7 +1190,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         if constexpr (CELL == CELL_LSTM) if (!(FWD_EXP_SKIP & 2)) a.cs[(bt * 2 + d) * H + cj] = cst;
         const long long ho = bt * 2 * H + d * H + cj;
         if (a.hprev) a.hprev[ho] = hst;
-        if (!(FWD_EXP_SKIP & 4)) a.out[ho] = hn;
+        if (a.out && !(FWD_EXP_SKIP & 4)) a.out[ho] = hn;
+        hsum += hn;
         // bf16 copies, 16-B aligned rows for the GEMMs: out_bf16 (B*T, pad8(2H)) with the
         // directions adjacent (the next layer's K), hprev_bf16 (B*T, 2 pad8(H)) with each
         // direction's block 16-B aligned (the per-direction dW_hh operand)
@@ -1189,6 +1203,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     }
     STAMP(4)
   }
+  // the layer output's mean over t (the ADDJUST / classifier time mean, EvalVer.py:363-377): each cell
+  // lane's own sum in step order -- no separate pass over the (B, T, 2H) output
+  if (a.hmean && cval) a.hmean[(long long)bg * 2 * H + d * H + cj] = hsum / (float)T;
   STAMP_FLUSH
 }
 
@@ -1656,9 +1673,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   constexpr bool PFF = BC >= 4;
   constexpr int CPWP = (BC * 20 + 1) / 2;  // raw staging pitch: cells per prefetch wave at J <= 20
   // PFF: the act slots 1-4 arrive as ONE 16-B item per cell (the cell-major act of the packed
-  // forward, a.act_cm, required at BC >= 4 by the launcher): the scalar loader carries the other
-  // slots (dOut, c, c_prev / dOut, h_prev), slot index = sl_of[scalar slot]
-  constexpr int NSLS = NSL - 4;
+  // forward, a.act_cm, required at BC >= 4 by the launcher); the scalar loader carries dOut and
+  // (LSTM) c_prev = c at the step's neighbour t -+ 1, or (GRU) h_prev.  The LSTM's c of a step is
+  // the c_prev the previous step loaded: pf_factors keeps it in the slot-5 row for the next step
+  // (one scalar load per cell and step fewer; the first step's c is loaded once before the loop)
+  constexpr int NSLS = 2;
   constexpr int NQ = PFF ? (NSLS * CPWP + 63) / 64 : (BC * 20 * NSL + NPF - 1) / NPF;
   constexpr int NQA = PFF ? (CPWP + 63) / 64 : 1;
   const int ncell = BC * J, cpw = (ncell + 1) / 2, pwi = wv - WPF;
@@ -1698,8 +1717,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     bool on;
     if constexpr (PFF) {
       const int i = lane + 64 * q;
-      const int ss = i / cpw;  // scalar slot 0, 1, 2 -> slot 0, 5, 6
-      slot = ss == 0 ? 0 : ss + 4;
+      const int ss = i / cpw;  // scalar slot 0, 1 -> slot 0, and 6 (LSTM c_prev) / 5 (GRU h_prev)
+      slot = ss == 0 ? 0 : CELL == CELL_LSTM ? 6 : 5;
       c = i - ss * cpw;
       cell = pwi * cpw + c;
       on = wv >= WPF && ss < NSLS && cell < ncell;
@@ -1734,6 +1753,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   if (wv >= WPF) {
     ld.issue(d == 0 ? T - 1 : 0, T);
     if constexpr (PFF) act_issue(d == 0 ? T - 1 : 0);
+    if constexpr (PFF && CELL == CELL_LSTM) {  // the first step's c (later steps reuse c_prev)
+      const int t0 = d == 0 ? T - 1 : 0;
+      for (int c = lane; c < cpw; c += 64) {
+        const int cell = pwi * cpw + c;
+        const int ib = b0 + cell / J, ij = j0 + cell % J;
+        sraw[5 * CPWP + c] = (cell < ncell && ib < a.B && ij < H) ? a.cs[((long long)(ib * T + t0) * 2 + d) * H + ij]
+                                                                     : 0.0f;
+      }
+    }
   }
   __syncthreads();
   const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
@@ -1859,6 +1887,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         float* rec = sop + (s & 1) * 2 * SOPP + cell * 4;
         *reinterpret_cast<float4*>(rec) = p0;
         *reinterpret_cast<float4*>(rec + SOPP) = p1;
+        if constexpr (CELL == CELL_LSTM) sraw[5 * CPWP + c] = v[6];  // the next step's c
       }
     };
     for (int s = 0; s < T; ++s) {
@@ -2484,13 +2513,30 @@ DL4SS_API int dl4ss_birnn_fwd_xw_supported(int cell, int B, int T, int H, int Ki
 // (16-B chunks: padding up to the next multiple of 8 finite); W_ih_bf16: (2*NGATE*H, ldw) bf16 (direction-major rows, the GEMM's B operand); b_ih
 // (2, NGATE*H) fp32.  ldx, ldw multiples of 8 and both bases 16-B aligned.  Same summation order as
 // the GEMM path (one k-ordered MFMA chain, then + b_ih): the outputs match it bit for bit.
+DL4SS_API int dl4ss_birnn_fwd_xw_ex(int cell, int B, int T, int H, const void* x_bf16, int Kin, long long ldx,
+                                    const void* W_ih_bf16, long long ldw, const float* b_ih, const float* W_hh,
+                                    const float* b_hh, float* out, float* hprev, float* act, float* cs,
+                                    void* out_bf16, void* hprev_bf16, float* h_mean, void* workspace,
+                                    long long ws_bytes, int* status, void* stream, int ws_zeroed);
+
 DL4SS_API int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf16, int Kin, long long ldx,
                                  const void* W_ih_bf16, long long ldw, const float* b_ih, const float* W_hh,
                                  const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
                                  void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream,
                                  int ws_zeroed) {
+  DL4SS_REQUIRE(out);
+  return dl4ss_birnn_fwd_xw_ex(cell, B, T, H, x_bf16, Kin, ldx, W_ih_bf16, ldw, b_ih, W_hh, b_hh, out, hprev, act, cs,
+                               out_bf16, hprev_bf16, nullptr, workspace, ws_bytes, status, stream, ws_zeroed);
+}
+
+DL4SS_API int dl4ss_birnn_fwd_xw_ex(int cell, int B, int T, int H, const void* x_bf16, int Kin, long long ldx,
+                                    const void* W_ih_bf16, long long ldw, const float* b_ih, const float* W_hh,
+                                    const float* b_hh, float* out, float* hprev, float* act, float* cs,
+                                    void* out_bf16, void* hprev_bf16, float* h_mean, void* workspace,
+                                    long long ws_bytes, int* status, void* stream, int ws_zeroed) {
   DL4SS_REQUIRE(dl4ss_birnn_fwd_xw_supported(cell, B, T, H, Kin));
-  DL4SS_REQUIRE(x_bf16 && W_ih_bf16 && b_ih && W_hh && b_hh && out && act && workspace && status);
+  DL4SS_REQUIRE(x_bf16 && W_ih_bf16 && b_ih && W_hh && b_hh && act && workspace && status);
+  DL4SS_REQUIRE(out || out_bf16);  // some output of the layer
   DL4SS_REQUIRE(cell == CELL_GRU || cs);
   DL4SS_REQUIRE(hprev || cell == CELL_LSTM);
   DL4SS_REQUIRE(ldx >= Kin && ldw >= Kin && ldx % 8 == 0 && ldw % 8 == 0);
@@ -2508,6 +2554,7 @@ DL4SS_API int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf
   fill_args(a, p, B, T, H);
   a.G = nullptr; a.Whh = W_hh; a.bhh = b_hh; a.out = out; a.hprev = hprev; a.act = act; a.cs = cs;
   a.act_cm = act_cell_major(p) ? 1 : 0;
+  a.hmean = h_mean;
   a.outb = reinterpret_cast<unsigned short*>(out_bf16);
   a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);

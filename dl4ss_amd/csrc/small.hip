@@ -287,10 +287,11 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 
 DL4SS_API int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* idx, const float* emb,
                               const float* w_adj, int K, int W, float* q, float* mean_out, void* stream) {
-  DL4SS_REQUIRE(h && idx && emb && q && B > 0 && T > 0 && D > 0 && K > 0 && W > 0);
+  // h NULL: mean_out already holds the time mean (the recurrence formed it, dl4ss_birnn_fwd_xw_ex)
+  DL4SS_REQUIRE((h || mean_out) && idx && emb && q && B > 0 && T > 0 && D > 0 && K > 0 && W > 0);
   DL4SS_REQUIRE(!w_adj || mean_out);  // ADJUST needs the time mean (also saved for the backward)
   hipStream_t st = as_stream(stream);
-  if (mean_out) {
+  if (mean_out && h) {
     hipLaunchKernelGGL(time_mean_kernel, dim3(B, cdiv(D, 64)), dim3(64 * TM_PH), 0, st, h, T, D, mean_out);
     DL4SS_CHECK_LAUNCH();
   }

@@ -369,6 +369,7 @@ class SepTrainer:
             self._hilo(net.cat_view("weight_ih", l), self.ws_ih[l], self.seg[l], W_SPLIT)
         self._hilo(net.view("mix.Linear.weight"), self.ws_lin, self.p8(2 * H), W_SPLIT)
         self._to_bf16_rows(x, self.xb0)
+        self._mean_done = False
         self._hilo(x, self.xs0, self.seg[0], A_SPLIT)
         xin = self.xs0
         for l in range(net.L):
@@ -391,17 +392,23 @@ class SepTrainer:
         self._weights_to_bf16()
         self._to_bf16_rows(x, self.xb0)
         xb = self.xb0[:, :x.shape[1]]
+        self._mean_done = False
         for l in range(net.L):
             D = xb.shape[1]
             hp = self.hprev[l]
             if self.xw and D <= self.xw_kmax and _lib.query("dl4ss_birnn_fwd_xw_supported", cell, B, T, H, D) == 1:
                 wih = self.wb_ih[l]
-                _lib.call("dl4ss_birnn_fwd_xw", cell, B, T, H, _lib.ptr(xb, strided=True), D, xb.stride(0),
+                # no fp32 layer output (the next layer and the GEMMs read the bf16 one); the last layer
+                # forms the time mean of ADDJUST / the query inside the recurrence (h_mean)
+                last = l == net.L - 1
+                _lib.call("dl4ss_birnn_fwd_xw_ex", cell, B, T, H, _lib.ptr(xb, strided=True), D, xb.stride(0),
                           _lib.ptr(wih), wih.stride(0), _lib.ptr(net.cat_view("bias_ih", l)),
                           _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
-                          _lib.ptr(self.out[l]), _lib.ptr(hp), _lib.ptr(self.act[l]),
+                          None, _lib.ptr(hp), _lib.ptr(self.act[l]),
                           _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.outb[l]), _lib.ptr(self.hprevb[l]),
+                          _lib.ptr(self.mean) if last else None,
                           _lib.ptr(self._ws_slot(l, False)), self.ws_bytes, _lib.ptr(self.status), st, 1)
+                self._mean_done = last
                 xb = self.outb[l][:, :2 * H]
                 continue
             self._gemm_fwd(xb, self.wb_ih[l][:, :D], net.cat_view("bias_ih", l), self.G)
@@ -429,7 +436,8 @@ class SepTrainer:
             else:
                 self._forward_fast(x)
             wadj = net.view("adj.layer.weight") if net.adjust else None
-            _lib.call("dl4ss_query_fwd", _lib.ptr(self.out[-1]), B, T, 2 * H, _lib.ptr(self.spk),
+            h_last = None if (not self.split and self._mean_done) else _lib.ptr(self.out[-1])
+            _lib.call("dl4ss_query_fwd", h_last, B, T, 2 * H, _lib.ptr(self.spk),
                       _lib.ptr(net.view("emb.layer.weight")), _lib.ptr(wadj), self.K, net.W, _lib.ptr(self.q),
                       _lib.ptr(self.mean), st)
             self._feats = x

@@ -220,6 +220,14 @@ int dl4ss_birnn_fwd_xw(int cell, int B, int T, int H, const void* x_bf16, int Ki
                        const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
                        void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream,
                        int ws_zeroed);
+/* dl4ss_birnn_fwd_xw with the fp32 layer output optional (out may be NULL when out_bf16 is not)
+ * and h_mean (B, 2H) (NULL: none) = the mean over t of the layer output, each (b, direction, unit)
+ * summed in step order by the unit's own cell lane -- the time mean of the last layer that ADDJUST
+ * (EvalVer.py:363-377) reads, without a pass over the output. */
+int dl4ss_birnn_fwd_xw_ex(int cell, int B, int T, int H, const void* x_bf16, int Kin, long long ldx,
+                          const void* W_ih_bf16, long long ldw, const float* b_ih, const float* W_hh, const float* b_hh,
+                          float* out, float* hprev, float* act, float* cs, void* out_bf16, void* hprev_bf16,
+                          float* h_mean, void* workspace, long long ws_bytes, int* status, void* stream, int ws_zeroed);
 /* 1 when dl4ss_birnn_fwd_xw applies to (cell, B, T, H, Kin) (the packed bf16 plan exists, Kin <= 640);
  * host-only. */
 int dl4ss_birnn_fwd_xw_supported(int cell, int B, int T, int H, int Kin);
@@ -279,7 +287,9 @@ int dl4ss_loss_finalize(const float* part_loss, int B, int K, int nblk, const in
 
 /* ---- speaker queries, reductions, optimizer ------------------------------ */
 /* q[b,k] = Emb[idx[b,k]] (+ W_adj [mean_t h[b]; Emb[idx[b,k]]]); h (B,T,D).
- * SPEECH_EMBEDDING + ADDJUST: EvalVer.py:348-377,606-608. w_adj may be NULL; an idx of -1 (no speaker) gives a zero query. */
+ * SPEECH_EMBEDDING + ADDJUST: EvalVer.py:348-377,606-608. w_adj may be NULL; an idx of -1 (no speaker) gives a zero query.
+ * mean_out (B,D) receives mean_t h; with h NULL it is instead READ as that mean, formed by the
+ * recurrence (dl4ss_birnn_fwd_xw_ex h_mean). */
 int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* idx, const float* emb, const float* w_adj, int K,
                     int W, float* q, float* mean_out, void* stream);
 /* d_emb (+=, scatter), d_wadj (+=), dh_bcast (B,D) = W_m^T sum_k dq / T. */
