@@ -40,6 +40,7 @@ SIGNATURES = {
     "dl4ss_gemm_bf16_gl_grouped_ex": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, I, I, I, P, P],
     "dl4ss_birnn_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_fwd_xw": [I, I, I, I, P, I, LL, P, LL, P, P, P, P, P, P, P, P, P, P, LL, P, P, I],
+    "dl4ss_birnn_fwd_mean": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, LL, P, P],
     "dl4ss_birnn_fwd_xw_ex": [I, I, I, I, P, I, LL, P, LL, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I],
     "dl4ss_birnn_fwd_xw_supported": [I, I, I, I, I],
     "dl4ss_birnn_bwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P],

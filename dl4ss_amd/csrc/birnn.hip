@@ -2457,14 +2457,30 @@ DL4SS_API int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, cons
                             ws_bytes, status, stream);
 }
 
+DL4SS_API int dl4ss_birnn_fwd_mean(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
+                                   const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                                   void* hprev_bf16, float* h_mean, void* workspace, long long ws_bytes, int* status,
+                                   void* stream);
+
 DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
                                  const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
                                  void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream) {
+  DL4SS_REQUIRE(out);
+  return dl4ss_birnn_fwd_mean(cell, precision, B, T, H, G, W_hh, b_hh, out, hprev, act, cs, out_bf16, hprev_bf16,
+                              nullptr, workspace, ws_bytes, status, stream);
+}
+
+// dl4ss_birnn_fwd_ex with the fp32 output optional (packed kernel: out may be NULL when out_bf16 is
+// not) and the time mean of the output formed in the recurrence (h_mean, packed kernel only)
+DL4SS_API int dl4ss_birnn_fwd_mean(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
+                                   const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                                   void* hprev_bf16, float* h_mean, void* workspace, long long ws_bytes, int* status,
+                                   void* stream) {
   DL4SS_REQUIRE(cell == CELL_LSTM || cell == CELL_GRU);
   const bool prezeroed = precision & DL4SS_RNN_WS_ZEROED;  // the caller zeroed the workspace (one fill per step)
   precision &= ~DL4SS_RNN_WS_ZEROED;
   DL4SS_REQUIRE(precision == 0 || precision == 1);
-  DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && out && act && workspace && status);
+  DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && (out || out_bf16) && act && workspace && status);
   DL4SS_REQUIRE(cell == CELL_GRU || cs);
   Plan p;
   DL4SS_REQUIRE(make_plan(cell, B, H, p, precision == 1));
@@ -2474,6 +2490,7 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
   const bool mf = precision == 1;
   const bool pk = mf && p.fwd_pk && T < 65535;
   const bool act_cm = pk && act_cell_major(p);
+  DL4SS_REQUIRE(pk || (out && !h_mean));  // the optional output and the fused mean are the packed kernel's
   if (!prezeroed) {
     hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.BC * p.NG * 8 * 8 : groups * 2 * p.BC * H * 8, st);
     if (e != hipSuccess) return (int)e;
@@ -2485,6 +2502,7 @@ DL4SS_API int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, c
   fill_args(a, p, B, T, H);
   a.G = G; a.Whh = W_hh; a.bhh = b_hh; a.out = out; a.hprev = hprev; a.act = act; a.cs = cs;
   a.act_cm = act_cm ? 1 : 0;
+  a.hmean = h_mean;
   a.outb = reinterpret_cast<unsigned short*>(out_bf16);
   a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);

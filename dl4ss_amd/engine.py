@@ -232,6 +232,10 @@ class SepTrainer:
             raise ValueError(f"DL4SS_RNN_XW={xw}: expected 0, 1 or l0")
         self.xw = self.fast and xw != "0" and not self.split
         self.xw_kmax = 160 if xw == "l0" else 640
+        # bf16s: the first layer's split-operand projection ([x_hi | x_lo | x_hi] . [w_hi | w_hi | w_lo],
+        # K' = 3 pad8(F) = 408 <= 640) fused into its recurrence too -- the same k-ordered chain + b_ih as
+        # the split GEMM; the 600-wide layers' K' = 1800 stays a GEMM
+        self.xw_split0 = self.split and xw != "0"
         # data parallel, bf16 step: the gradient leaves in two buckets ("can
         # overlap with BPTT of the lower layers").  The Linear / embedding / ADDJUST gradients are
         # complete before the first BPTT (dW_lin then runs on its own, not in the grouped launch) and
@@ -373,6 +377,19 @@ class SepTrainer:
         self._hilo(x, self.xs0, self.seg[0], A_SPLIT)
         xin = self.xs0
         for l in range(net.L):
+            Ks = xin.shape[1]
+            if (l == 0 and self.xw_split0 and
+                    _lib.query("dl4ss_birnn_fwd_xw_supported", cell, B, T, H, Ks) == 1):
+                wih = self.ws_ih[0]
+                _lib.call("dl4ss_birnn_fwd_xw_ex", cell, B, T, H, _lib.ptr(xin), Ks, xin.stride(0), _lib.ptr(wih),
+                          wih.stride(0), _lib.ptr(net.cat_view("bias_ih", 0)),
+                          _lib.ptr(net.cat_view("weight_hh", 0)), _lib.ptr(net.cat_view("bias_hh", 0)),
+                          _lib.ptr(self.out[0]), _lib.ptr(self.hprev[0]), _lib.ptr(self.act[0]),
+                          _lib.ptr(self.cs[0]) if self.cs else None, _lib.ptr(self.outb[0]), _lib.ptr(self.hprevb[0]),
+                          None, _lib.ptr(self._ws_slot(0, False)), self.ws_bytes, _lib.ptr(self.status), st, 1)
+                self._hilo(self.out[0].view(B * T, 2 * H), self.xs, self.p8(2 * H), A_SPLIT)
+                xin = self.xs
+                continue
             self._gemm_fwd(xin, self.ws_ih[l], net.cat_view("bias_ih", l), self.G)
             _lib.call("dl4ss_birnn_fwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(self.G),
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
@@ -412,11 +429,14 @@ class SepTrainer:
                 xb = self.outb[l][:, :2 * H]
                 continue
             self._gemm_fwd(xb, self.wb_ih[l][:, :D], net.cat_view("bias_ih", l), self.G)
-            _lib.call("dl4ss_birnn_fwd_ex", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(self.G),
+            last = l == net.L - 1  # (the time mean formed as on the fused path)
+            _lib.call("dl4ss_birnn_fwd_mean", cell, 1 | WS_ZEROED, B, T, H, _lib.ptr(self.G),
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(net.cat_view("bias_hh", l)),
                       _lib.ptr(self.out[l]), _lib.ptr(hp), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.outb[l]), _lib.ptr(self.hprevb[l]),
+                      _lib.ptr(self.mean) if last else None,
                       _lib.ptr(self._ws_slot(l, False)), self.ws_bytes, _lib.ptr(self.status), st)
+            self._mean_done = last
             xb = self.outb[l][:, :2 * H]
         self._gemm_fwd(xb, self.wb_lin[:, :2 * H], net.view("mix.Linear.bias"), self.Vb, ops.EPI_TANH_BF16)
 

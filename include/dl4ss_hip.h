@@ -207,6 +207,12 @@ int dl4ss_birnn_fwd(int cell, int precision, int B, int T, int H, const float* G
 int dl4ss_birnn_fwd_ex(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
                        const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
                        void* hprev_bf16, void* workspace, long long ws_bytes, int* status, void* stream);
+/* dl4ss_birnn_fwd_ex with, in the packed kernel (precision 1), the fp32 output optional (out NULL when
+ * out_bf16 is given) and h_mean (B, 2H) = the mean over t of the output, summed in step order by each
+ * unit's cell lane (NULL: none) -- as dl4ss_birnn_fwd_xw_ex, for the unfused projection. */
+int dl4ss_birnn_fwd_mean(int cell, int precision, int B, int T, int H, const float* G, const float* W_hh,
+                         const float* b_hh, float* out, float* hprev, float* act, float* cs, void* out_bf16,
+                         void* hprev_bf16, float* h_mean, void* workspace, long long ws_bytes, int* status, void* stream);
 /* dl4ss_birnn_fwd_ex with the input projection fused into the recurrence (bf16 packed kernel):
  * no G buffer and no separate GEMM -- every workgroup forms x_t W_ih^T + b_ih of its own gate rows
  * with MFMAs while the previous step's hand-off travels.  x_bf16 (B*T, ldx) bf16 layer input rows
