@@ -587,23 +587,18 @@ class SepTrainer:
             _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                       _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
                       self.colsum_part.numel() * 4, st)
-        else:
-            if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
-                _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
-                          _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
-                          self.colsum_part.numel() * 4, st)
-            if not self.buckets:  # (bucketed: step() / step_graph() launch it, with the early all-reduce)
-                self._side_launch()
 
     def _side_launch(self):
-        """Fork: the side stream waits for the work enqueued so far on the current stream, then runs
-        the persistent dW_lin (+ bias row sums) launch beside what the current stream does next."""
-        net, H = self.net, self.net.H
+        """Fork: the side stream waits for the work enqueued so far on the current stream, then zeroes
+        the flat gradient, runs the query backward (event _ev_q: dh_bcast ready), and the persistent
+        dW_lin (+ bias row sums) launch -- beside the dH GEMM and the BPTT chain."""
+        net, B, T, H = self.net, self.B, self.T, self.net.H
         g = net.grad
+        FE = self.F * net.E
         if self._side_stream is None:
             grid, cfg, split, one = self.side
-            FE = self.F * net.E
             self._side_stream = torch.cuda.Stream(device=net.device)
+            self._ev_q = torch.cuda.Event()
             self._side_gemm = ops.GroupedGemm(
                 [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
                       transA=True, transB=False, beta=1.0, splitk=split,
@@ -611,6 +606,13 @@ class SepTrainer:
                 net.device, grid=grid, cfg=cfg, one_per_cu=one)
         self._side_stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._side_stream):
+            g.zero_()
+            self._query_bwd()
+            self._ev_q.record()
+            if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
+                _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
+                          _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
+                          self.colsum_part.numel() * 4, _lib.stream_ptr())
             self._side_gemm.run()
 
     def _side_join(self):
@@ -687,14 +689,18 @@ class SepTrainer:
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         g = net.grad
-        st = _lib.stream_ptr()
+        if self.fast and self.side:
+            # the gradient zeroing, the query backward and the Linear's gradients on the side stream,
+            # beside the dH GEMM; the BPTT chain waits only for the query backward's dh_bcast
+            # (bucketed data parallel: step() / step_graph() fork it, with the early all-reduce)
+            if not self.buckets:
+                self._side_launch()
+            self._backward_fast_early()
+            if not self.buckets:
+                torch.cuda.current_stream().wait_event(self._ev_q)
+            return
         g.zero_()
-        wadj = net.view("adj.layer.weight") if net.adjust else None
-        _lib.call("dl4ss_query_bwd", _lib.ptr(self.dq), B, T, 2 * H, _lib.ptr(self.spk),
-                  _lib.ptr(net.view("emb.layer.weight")), _lib.ptr(wadj), _lib.ptr(self.mean), self.K, net.W,
-                  _lib.ptr(net.view("emb.layer.weight", g)),
-                  _lib.ptr(net.view("adj.layer.weight", g)) if net.adjust else None,
-                  _lib.ptr(self.dh_bcast) if net.adjust else None, st)
+        self._query_bwd()
         if self.fast:
             self._backward_fast_early()
             return
@@ -705,6 +711,18 @@ class SepTrainer:
                  precision=self.precision)
         ops.colsum(dPre, net.view("mix.Linear.bias", g))
         ops.gemm(dPre, net.view("mix.Linear.weight"), out=self.dH[0], splitk="auto", precision=self.precision)
+
+    def _query_bwd(self):
+        """SPEECH_EMBEDDING / ADDJUST backward: the embedding and ADDJUST gradients (added into the
+        zeroed flat gradient) and dh_bcast, ADDJUST's share of the last layer's output gradient."""
+        net, B, T, H = self.net, self.B, self.T, self.net.H
+        g = net.grad
+        wadj = net.view("adj.layer.weight") if net.adjust else None
+        _lib.call("dl4ss_query_bwd", _lib.ptr(self.dq), B, T, 2 * H, _lib.ptr(self.spk),
+                  _lib.ptr(net.view("emb.layer.weight")), _lib.ptr(wadj), _lib.ptr(self.mean), self.K, net.W,
+                  _lib.ptr(net.view("emb.layer.weight", g)),
+                  _lib.ptr(net.view("adj.layer.weight", g)) if net.adjust else None,
+                  _lib.ptr(self.dh_bcast) if net.adjust else None, _lib.stream_ptr())
 
     def backward_late(self):
         """The BPTT chain and the recurrent layers' weight / bias gradients, then the status flag."""
@@ -779,6 +797,7 @@ class SepTrainer:
             self._side_launch()
             with torch.cuda.stream(self._side_stream):
                 self.allreduce_early()
+            torch.cuda.current_stream().wait_event(self._ev_q)  # the BPTT chain needs dh_bcast
         else:
             self.allreduce_early()
 

@@ -1,7 +1,8 @@
 """The data-parallel path on the GPU at world size 1 over RCCL: an ``nccl``
 process group with a private TCP rendezvous (as ``bench.py --dist``), and SepTrainer's graph
-step with ``process_group=pg`` -- status flag behind the flat gradient -> RCCL all-reduce of
-``grad_ext`` -> ``dl4ss_adam_guarded_dp`` -- beside the 240-workgroup persistent recurrence.
+step with ``process_group=pg`` -- status flag in front of the flat gradient -> RCCL SUM all-reduce of
+``grad_ext`` (two buckets, or flat) -> ``dl4ss_adam_guarded_dp_scaled`` (x 1 / world) -- beside the
+240-workgroup persistent recurrence and the side-stream dW_lin.
 
 * At world size 1 the all-reduce is an identity, so the pg step must be BITWISE the pg=None step:
   losses, gradients, parameters, Adam moments and the status word, over several steps, for C2
@@ -90,7 +91,7 @@ def test_rccl_world1_graph_step_bitwise_equal_to_single_gpu(dev, pg, name, bucke
 
 
 def test_rccl_world1_forced_timeout_refused_through_allreduce(dev, pg):
-    """The timed-out step's status flag is written behind the flat gradient, goes through the
+    """The timed-out step's status flag is written in front of the flat gradient, goes through the
     RCCL all-reduce, and the guarded DP Adam refuses the update: weights and moments untouched,
     loss NaN, check() raises and rolls the step count back, the next step is normal."""
     B, K, N = 4, 2, 8000
