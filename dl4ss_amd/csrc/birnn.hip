@@ -217,6 +217,7 @@ struct RnnArgs {
   // as one 16-B item
   int act_cm;
   float* hmean;  // fwd (packed): (B, 2H) mean over t of h, summed by each cell lane in step order (or null)
+  unsigned* gctl;  // packed kernels: the group-formation counters (zeroed with the workspace; group_pk)
 };
 
 __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& group, int& w) {
@@ -605,6 +606,70 @@ __device__ __forceinline__ unsigned xcc_id() {
   return x & 0xFu;
 }
 
+// Group formation of the packed kernels by PLACEMENT, not by block index (round 5).  group_of assumes
+// blocks b and b + 8 share an XCD -- true when a launch is dispatched alone, but a kernel dispatched
+// concurrently on another stream (the side-stream GEMM, RCCL kernels) interleaves its workgroups into the
+// XCD round robin, the groups then span XCDs, and every hand-off of the launch goes write-through and
+// cross-XCD: the BPTT ran at twice its time (662 vs 336 us per launch).  Here each workgroup takes a slot
+// on a per-XCD counter (device-scope atomic, returning): slot s < cap = NG * ngroups / 8 of XCD x is
+// member s % NG of group x * ngroups / 8 + s / NG -- every group on one XCD whatever the dispatch order.
+// A workgroup past its XCD's cap waits until every workgroup has taken a slot (the sum of the counters
+// reaches the grid: all are co-resident, the plan guarantees it), then takes the ov-th unfilled (group,
+// member) in XCD order.  Roles never depend on results, so the arithmetic is bitwise the same.
+// ctl: 9 zeroed words (8 per-XCD counters, 1 overflow counter); smem: 2 words of scratch LDS.
+__device__ __forceinline__ void group_pk(unsigned* ctl, int NG, int ngroups, unsigned limit, int* status, float* smem,
+                                         int& group, int& w) {
+  if (ctl == nullptr || (ngroups & 7) != 0) {
+    group_of(blockIdx.x, NG, ngroups, group, w);
+    return;
+  }
+  int* sg = reinterpret_cast<int*>(smem);
+  if (threadIdx.x == 0) {
+    const int per = ngroups >> 3, cap = per * NG, nwg = ngroups * NG;
+    const unsigned x = xcc_id() & 7u;
+    const int slot = (int)__hip_atomic_fetch_add(ctl + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int g = -1, m = 0;
+    if (slot < cap) {
+      g = (int)x * per + slot / NG;
+      m = slot % NG;
+    } else {
+      const int ov = (int)__hip_atomic_fetch_add(ctl + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned c[8];
+      unsigned spins = 0;
+      while (true) {
+        int tot = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          c[i] = __hip_atomic_load(ctl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tot += (int)c[i];
+        }
+        if (tot >= nwg) break;
+        if (++spins > limit) {
+          atomicOr(status, 8);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      int k = ov;
+      for (int i = 0; i < 8 && g < 0; ++i) {
+        const int filled = min((int)c[i], cap), holes = cap - filled;
+        if (k < holes) {
+          g = i * per + (filled + k) / NG;
+          m = (filled + k) % NG;
+        }
+        k -= holes;
+      }
+      if (g < 0) group_of(blockIdx.x, NG, ngroups, g, m);  // timed out (status 8): any role, results invalid
+    }
+    sg[0] = g;
+    sg[1] = m;
+  }
+  __syncthreads();
+  group = sg[0];
+  w = sg[1];
+  __syncthreads();  // the scratch words are reused by the kernel's own LDS
+}
+
 // Placement check at launch start (packed kernels).  A group's hand-off granules may be
 // written with PLAIN stores only when every workgroup of the group runs on one XCD: a plain
 // store stays in that XCD's L2, which serves the peers' `sc1` polls (MI355X_MICROARCH.md,
@@ -647,8 +712,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const int R = NGATE * J;
   const int MT = (R + 15) / 16;
   const int ngroups = 2 * a.nchunk;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   int group, w;
-  group_of(blockIdx.x, NG, ngroups, group, w);
+  group_pk(a.gctl, NG, ngroups, a.spin_limit, a.status, smem, group, w);
   const int d = group / a.nchunk, chunk = group % a.nchunk;
   const int b0 = chunk * BC;
   const int j0 = w * J;
@@ -666,7 +732,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   const bool mvh = t4h && (wv == WPOLL || wv == 7);
   const int SGS = MT * 16 + 4;  // sgate row stride (floats): 4 batch rows on 4 distinct bank quads
 
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   // h B image [16][SHB]: rows 0..BC-1 are the gathered h, row BC stays zero and every MFMA lane
   // of a row >= BC reads it (one broadcast address instead of 15 - BC zero rows: the matvec's B
   // reads are conflict-free, tools/lds_banks.py)
@@ -1591,8 +1656,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   const int H = a.H, T = a.T, J = a.J, NG = a.NG;
   const int R = NGATE * J;
   const int ngroups = 2 * a.nchunk;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   int group, w;
-  group_of(blockIdx.x, NG, ngroups, group, w);
+  group_pk(a.gctl, NG, ngroups, a.spin_limit, a.status, smem, group, w);
   const int d = group / a.nchunk, chunk = group % a.nchunk;
   const int b0 = chunk * BC;
   const int j0 = w * J;
@@ -1602,7 +1668,6 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   const int AH = 4 * H;
   const int HG = ((H + 1) / 2 + 1) & ~1;  // granules per (producer, row), even: 16-B aligned rows
 
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   unsigned short* sdgb = reinterpret_cast<unsigned short*>(smem);  // [16][SDG] bf16 dgh B image
   float* sdh = smem + 8 * SDG;                                      // [16][BC][J] gathered partials (rows >= NG stay 0)
   float* wsc = sdh + ((16 * BC * J + 3) & ~3);                      // [4 waves][BC][WSP]
@@ -2404,8 +2469,11 @@ static long long handoff_bytes(const Plan& p, int H) {
   const long long bwd_pk = groups * 4LL * p.NG * p.BC * (((H + 1) / 2 + 1) & ~1) * 8;
   if (bwd_pk > bwd) bwd = bwd_pk;
   const long long n = fwd > bwd ? fwd : bwd;
-  return (n + 255) / 256 * 256;
+  return (n + 255) / 256 * 256 + 256;  // + the group-formation counters (ctl_offset)
 }
+
+// the packed kernels' group-formation counters: the last 256 B of the hand-off area (group_pk)
+static long long ctl_offset(const Plan& p, int H) { return handoff_bytes(p, H) - 256; }
 
 // Polls a hand-off may spin before it times out (sets *status and the polling wave exits;
 // the launch still completes).  0 restores the default (SPIN_LIMIT, ~1 s).  Test hook: a
@@ -2493,6 +2561,7 @@ DL4SS_API int dl4ss_birnn_fwd_mean(int cell, int precision, int B, int T, int H,
   DL4SS_REQUIRE(pk || (out && !h_mean));  // the optional output and the fused mean are the packed kernel's
   if (!prezeroed) {
     hipError_t e = hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.BC * p.NG * 8 * 8 : groups * 2 * p.BC * H * 8, st);
+    if (e == hipSuccess && pk) e = hipMemsetAsync(static_cast<char*>(workspace) + ctl_offset(p, H), 0, 256, st);
     if (e != hipSuccess) return (int)e;
   }
   // the bf16 copies, and dropping the fp32 h_{t-1} (only the GRU BPTT reads it), need the packed kernel
@@ -2506,6 +2575,7 @@ DL4SS_API int dl4ss_birnn_fwd_mean(int cell, int precision, int B, int T, int H,
   a.outb = reinterpret_cast<unsigned short*>(out_bf16);
   a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
+  a.gctl = pk ? reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ctl_offset(p, H)) : nullptr;
   a.status = status;
   const int grid = (int)(groups * p.NG);
   const size_t smem = pk ? p.smem_fwd_pk : mf ? p.smem_fwd_mf : p.smem_fwd;
@@ -2566,6 +2636,7 @@ DL4SS_API int dl4ss_birnn_fwd_xw_ex(int cell, int B, int T, int H, const void* x
   const long long groups = 2LL * p.nchunk;
   if (!ws_zeroed) {
     hipError_t e = hipMemsetAsync(workspace, 0, groups * 4 * p.BC * p.NG * 8 * 8, st);
+    if (e == hipSuccess) e = hipMemsetAsync(static_cast<char*>(workspace) + ctl_offset(p, H), 0, 256, st);
     if (e != hipSuccess) return (int)e;
   }
   RnnArgs a{};
@@ -2576,6 +2647,7 @@ DL4SS_API int dl4ss_birnn_fwd_xw_ex(int cell, int B, int T, int H, const void* x
   a.outb = reinterpret_cast<unsigned short*>(out_bf16);
   a.hprevb = reinterpret_cast<unsigned short*>(hprev_bf16);
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
+  a.gctl = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ctl_offset(p, H));
   a.status = status;
   a.Xb = reinterpret_cast<const unsigned short*>(x_bf16);
   a.Wihb = reinterpret_cast<const unsigned short*>(W_ih_bf16);
@@ -2631,6 +2703,7 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   if (!prezeroed) {
     hipError_t e =
         hipMemsetAsync(workspace, 0, pk ? groups * 4 * p.NG * p.BC * HG * 8 : groups * 2 * p.NG * p.BC * H * 8, st);
+    if (e == hipSuccess && pk) e = hipMemsetAsync(static_cast<char*>(workspace) + ctl_offset(p, H), 0, 256, st);
     if (e != hipSuccess) return (int)e;
   }
   // bf16 gradient copies, dropping the fp32 ones and the fused bias sums need the packed kernel
@@ -2644,6 +2717,7 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   a.ghb = dgh_pad8 ? (GHc + 7) / 8 * 8 : GHc;
   a.dbi = db_ih; a.dbh = db_hh;
   a.xbuf = reinterpret_cast<unsigned long long*>(workspace);
+  a.gctl = pk ? reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ctl_offset(p, H)) : nullptr;
   const bool bias = pk && (db_ih || db_hh);
   a.dbpart = bias ? reinterpret_cast<float*>(static_cast<char*>(workspace) + handoff_bytes(p, H)) : nullptr;
   a.status = status;

@@ -257,6 +257,7 @@ class SepTrainer:
         self.side = None
         self._side_stream = None
         self._side_gemm = None
+        self._side_early = os.environ.get("DL4SS_SIDE_EARLY", "0") == "1"  # A/B knob: GEMM forked before dH
         side = os.environ.get("DL4SS_SIDE_DWLIN", "")
         if self.fast and net.L <= 5 and side != "0" and dev.type == "cuda":
             if side and side != "1":
@@ -588,10 +589,13 @@ class SepTrainer:
                       _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
                       self.colsum_part.numel() * 4, st)
 
-    def _side_launch(self):
-        """Fork: the side stream waits for the work enqueued so far on the current stream, then zeroes
-        the flat gradient, runs the query backward (event _ev_q: dh_bcast ready), and the persistent
-        dW_lin (+ bias row sums) launch -- beside the dH GEMM and the BPTT chain."""
+    def _side_launch(self, pre=True, gemm=True):
+        """Fork: the side stream waits for the work enqueued so far on the current stream, then (pre)
+        zeroes the flat gradient and runs the query backward (event _ev_q: dh_bcast ready) -- beside the
+        dH GEMM -- and (gemm) the persistent dW_lin (+ bias row sums) launch beside the BPTT chain.
+        The GEMM is forked after the dH GEMM: started beside it, its 16 workgroups took their CUs while
+        dH's workgroups filled the chip, and the BPTTs that ran beside it took twice as long (662 vs
+        336 us per launch, profiles/r05_prof_a notes) -- placed on an idle chip they do not slow them."""
         net, B, T, H = self.net, self.B, self.T, self.net.H
         g = net.grad
         FE = self.F * net.E
@@ -606,14 +610,16 @@ class SepTrainer:
                 net.device, grid=grid, cfg=cfg, one_per_cu=one)
         self._side_stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._side_stream):
-            g.zero_()
-            self._query_bwd()
-            self._ev_q.record()
-            if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
-                _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
-                          _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
-                          self.colsum_part.numel() * 4, _lib.stream_ptr())
-            self._side_gemm.run()
+            if pre:
+                g.zero_()
+                self._query_bwd()
+                self._ev_q.record()
+            if gemm:
+                if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
+                    _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
+                              _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
+                              self.colsum_part.numel() * 4, _lib.stream_ptr())
+                self._side_gemm.run()
 
     def _side_join(self):
         """Join: the current stream waits for the side stream's work."""
@@ -694,9 +700,11 @@ class SepTrainer:
             # beside the dH GEMM; the BPTT chain waits only for the query backward's dh_bcast
             # (bucketed data parallel: step() / step_graph() fork it, with the early all-reduce)
             if not self.buckets:
-                self._side_launch()
+                self._side_launch(gemm=self._side_early)
             self._backward_fast_early()
             if not self.buckets:
+                if not self._side_early:
+                    self._side_launch(pre=False)
                 torch.cuda.current_stream().wait_event(self._ev_q)
             return
         g.zero_()

@@ -203,3 +203,57 @@ def test_captured_trainer_freed_by_refcount(dev):
     finally:
         if was:
             gc.enable()
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_recurrence_beside_concurrent_persistent_kernel(dev, cell):
+    """A persistent GEMM dispatched on another stream at the same time as the recurrence (the
+    side-stream dW_lin; RCCL kernels under data parallelism) interleaves its workgroups into the XCD
+    round robin.  The packed kernels form their groups by placement (group_pk: per-XCD slot counters),
+    so the roles change but never the arithmetic: forward outputs and BPTT gradients bitwise equal to
+    the recurrence run alone, no hand-off timeout."""
+    B, T, H = 32, 64, 300
+    ng = 4 if cell == "lstm" else 3
+    NGH = ng * H
+    g = torch.Generator().manual_seed(3)
+    G = (torch.randn(B, T, 2, NGH, generator=g) * 0.5).to(dev)
+    whh = (torch.randn(2, NGH, H, generator=g) / H ** 0.5).to(dev)
+    bhh = (torch.randn(2, NGH, generator=g) * 0.1).to(dev)
+    gout = torch.randn(B, T, 2 * H, generator=g).to(dev)
+    cellid = 0 if cell == "lstm" else 1
+    ws = _lib.query("dl4ss_birnn_workspace_bytes", cellid, B, H)
+    # the side GEMM: 16 persistent 256 x 128 workgroups over a long-K problem
+    A = ops.to_bf16(torch.randn(8192, 2048, generator=g).to(dev))
+    Bm = ops.to_bf16(torch.randn(8192, 512, generator=g).to(dev))
+    C = torch.zeros(2048, 512, device=dev)
+    side = ops.GroupedGemm([dict(A=A, B=Bm, out=C, transA=True, transB=False, beta=0.0, splitk=1)], dev, grid=16,
+                           cfg=2)
+    stream = torch.cuda.Stream(device=dev)
+    res = []
+    for concurrent in (False, True, True):
+        o = torch.empty(B, T, 2 * H, device=dev)
+        hp = torch.empty_like(o)
+        act = torch.empty(B, T, 2, 4 * H, device=dev)
+        cs = torch.empty(B, T, 2, H, device=dev)
+        dG = torch.zeros(B * T, 2 * NGH, device=dev)
+        dGh = torch.zeros_like(dG)
+        wsb = torch.zeros((ws + 7) // 8, dtype=torch.int64, device=dev)
+        st = torch.zeros(1, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        if concurrent:
+            stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(stream):
+                side.run()
+        _lib.call("dl4ss_birnn_fwd", cellid, 1, B, T, H, _lib.ptr(G), _lib.ptr(whh), _lib.ptr(bhh), _lib.ptr(o),
+                  _lib.ptr(hp), _lib.ptr(act), _lib.ptr(cs), _lib.ptr(wsb), ws, _lib.ptr(st), _lib.stream_ptr())
+        if concurrent:
+            with torch.cuda.stream(stream):
+                side.run()
+        _lib.call("dl4ss_birnn_bwd", cellid, 1, B, T, H, _lib.ptr(gout), None, _lib.ptr(whh), _lib.ptr(act),
+                  _lib.ptr(cs), _lib.ptr(hp), _lib.ptr(dG), _lib.ptr(dGh), _lib.ptr(wsb), ws, _lib.ptr(st),
+                  _lib.stream_ptr())
+        torch.cuda.synchronize()
+        assert int(st.item()) == 0
+        res.append((o, dG, dGh))
+    for o, dG, dGh in res[1:]:
+        assert torch.equal(o, res[0][0]) and torch.equal(dG, res[0][1]) and torch.equal(dGh, res[0][2])
