@@ -257,7 +257,6 @@ class SepTrainer:
         self.side = None
         self._side_stream = None
         self._side_gemm = None
-        self._side_early = os.environ.get("DL4SS_SIDE_EARLY", "0") == "1"  # A/B knob: GEMM forked before dH
         side = os.environ.get("DL4SS_SIDE_DWLIN", "")
         if self.fast and net.L <= 5 and side != "0" and dev.type == "cuda":
             if side and side != "1":
@@ -588,21 +587,24 @@ class SepTrainer:
             _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                       _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
                       self.colsum_part.numel() * 4, st)
+        elif not self.buckets:  # (bucketed: _early_bucket forks it, with the early all-reduce)
+            self._side_launch()
 
-    def _side_launch(self, pre=True, gemm=True):
-        """Fork: the side stream waits for the work enqueued so far on the current stream, then (pre)
-        zeroes the flat gradient and runs the query backward (event _ev_q: dh_bcast ready) -- beside the
-        dH GEMM -- and (gemm) the persistent dW_lin (+ bias row sums) launch beside the BPTT chain.
-        The GEMM is forked after the dH GEMM: started beside it, its 16 workgroups took their CUs while
-        dH's workgroups filled the chip, and the BPTTs that ran beside it took twice as long (662 vs
-        336 us per launch, profiles/r05_prof_a notes) -- placed on an idle chip they do not slow them."""
+    def _side_launch(self):
+        """Fork: the side stream waits for the work enqueued so far on the current stream (the dH
+        GEMM last), then runs the persistent dW_lin (+ bias row sums) launch beside the BPTT chain.
+        Measured alternatives (tools/ab_bench.sh, C2, round 5): moving the gradient zeroing and the
+        query backward onto the side stream too (beside the dH GEMM, the chain waiting on an event
+        for dh_bcast) made the two BPTTs that ran beside the side GEMM take twice as long (665 vs
+        338 us per launch; step 4.11 vs 3.51 ms), with or without a delay before the side GEMM and
+        with the recurrence's groups formed by placement (group_pk) -- so they stay on the main
+        stream, before dH."""
         net, B, T, H = self.net, self.B, self.T, self.net.H
         g = net.grad
         FE = self.F * net.E
         if self._side_stream is None:
             grid, cfg, split, one = self.side
             self._side_stream = torch.cuda.Stream(device=net.device)
-            self._ev_q = torch.cuda.Event()
             self._side_gemm = ops.GroupedGemm(
                 [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
                       transA=True, transB=False, beta=1.0, splitk=split,
@@ -610,16 +612,11 @@ class SepTrainer:
                 net.device, grid=grid, cfg=cfg, one_per_cu=one)
         self._side_stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._side_stream):
-            if pre:
-                g.zero_()
-                self._query_bwd()
-                self._ev_q.record()
-            if gemm:
-                if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
-                    _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
-                              _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
-                              self.colsum_part.numel() * 4, _lib.stream_ptr())
-                self._side_gemm.run()
+            if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
+                _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
+                          _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
+                          self.colsum_part.numel() * 4, _lib.stream_ptr())
+            self._side_gemm.run()
 
     def _side_join(self):
         """Join: the current stream waits for the side stream's work."""
@@ -695,18 +692,6 @@ class SepTrainer:
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         g = net.grad
-        if self.fast and self.side:
-            # the gradient zeroing, the query backward and the Linear's gradients on the side stream,
-            # beside the dH GEMM; the BPTT chain waits only for the query backward's dh_bcast
-            # (bucketed data parallel: step() / step_graph() fork it, with the early all-reduce)
-            if not self.buckets:
-                self._side_launch(gemm=self._side_early)
-            self._backward_fast_early()
-            if not self.buckets:
-                if not self._side_early:
-                    self._side_launch(pre=False)
-                torch.cuda.current_stream().wait_event(self._ev_q)
-            return
         g.zero_()
         self._query_bwd()
         if self.fast:
@@ -805,7 +790,6 @@ class SepTrainer:
             self._side_launch()
             with torch.cuda.stream(self._side_stream):
                 self.allreduce_early()
-            torch.cuda.current_stream().wait_event(self._ev_q)  # the BPTT chain needs dh_bcast
         else:
             self.allreduce_early()
 
