@@ -22,6 +22,7 @@ U = ctypes.c_uint
 # name -> argtypes (all return int hipError_t)
 SIGNATURES = {
     "dl4ss_stft_fwd": [P, LL, I, I, I, I, P, P, P],
+    "dl4ss_stft_fwd_ex": [P, LL, I, I, I, I, P, P, P, LL, LL, P],
     "dl4ss_istft": [P, LL, I, I, I, I, P, P],
     "dl4ss_mix_sources": [P, P, I, I, I, P, P, P, P],
     "dl4ss_gemm": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, P],
@@ -29,9 +30,11 @@ SIGNATURES = {
     "dl4ss_f32_to_bf16_2d": [P, LL, I, I, P, LL, P],
     "dl4ss_f32_to_bf16_hilo": [P, LL, I, I, P, LL, I, I, U, P],
     "dl4ss_birnn_bias_reduce": [I, I, I, I, P, P, P, P],
+    "dl4ss_birnn_bias_reduce_ex": [I, I, I, I, P, P, P, F, P],
     "dl4ss_colsum_bf16": [P, LL, I, I, P, P],
     "dl4ss_colsum_bf16_part_bytes": [I, I],
     "dl4ss_colsum_bf16_det": [P, LL, I, I, P, P, LL, P],
+    "dl4ss_colsum_bf16_det_ex": [P, LL, I, I, P, P, LL, F, P],
     "dl4ss_gemm_bf16_gl_ws_bytes": [I, I, I, I, I],
     "dl4ss_gemm_gl_set_config": [I],
     "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
@@ -54,6 +57,7 @@ SIGNATURES = {
     "dl4ss_loss_finalize": [P, I, I, I, P, F, F, P, P, I, P, P],
     "dl4ss_query_fwd": [P, I, I, I, P, P, P, I, I, P, P, P],
     "dl4ss_query_bwd": [P, I, I, I, P, P, P, P, I, I, P, P, P, P],
+    "dl4ss_query_bwd_ex": [P, I, I, I, P, P, P, P, I, I, P, P, P, I, F, P],
     "dl4ss_colsum": [P, LL, I, I, P, P],
     "dl4ss_adam": [P, P, P, P, LL, F, F, F, F, I, P],
     "dl4ss_istft_apply": [P, P, LL, I, I, I, I, P, P],
@@ -75,6 +79,7 @@ SIGNATURES = {
     "dl4ss_adam_guarded": [P, P, P, P, LL, F, F, F, F, I, P, P, P],
     "dl4ss_adam_guarded_dp": [P, P, P, P, LL, F, F, F, F, I, P, P, P, P],
     "dl4ss_adam_guarded_dp_scaled": [P, P, P, P, LL, F, F, F, F, I, P, P, F, P, P],
+    "dl4ss_adam_guarded_dp_scaled_bf16": [P, P, P, P, LL, F, F, F, F, I, P, P, F, P, I, P, P, P, P, P, P],
     "dl4ss_status_flag": [P, P, P],
     "dl4ss_birnn_plan_info": [I, I, I, I, I, P],
     "dl4ss_debug_set_spin_limit": [ctypes.c_uint],

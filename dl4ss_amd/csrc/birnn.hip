@@ -616,7 +616,8 @@ __device__ __forceinline__ unsigned xcc_id() {
 // A workgroup past its XCD's cap waits until every workgroup has taken a slot (the sum of the counters
 // reaches the grid: all are co-resident, the plan guarantees it), then takes the ov-th unfilled (group,
 // member) in XCD order.  Roles never depend on results, so the arithmetic is bitwise the same.
-// ctl: 9 zeroed words (8 per-XCD counters, 1 overflow counter); smem: 2 words of scratch LDS.
+// ctl: 10 zeroed words (8 per-XCD counters, 1 overflow counter, the release_start count); smem: 2
+// words of scratch LDS.
 __device__ __forceinline__ void group_pk(unsigned* ctl, int NG, int ngroups, unsigned limit, int* status, float* smem,
                                          int& group, int& w) {
   if (ctl == nullptr || (ngroups & 7) != 0) {
@@ -668,6 +669,27 @@ __device__ __forceinline__ void group_pk(unsigned* ctl, int NG, int ngroups, uns
   group = sg[0];
   w = sg[1];
   __syncthreads();  // the scratch words are reused by the kernel's own LDS
+}
+
+// Workspace reuse without a zero fill (round 5).  The packed kernels' hand-off granules need no
+// clearing between launches of the same shape: a consumer polls slot (s-1)&1 for tag s at step s
+// and a completed launch leaves tags T and T-1 behind, which only steps 1 and 2 could see before
+// this launch overwrites them -- never equal for T >= 4 (tags are (step + 1) mod 2^16, T < 65535).
+// The group-formation counters and the placement granules {tag 1, XCC id} are what a fill was
+// for: the LAST workgroup past the start (all have formed their groups and read the placement by
+// then) puts them back to zero.  ctl word 9 counts the workgroups past the start.
+// place_stride: u64 between groups' granule blocks; place_off: the placement granules' offset.
+__device__ __forceinline__ void release_start(unsigned* ctl, u64* xbuf, int ngroups, int NG, long long place_stride,
+                                              long long place_off) {
+  if (ctl == nullptr) return;
+  // relaxed: this workgroup's reads of the counters and placement granules completed before the
+  // startup barrier (their values were used); an acq_rel RMW would write back / invalidate the L2
+  const unsigned k = __hip_atomic_fetch_add(ctl + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int)k != ngroups * NG - 1) return;
+  for (int g = 0; g < ngroups; ++g)
+    for (int m = 0; m < NG; ++m)
+      __hip_atomic_store(xbuf + g * place_stride + place_off + m, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = 0; i < 10; ++i) __hip_atomic_store(ctl + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Placement check at launch start (packed kernels).  A group's hand-off granules may be
@@ -908,6 +930,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   }
   __syncthreads();
   const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
+  if (tid == 0) release_start(a.gctl, a.xbuf, ngroups, NG, 4LL * slot_g, 3LL * slot_g);
   STAMP_DECL
 
   // XW: G of block kb (steps kb*SPB .. +SPB-1) for this wave's tiles' rows: x W_ih^T as one
@@ -1241,7 +1264,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
       STAMP(6)
       if (tid == 0) TRACE(0, s);
 #ifndef FWD_EXP_SKIP
-#define FWD_EXP_SKIP 0  // timing experiments only (results wrong): skip saved-state stores, bits 1 act, 2 cs, 4 out, 8 outb, 16 hprevb
+#define FWD_EXP_SKIP 0  // timing experiments only (results wrong): skip saved-state stores, bits 1 act, 2 cs, 4 out, 8 outb, 16 hprevb, 32 hprev
 #endif
       if (cval) {
         const long long bt = (long long)bg * T + t;
@@ -1254,7 +1277,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         }
         if constexpr (CELL == CELL_LSTM) if (!(FWD_EXP_SKIP & 2)) a.cs[(bt * 2 + d) * H + cj] = cst;
         const long long ho = bt * 2 * H + d * H + cj;
-        if (a.hprev) a.hprev[ho] = hst;
+        if (a.hprev && !(FWD_EXP_SKIP & 32)) a.hprev[ho] = hst;
         if (a.out && !(FWD_EXP_SKIP & 4)) a.out[ho] = hn;
         hsum += hn;
         // bf16 copies, 16-B aligned rows for the GEMMs: out_bf16 (B*T, pad8(2H)) with the
@@ -1830,6 +1853,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   }
   __syncthreads();
   const bool wt = __builtin_amdgcn_readfirstlane(s_wt) != 0;  // granules written through (group spans XCDs)
+  if (tid == 0) release_start(a.gctl, a.xbuf, ngroups, NG, 4LL * copy_g, 3LL * copy_g);
   STAMP_DECL
 
   if (wv >= WPOLL && wv < WPF) {
@@ -2411,6 +2435,7 @@ DL4SS_API void dl4ss_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<uns
 constexpr int BIAS_JOBS_MAX = 8;
 struct BiasJobs {
   int n, B, GH;
+  float beta;  // db = beta db + sums (beta 0: written, not read)
   const float* part[BIAS_JOBS_MAX];
   float* dbi[BIAS_JOBS_MAX];
   float* dbh[BIAS_JOBS_MAX];
@@ -2445,8 +2470,8 @@ __global__ __launch_bounds__(256) void bias_reduce_kernel(BiasJobs j) {
         sh += vh[u];
       }
   }
-  if (dbi) dbi[i] += si;
-  if (dbh) dbh[i] += sh;
+  if (dbi) dbi[i] = j.beta != 0.f ? si + j.beta * dbi[i] : si;
+  if (dbh) dbh[i] = j.beta != 0.f ? sh + j.beta * dbh[i] : sh;
 }
 
 // hand-off area of the BPTT / forward workspace, 256-B aligned
@@ -2728,7 +2753,7 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   if (e || !bias || defer_bias) return e;
   const int GH = (cell == CELL_LSTM ? 4 : 3) * H;
   BiasJobs j{};
-  j.n = 1; j.B = B; j.GH = GH; j.part[0] = a.dbpart; j.dbi[0] = db_ih; j.dbh[0] = db_hh;
+  j.n = 1; j.B = B; j.GH = GH; j.beta = 1.f; j.part[0] = a.dbpart; j.dbi[0] = db_ih; j.dbh[0] = db_hh;
   hipLaunchKernelGGL(bias_reduce_kernel, dim3((2 * GH + 255) / 256, 1), dim3(256), 0, st, j);
   return (int)hipGetLastError();
 }
@@ -2736,15 +2761,15 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
 // The deferred form: the bias partials of n BPTT launches (DL4SS_RNN_DEFER_BIAS) reduced by ONE
 // launch after the last of them -- the per-layer reduce was a 5 us latency-bound launch between
 // each BPTT and the input-gradient GEMM that the next BPTT waits on.
-DL4SS_API int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
-                                      float* const* db_hh, void* stream) {
+DL4SS_API int dl4ss_birnn_bias_reduce_ex(int cell, int B, int H, int n, void* const* workspaces,
+                                         float* const* db_ih, float* const* db_hh, float beta, void* stream) {
   DL4SS_REQUIRE((cell == CELL_LSTM || cell == CELL_GRU) && B > 0 && H > 0 && n >= 1 && n <= BIAS_JOBS_MAX);
   DL4SS_REQUIRE(workspaces && db_ih && db_hh);
   Plan p;
   if (!make_plan(cell, B, H, p, true)) return (int)hipErrorInvalidValue;  // the bf16 BPTT's plan
   const int GH = (cell == CELL_LSTM ? 4 : 3) * H;
   BiasJobs j{};
-  j.n = n; j.B = B; j.GH = GH;
+  j.n = n; j.B = B; j.GH = GH; j.beta = beta;
   for (int i = 0; i < n; ++i) {
     DL4SS_REQUIRE(workspaces[i] && db_ih[i] && db_hh[i]);
     j.part[i] = reinterpret_cast<const float*>(static_cast<const char*>(workspaces[i]) + handoff_bytes(p, H));
@@ -2754,4 +2779,9 @@ DL4SS_API int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const
   hipLaunchKernelGGL(bias_reduce_kernel, dim3((2 * GH + 255) / 256, n), dim3(256), 0, as_stream(stream), j);
   DL4SS_CHECK_LAUNCH();
   return 0;
+}
+
+DL4SS_API int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
+                                      float* const* db_hh, void* stream) {
+  return dl4ss_birnn_bias_reduce_ex(cell, B, H, n, workspaces, db_ih, db_hh, 1.f, stream);
 }

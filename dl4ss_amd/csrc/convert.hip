@@ -150,12 +150,12 @@ __global__ __launch_bounds__(256) void colsum_bf16_v_kernel(const unsigned short
 
 // out[n] += sum_{y < nby} part[y][n], y in order (the deterministic colsum's second pass)
 __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int nby, int N,
-                                                            float* __restrict__ out) {
+                                                            float* __restrict__ out, float beta) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
   float a = 0.f;
   for (int y = 0; y < nby; ++y) a += part[(long long)y * N + n];
-  out[n] += a;
+  out[n] = beta != 0.f ? a + beta * out[n] : a;  // beta 0: out is not read (the step's unzeroed gradient)
 }
 
 // Split-precision operand images: x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (|lo| <= 2^-9 |x|,
@@ -212,7 +212,8 @@ DL4SS_API int dl4ss_f32_to_bf16_2d(const float* x, long long ldx, int rows, int 
   return 0;
 }
 
-static int colsum_bf16_launch(const void* A, long long lda, int M, int N, float* out, float* part, void* stream) {
+static int colsum_bf16_launch(const void* A, long long lda, int M, int N, float* out, float* part, void* stream,
+                              float beta = 1.f) {
   const int rpb = 256;
   const auto* a = reinterpret_cast<const unsigned short*>(A);
   if (lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && lda >= ((N + 7) & ~7))  // 16-B rows, padding readable
@@ -224,7 +225,7 @@ static int colsum_bf16_launch(const void* A, long long lda, int M, int N, float*
   DL4SS_CHECK_LAUNCH();
   if (part) {
     hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cdiv(N, 256)), dim3(256), 0, as_stream(stream), part, cdiv(M, rpb), N,
-                       out);
+                       out, beta);
     DL4SS_CHECK_LAUNCH();
   }
   return 0;
@@ -249,6 +250,19 @@ DL4SS_API int dl4ss_colsum_bf16_det(const void* A, long long lda, int M, int N, 
   if (M == 0 || N == 0) return 0;
   DL4SS_REQUIRE(part && part_bytes >= dl4ss_colsum_bf16_part_bytes(M, N));
   return colsum_bf16_launch(A, lda, M, N, out, part, stream);
+}
+
+// dl4ss_colsum_bf16_det with out = beta out + sums (beta 0: out is written without being read)
+DL4SS_API int dl4ss_colsum_bf16_det_ex(const void* A, long long lda, int M, int N, float* out, float* part,
+                                       long long part_bytes, float beta, void* stream) {
+  DL4SS_REQUIRE(A && out && M >= 0 && N >= 0);
+  if (N == 0) return 0;
+  if (M == 0) {  // an empty sum: out = beta out (beta 0: zeros)
+    DL4SS_REQUIRE(beta == 0.f || beta == 1.f);
+    return beta == 0.f ? (int)hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, as_stream(stream)) : 0;
+  }
+  DL4SS_REQUIRE(part && part_bytes >= dl4ss_colsum_bf16_part_bytes(M, N));
+  return colsum_bf16_launch(A, lda, M, N, out, part, stream, beta);
 }
 
 DL4SS_API int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ldx, const int* rows,

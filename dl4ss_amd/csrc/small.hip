@@ -118,7 +118,7 @@ __device__ __forceinline__ void query_bwd_dh(int bx, int by, const float* __rest
 // batch gets the same bits on every run)
 __device__ __forceinline__ void query_bwd_emb(int bk, const float* __restrict__ dq, const int* __restrict__ idx,
                                               int BK, const float* __restrict__ wadj, int D, int W,
-                                              float* __restrict__ demb) {
+                                              float* __restrict__ demb, float beta) {
   const int id = idx[bk];
   if (id < 0) return;
   for (int j = 0; j < bk; ++j)
@@ -137,14 +137,15 @@ __device__ __forceinline__ void query_bwd_emb(int bk, const float* __restrict__ 
       }
       acc += g;
     }
-    demb[(long long)id * W + c] += acc;
+    float* o = demb + (long long)id * W + c;
+    *o = beta != 0.f ? acc + beta * *o : acc;  // beta 0: the row is written without being read
   }
 }
 
 __device__ __forceinline__ void query_bwd_w(int bx, int by, float* sm, const float* __restrict__ dq,
                                             const int* __restrict__ idx, const float* __restrict__ emb,
                                             const float* __restrict__ mean, int B, int D, int K, int W,
-                                            float* __restrict__ dwadj) {
+                                            float* __restrict__ dwadj, float beta) {
   // block (column chunk, o): the o-th dq column (and its per-utterance sums u) and the
   // speaker ids staged in LDS, then 8 independent loads in flight per thread
   float* sdq = sm;            // [B*K]  dq[bk][o]
@@ -187,7 +188,9 @@ __device__ __forceinline__ void query_bwd_w(int bx, int by, float* sm, const flo
         if (b0 + j < B * K) acc[j] = fmaf(sdq[b0 + j], e[j], acc[j]);
     }
   }
-  dwadj[(long long)o * (D + W) + c] += ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  const float sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  float* od = dwadj + (long long)o * (D + W) + c;
+  *od = beta != 0.f ? sum + beta * *od : sum;
 }
 
 // The three query backward parts as ONE launch (64-thread blocks, role by block range: the
@@ -204,21 +207,30 @@ struct QbArgs {
   float* dwadj;
   float* dh;
   int n_emb, n_dh_x, n_dh, n_w_x;
+  float beta;       // d_emb / d_wadj = beta (old) + this step's (beta 0: written, not read)
+  int n_zero;       // beta 0: embedding rows 0 .. n_zero-1 that no speaker of the batch owns are zeroed
 };
 __global__ __launch_bounds__(64) void query_bwd_kernel(QbArgs a) {
   extern __shared__ float sm[];
   int blk = blockIdx.x;
   if (blk < a.n_emb) {
-    query_bwd_emb(blk, a.dq, a.idx, a.B * a.K, a.wadj, a.D, a.W, a.demb);
+    query_bwd_emb(blk, a.dq, a.idx, a.B * a.K, a.wadj, a.D, a.W, a.demb, a.beta);
     return;
   }
   blk -= a.n_emb;
+  if (blk < a.n_zero) {  // (beta 0) embedding row blk: zero unless a speaker of the batch owns it
+    for (int j = 0; j < a.B * a.K; ++j)
+      if (a.idx[j] == blk) return;
+    for (int c = threadIdx.x; c < a.W; c += 64) a.demb[(long long)blk * a.W + c] = 0.f;
+    return;
+  }
+  blk -= a.n_zero;
   if (blk < a.n_dh) {
     query_bwd_dh(blk % a.n_dh_x, blk / a.n_dh_x, a.dq, a.wadj, a.T, a.D, a.K, a.W, a.dh);
     return;
   }
   blk -= a.n_dh;
-  query_bwd_w(blk % a.n_w_x, blk / a.n_w_x, sm, a.dq, a.idx, a.emb, a.mean, a.B, a.D, a.K, a.W, a.dwadj);
+  query_bwd_w(blk % a.n_w_x, blk / a.n_w_x, sm, a.dq, a.idx, a.emb, a.mean, a.B, a.D, a.K, a.W, a.dwadj, a.beta);
 }
 
 // out[n] (+)= sum_m A[m*lda + n]   (bias gradients); block = 64 columns x 4 row lanes
@@ -237,14 +249,60 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ A
   if (rl == 0 && c < N) atomicAdd(out + c, s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
 }
 
+// bf16 shadow copies written by the Adam update (the bf16 step's GEMM / recurrence operands): segment s
+// maps the flat range [off, off + rows*cols) row-major onto y[r * ldy + c] (columns >= cols untouched)
+constexpr int SHADOW_MAX = 8;
+struct ShadowSegs {
+  long long off[SHADOW_MAX], len[SHADOW_MAX], ldy[SHADOW_MAX];
+  int cols[SHADOW_MAX];
+  unsigned short* y[SHADOW_MAX];
+  int n;
+};
+__device__ __forceinline__ void shadow_store(const ShadowSegs& sh, long long i, float x) {
+#pragma unroll
+  for (int s = 0; s < SHADOW_MAX; ++s) {
+    if (s >= sh.n) break;
+    const long long j = i - sh.off[s];
+    if (j >= 0 && j < sh.len[s]) {
+      const unsigned r = (unsigned)j / (unsigned)sh.cols[s], c = (unsigned)j - r * (unsigned)sh.cols[s];
+      sh.y[s][r * sh.ldy[s] + c] = (unsigned short)bf16_bits_rne(x);
+      return;
+    }
+  }
+}
+// four consecutive flat elements i..i+3: one 8-B store when they sit in one row of one segment at
+// an 8-B aligned destination (the 600-column weights: every quad), else element by element
+__device__ __forceinline__ void shadow_store4(const ShadowSegs& sh, long long i, float4 x) {
+#pragma unroll
+  for (int s = 0; s < SHADOW_MAX; ++s) {
+    if (s >= sh.n) break;
+    const long long j = i - sh.off[s];
+    if (j + 3 < 0 || j >= sh.len[s]) continue;
+    if (j >= 0 && j + 3 < sh.len[s]) {
+      const unsigned r = (unsigned)j / (unsigned)sh.cols[s], c = (unsigned)j - r * (unsigned)sh.cols[s];
+      const long long o = r * sh.ldy[s] + c;
+      if (c + 3 < (unsigned)sh.cols[s] && (o & 3) == 0) {
+        const unsigned lo = bf16_bits_rne(x.x) | (bf16_bits_rne(x.y) << 16);
+        const unsigned hi = bf16_bits_rne(x.z) | (bf16_bits_rne(x.w) << 16);
+        *reinterpret_cast<uint2*>(sh.y[s] + o) = make_uint2(lo, hi);
+        return;
+      }
+    }
+    break;  // a quad across a row or segment boundary
+  }
+  shadow_store(sh, i, x.x); shadow_store(sh, i + 1, x.y); shadow_store(sh, i + 2, x.z); shadow_store(sh, i + 3, x.w);
+}
+
 // torch.optim.Adam (weight_decay 0, amsgrad off; m via lerp as torch) on flat fp32 buffers
-// (EvalVer.py:538-544,673-675: Adam(lr=2e-4), betas (0.9, 0.999), eps 1e-8)
+// (EvalVer.py:538-544,673-675: Adam(lr=2e-4), betas (0.9, 0.999), eps 1e-8).  SH: also the bf16
+// shadow copies of the updated parameters (bitwise dl4ss_f32_to_bf16_2d_multi of the new values)
+template <bool SH>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2s,
                                                    const int* __restrict__ status, int* __restrict__ refused,
                                                    const float* __restrict__ dp_flag, float gscale,
-                                                   float* __restrict__ loss) {
+                                                   float* __restrict__ loss, ShadowSegs sh) {
   // refuse the update when a recurrence hand-off of this step timed out on this rank
   // (status[0]) or on any data-parallel peer (dp_flag: the all-reduced status flag)
   if ((status && status[0]) || (dp_flag && dp_flag[0] != 0.f)) {
@@ -272,12 +330,16 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
       *reinterpret_cast<float4*>(p + i) = pp;
       *reinterpret_cast<float4*>(m + i) = mm;
       *reinterpret_cast<float4*>(v + i) = vv;
+      if constexpr (SH) {
+        shadow_store4(sh, i, pp);
+      }
     } else {
       for (long long j = i; j < n; ++j) {
         const float gj = g[j] * gscale;
         m[j] = m[j] + (1.f - b1) * (gj - m[j]);
         v[j] = b2 * v[j] + (1.f - b2) * gj * gj;
         p[j] -= step * (m[j] / (sqrtf(v[j]) / bc2s + eps));
+        if constexpr (SH) shadow_store(sh, j, p[j]);
       }
     }
   }
@@ -309,13 +371,14 @@ DL4SS_API int dl4ss_time_mean(const float* h, int B, int T, int D, float* mean_o
   return 0;
 }
 
-DL4SS_API int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* idx, const float* emb,
-                              const float* w_adj, const float* mean, int K, int W, float* d_emb, float* d_wadj,
-                              float* dh_bcast, void* stream) {
-  DL4SS_REQUIRE(dq && idx && B > 0 && K > 0 && W > 0);
+DL4SS_API int dl4ss_query_bwd_ex(const float* dq, int B, int T, int D, const int* idx, const float* emb,
+                                 const float* w_adj, const float* mean, int K, int W, float* d_emb, float* d_wadj,
+                                 float* dh_bcast, int n_labels, float beta, void* stream) {
+  DL4SS_REQUIRE(dq && idx && B > 0 && K > 0 && W > 0 && (beta != 0.f || !d_emb || n_labels > 0));
   hipStream_t st = as_stream(stream);
-  QbArgs a{dq, idx, emb, w_adj, mean, B, T, D, K, W, d_emb, d_wadj, dh_bcast, 0, 0, 0, 0};
+  QbArgs a{dq, idx, emb, w_adj, mean, B, T, D, K, W, d_emb, d_wadj, dh_bcast, 0, 0, 0, 0, beta, 0};
   a.n_emb = d_emb ? B * K : 0;
+  a.n_zero = (d_emb && beta == 0.f) ? n_labels : 0;
   a.n_dh_x = (int)cdiv(D, 64);
   a.n_dh = (w_adj && dh_bcast) ? a.n_dh_x * B : 0;
   a.n_w_x = (int)cdiv(D + W, 64);
@@ -326,11 +389,17 @@ DL4SS_API int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* i
     n_w = a.n_w_x * W;
     smem = sizeof(float) * (2 * (size_t)B * K + B);
   }
-  const int nblk = a.n_emb + a.n_dh + n_w;
+  const int nblk = a.n_emb + a.n_zero + a.n_dh + n_w;
   if (nblk == 0) return 0;
   hipLaunchKernelGGL(query_bwd_kernel, dim3(nblk), dim3(64), smem, st, a);
   DL4SS_CHECK_LAUNCH();
   return 0;
+}
+
+DL4SS_API int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* idx, const float* emb,
+                              const float* w_adj, const float* mean, int K, int W, float* d_emb, float* d_wadj,
+                              float* dh_bcast, void* stream) {
+  return dl4ss_query_bwd_ex(dq, B, T, D, idx, emb, w_adj, mean, K, W, d_emb, d_wadj, dh_bcast, 0, 1.f, stream);
 }
 
 DL4SS_API int dl4ss_colsum(const float* A, long long lda, int M, int N, float* out, void* stream) {
@@ -346,15 +415,19 @@ DL4SS_API int dl4ss_colsum(const float* A, long long lda, int M, int N, float* o
 namespace {
 int adam_launch(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
                 float eps, int step, const int* status, int* refused, const float* dp_flag, float gscale,
-                float* loss, void* stream) {
+                float* loss, void* stream, const ShadowSegs* sh = nullptr) {
   DL4SS_REQUIRE(p && g && m && v && n >= 0 && step >= 1);
   if (n == 0) return 0;
   // bias corrections in double on the host, as torch computes them in Python floats
   const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   const unsigned grid = (unsigned)min(8192LL, (n / 4 + 255) / 256 + 1);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr, beta1, beta2, eps,
-                     bc1, bc2s, status, refused, dp_flag, gscale, loss);
+  if (sh && sh->n > 0)
+    hipLaunchKernelGGL(adam_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr, beta1, beta2,
+                       eps, bc1, bc2s, status, refused, dp_flag, gscale, loss, *sh);
+  else
+    hipLaunchKernelGGL(adam_kernel<false>, dim3(grid), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr, beta1,
+                       beta2, eps, bc1, bc2s, status, refused, dp_flag, gscale, loss, ShadowSegs{});
   DL4SS_CHECK_LAUNCH();
   return 0;
 }
@@ -396,4 +469,31 @@ DL4SS_API int dl4ss_status_flag(const int* status, float* flag, void* stream) {
   hipLaunchKernelGGL(status_flag_kernel, dim3(1), dim3(64), 0, as_stream(stream), status, flag);
   DL4SS_CHECK_LAUNCH();
   return 0;
+}
+
+// dl4ss_adam_guarded_dp_scaled that also writes bf16 shadow copies of the updated parameters: segment
+// s (s < nseg <= 8) maps the flat range [seg_off, seg_off + rows*cols) row-major onto seg_y (row stride
+// seg_ldy >= cols bf16; columns >= cols are not written).  The step's bf16 weight operands then need
+// no conversion pass before the next forward (bitwise dl4ss_f32_to_bf16_2d_multi of the new values;
+// a refused update leaves parameters and shadows untouched).
+DL4SS_API int dl4ss_adam_guarded_dp_scaled_bf16(float* p, const float* g, float* m, float* v, long long n, float lr,
+                                                float beta1, float beta2, float eps, int step, int* status,
+                                                const float* dp_flag, float gscale, float* loss, int nseg,
+                                                const long long* seg_off, const int* seg_rows, const int* seg_cols,
+                                                void* const* seg_y, const long long* seg_ldy, void* stream) {
+  DL4SS_REQUIRE(nseg >= 0 && nseg <= SHADOW_MAX && (nseg == 0 || (seg_off && seg_rows && seg_cols && seg_y && seg_ldy)));
+  ShadowSegs sh{};
+  sh.n = nseg;
+  for (int i = 0; i < nseg; ++i) {
+    DL4SS_REQUIRE(seg_y[i] && seg_rows[i] >= 0 && seg_cols[i] > 0 && seg_ldy[i] >= seg_cols[i] && seg_off[i] >= 0 &&
+                  seg_off[i] + (long long)seg_rows[i] * seg_cols[i] <= n && (long long)seg_rows[i] * seg_cols[i] < (1LL << 31));
+    DL4SS_REQUIRE(((uintptr_t)seg_y[i] & 7) == 0);  // the 8-B quad stores
+    sh.off[i] = seg_off[i];
+    sh.len[i] = (long long)seg_rows[i] * seg_cols[i];
+    sh.cols[i] = seg_cols[i];
+    sh.ldy[i] = seg_ldy[i];
+    sh.y[i] = reinterpret_cast<unsigned short*>(seg_y[i]);
+  }
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, step, status, status ? status + 1 : nullptr, dp_flag, gscale,
+                     loss, stream, &sh);
 }

@@ -139,7 +139,8 @@ __device__ __forceinline__ void load_span(const float* __restrict__ x, int n_sam
 template <bool WC, bool WM, bool LOG, bool CONJ>
 __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restrict__ x, int n_samples, int T,
                                                           int tiles_per_sig, int n_tiles,
-                                                          float2* __restrict__ Xc, float* __restrict__ mag) {
+                                                          float2* __restrict__ Xc, float* __restrict__ mag,
+                                                          unsigned short* __restrict__ mb, long long ldb, int nbsig) {
   __shared__ float sw[NFFT];
   __shared__ float2 stw[NFFT];
   // transpose [pair][row][col ^ row] (XOR swizzle instead of padding), then Z[pair][256]
@@ -217,6 +218,9 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
     const int km = (NFFT - k) & (NFFT - 1);
     float2* xc = Xc + row0 + par * NBIN + k;
     float* xm = mag + row0 + par * NBIN + k;
+    // the bf16 copy of the magnitudes of signals < nbsig (the recurrence's first-layer input rows,
+    // row stride ldb): no conversion pass over the features (round 5)
+    unsigned short* xb = (WM && mb && sig < nbsig) ? mb + ((long long)sig * T + t0 + par) * ldb + k : nullptr;
     auto emit = [&](int it, float2 zk, float2 zm) {
       float2 X = par == 0 ? make_float2(zk.x + zm.x, zk.y - zm.y) : make_float2(zk.y + zm.y, zm.x - zk.x);
       if (CONJ) X.y = -X.y;
@@ -225,6 +229,7 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
         float m = __builtin_amdgcn_sqrtf(X.x * X.x + X.y * X.y);
         if (LOG) m = __logf(m + 2.220446049250313e-16f);
         xm[2 * it * NBIN] = m;
+        if (xb) xb[2 * it * ldb] = (unsigned short)bf16_bits_rne(m);
       }
     };
     if (nfr == FPT) {  // full tile: the LDS reads of four frames issued together
@@ -252,6 +257,7 @@ __global__ __launch_bounds__(256, 3) void stft_fwd_kernel(const float* __restric
         float m = fabsf(X.x);
         if (LOG) m = __logf(m + 2.220446049250313e-16f);
         mag[row0 + f * NBIN + 128] = m;
+        if (WM && mb && sig < nbsig) mb[((long long)sig * T + t0 + f) * ldb + 128] = (unsigned short)bf16_bits_rne(m);
       }
     }
   }
@@ -357,13 +363,15 @@ __global__ __launch_bounds__(256) void istft_kernel(const float2* __restrict__ S
 
 }  // namespace
 
-DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int n_fft, int hop, int flags,
-                             float* X_c64, float* mag, void* stream) {
+DL4SS_API int dl4ss_stft_fwd_ex(const float* x, long long n_sig, int n_samples, int n_fft, int hop, int flags,
+                                float* X_c64, float* mag, void* mag_bf16, long long ld_bf16, long long n_sig_bf16,
+                                void* stream) {
   DL4SS_REQUIRE(n_fft == NFFT && hop == HOPL && n_samples > NFFT / 2 && n_sig >= 0);
   if (n_sig == 0) return 0;  // empty batch: no-op (an empty tensor's pointer may be null)
   DL4SS_REQUIRE(x);
   DL4SS_REQUIRE(!((flags & F_COMPLEX) && !X_c64));
   DL4SS_REQUIRE(!((flags & (F_MAG | F_LOGMAG)) && !mag));
+  DL4SS_REQUIRE(!mag_bf16 || ((flags & (F_MAG | F_LOGMAG)) && ld_bf16 >= NBIN && n_sig_bf16 >= 0 && n_sig_bf16 <= n_sig));
   const int T = 1 + n_samples / HOPL;
   const int tiles = (T + FPT - 1) / FPT;
   // one workgroup per tile: measured on MI355X (2048 x 4 s signals, complex + magnitude)
@@ -372,7 +380,7 @@ DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int
   const long long n_tiles = n_sig * tiles;
   DL4SS_REQUIRE(n_tiles < (1LL << 31));
   const long long grid = n_tiles;
-  using K = void (*)(const float*, int, int, int, int, float2*, float*);
+  using K = void (*)(const float*, int, int, int, int, float2*, float*, unsigned short*, long long, int);
   static const K kern[16] = {
       stft_fwd_kernel<0, 0, 0, 0>, stft_fwd_kernel<1, 0, 0, 0>, stft_fwd_kernel<0, 1, 0, 0>, stft_fwd_kernel<1, 1, 0, 0>,
       stft_fwd_kernel<0, 0, 1, 0>, stft_fwd_kernel<1, 0, 1, 0>, stft_fwd_kernel<0, 1, 1, 0>, stft_fwd_kernel<1, 1, 1, 0>,
@@ -381,9 +389,15 @@ DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int
   const int sel = ((flags & F_COMPLEX) ? 1 : 0) | ((flags & (F_MAG | F_LOGMAG)) ? 2 : 0) |
                   ((flags & F_LOGMAG) ? 4 : 0) | ((flags & F_CONJ) ? 8 : 0);
   hipLaunchKernelGGL(kern[sel], dim3((unsigned)grid), dim3(256), 0, as_stream(stream), x, n_samples, T, tiles,
-                     (int)n_tiles, reinterpret_cast<float2*>(X_c64), mag);
+                     (int)n_tiles, reinterpret_cast<float2*>(X_c64), mag, static_cast<unsigned short*>(mag_bf16), ld_bf16,
+                     (int)(mag_bf16 ? n_sig_bf16 : 0));
   DL4SS_CHECK_LAUNCH();
   return 0;
+}
+
+DL4SS_API int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int n_fft, int hop, int flags,
+                             float* X_c64, float* mag, void* stream) {
+  return dl4ss_stft_fwd_ex(x, n_sig, n_samples, n_fft, hop, flags, X_c64, mag, nullptr, 0, 0, stream);
 }
 
 DL4SS_API int dl4ss_istft(const float* S_c64, long long n_sig, int T, int n_fft, int hop, int flags, float* y,

@@ -184,11 +184,16 @@ class SepTrainer:
             raise RuntimeError("unsupported BiRNN configuration")
         self.ws_bytes = ws
         self.rnn_ws = torch.empty((ws + 7) // 8, device=dev, dtype=torch.int64)
-        # bf16 fast path: one workspace per (layer, pass), zeroed by one fill per pass
-        # (DL4SS_RNN_WS_ZEROED) instead of a memset in front of every recurrence launch
+        # bf16 fast path: one workspace per (layer, pass) (DL4SS_RNN_WS_ZEROED) instead of a memset
+        # in front of every recurrence launch.  Zeroed once: a launch that completes leaves its
+        # workspace fit for the next launch of the same shape (T >= 4: no stale tag can match, and
+        # the packed kernels put their start counters / placement granules back, release_start in
+        # birnn.hip), so there is no per-step fill (round 5, 10.4 us); check() zeroes it again after
+        # a timed-out launch, whose half-written hand-offs could.  DL4SS_WS_FILL=1: the fill per step.
         w8 = (ws + 255) // 256 * 32
-        self.rnn_ws_all = torch.empty(2, net.L * w8, device=dev, dtype=torch.int64)  # [fwd | bwd][layer]
+        self.rnn_ws_all = torch.zeros(2, net.L * w8, device=dev, dtype=torch.int64)  # [fwd | bwd][layer]
         self._w8 = w8
+        self._ws_fill = self.T < 4 or os.environ.get("DL4SS_WS_FILL", "0") == "1"
         # {hand-off timed out, refused-update count} (the recurrence kernels set [0]; the guarded
         # Adam counts its refusals in [1])
         self.status = torch.zeros(2, device=dev, dtype=torch.int32)
@@ -268,12 +273,24 @@ class SepTrainer:
                 flops = 2.0 * (F * net.E) * (2 * H) * BT
                 if free >= 8 and (flops / (free * 2.75e12) < net.L * T * 1.75e-6 * 0.85 or side == "1"):
                     self.side = (free, 2, 1, False)
+        # No zeroing pass over the flat gradient (round 5): in the grouped bf16 backward every
+        # gradient has exactly one writer -- the grouped / side GEMMs (beta 0), the bias reduce, the
+        # Linear-bias row sums or colsum, the query backward (beta 0: it also zeroes the embedding
+        # rows no speaker of the batch owns) -- and each writes its region without reading it.
+        # Bitwise the zeroed form (0 + x = x).  DL4SS_GRAD_ZERO=1 restores the zeroing (A/B).
+        self.zero_free = (self.fast and net.L <= 5 and self.defer_bias and
+                          os.environ.get("DL4SS_GRAD_ZERO", "0") != "1")
+        self._gbeta = 0.0 if self.zero_free else 1.0
+        # the bf16 weight copies kept by Adam (dl4ss_adam_guarded_dp_scaled_bf16) instead of a
+        # conversion launch per step; DL4SS_ADAM_SHADOW=0: the conversion every step (A/B)
+        self._shadow_on = self.fast and os.environ.get("DL4SS_ADAM_SHADOW", "1") != "0"
+        self._wb_ver = None
         if self.fast:
             bf = dict(device=dev, dtype=torch.bfloat16)
             p8 = lambda n: (n + 7) // 8 * 8
             self.p8 = p8
             D0 = net.F
-            self.xb0 = torch.empty(BT, p8(D0), **bf)
+            self.xb0 = torch.zeros(BT, p8(D0), **bf)  # (row padding zero: the STFT writes columns < F only)
             self.outb = [torch.empty(BT, p8(2 * H), **bf) for _ in range(net.L)]
             self.hprevb = [torch.empty(BT, 2 * p8(H), **bf) for _ in range(net.L)]
             # every layer's bf16 dG (and GRU dGh) stays until the end of backward: the weight
@@ -322,12 +339,15 @@ class SepTrainer:
         spectra (two launches); magnitude modes, mixtures and sources in one launch over the
         shared signal buffer."""
         B, K, N = self.B, self.K, self.N
+        # bf16 step: the mixtures' magnitudes also land in bf16 in the recurrence's input rows (xb0)
+        xb = dict(out_bf16=self.xb0, n_bf16=B) if self.fast else {}
         if self.mode == "crm":
-            ops.stft(self.mix, complex_out=True, mag_out=True, out_c=self.Xc_mix, out_mag=self.mag_mix)
+            ops.stft(self.mix, complex_out=True, mag_out=True, out_c=self.Xc_mix, out_mag=self.mag_mix, **xb)
             ops.stft(self.src.view(B * K, N), complex_out=True, mag_out=False, out_c=self.Xc_src.view(B * K, self.T,
                                                                                                      self.F, 2))
         else:
-            ops.stft(self._sig, complex_out=False, mag_out=True, out_mag=self._mag)
+            ops.stft(self._sig, complex_out=False, mag_out=True, out_mag=self._mag, **xb)
+        self._xb0_fresh = self.fast
 
     # ------------------------------------------------------------------ forward
     def _to_bf16_rows(self, x, out):
@@ -335,13 +355,16 @@ class SepTrainer:
         _lib.call("dl4ss_f32_to_bf16_2d", _lib.ptr(x, True), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(out),
                   out.stride(0), _lib.stream_ptr())
 
-    def _weights_to_bf16(self):
+    def _weights_to_bf16(self, force=False):
         """The bf16 copies of every layer's W_ih and the Linear weight, one launch
-        (dl4ss_f32_to_bf16_2d_multi)."""
+        (dl4ss_f32_to_bf16_2d_multi) -- only when the parameters changed by other means than this
+        trainer's Adam, which writes the copies itself (dl4ss_adam_guarded_dp_scaled_bf16, round 5):
+        a torch in-place op on net.flat (a checkpoint load, the DP broadcast, a test's state restore)
+        bumps its version counter, the device-side Adam does not."""
         net = self.net
-        pairs = [(net.cat_view("weight_ih", l), self.wb_ih[l]) for l in range(net.L)]
-        pairs.append((net.view("mix.Linear.weight"), self.wb_lin))
         if not hasattr(self, "_cvt_args"):
+            pairs = [(net.cat_view("weight_ih", l), self.wb_ih[l]) for l in range(net.L)]
+            pairs.append((net.view("mix.Linear.weight"), self.wb_lin))
             n = len(pairs)
             P = ctypes.c_void_p
             self._cvt_args = (n, (P * n)(*[x.data_ptr() for x, _ in pairs]),
@@ -350,7 +373,14 @@ class SepTrainer:
                               (ctypes.c_int * n)(*[x.shape[1] for x, _ in pairs]),
                               (P * n)(*[y.data_ptr() for _, y in pairs]),
                               (ctypes.c_longlong * n)(*[y.stride(0) for _, y in pairs]))
+            base = net.flat.data_ptr()
+            assert all(x.is_contiguous() for x, _ in pairs)
+            self._shadow = (n, (ctypes.c_longlong * n)(*[(x.data_ptr() - base) // 4 for x, _ in pairs]),
+                            self._cvt_args[3], self._cvt_args[4], self._cvt_args[5], self._cvt_args[6])
+        if not force and self._shadow_on and self._wb_ver == net.flat._version:
+            return
         _lib.call("dl4ss_f32_to_bf16_2d_multi", *self._cvt_args, _lib.stream_ptr())
+        self._wb_ver = net.flat._version
 
     @staticmethod
     def _hilo(x, y, segw, pattern):
@@ -367,12 +397,14 @@ class SepTrainer:
         st = _lib.stream_ptr()
         cell = CELLS[net.cell]
         A_SPLIT, W_SPLIT = 0b010, 0b100  # [hi | lo | hi] and [hi | hi | lo]
-        self.rnn_ws_all.zero_()  # every layer's forward AND BPTT hand-off workspaces, one fill per step
+        if self._ws_fill:
+            self.rnn_ws_all.zero_()  # every layer's forward AND BPTT hand-off workspaces, one fill per step
         self._weights_to_bf16()
         for l in range(net.L):
             self._hilo(net.cat_view("weight_ih", l), self.ws_ih[l], self.seg[l], W_SPLIT)
         self._hilo(net.view("mix.Linear.weight"), self.ws_lin, self.p8(2 * H), W_SPLIT)
-        self._to_bf16_rows(x, self.xb0)
+        if not self._xb0_ok:
+            self._to_bf16_rows(x, self.xb0)
         self._mean_done = False
         self._hilo(x, self.xs0, self.seg[0], A_SPLIT)
         xin = self.xs0
@@ -405,9 +437,11 @@ class SepTrainer:
         BT = B * T
         st = _lib.stream_ptr()
         cell = CELLS[net.cell]
-        self.rnn_ws_all.zero_()  # every layer's forward AND BPTT hand-off workspaces, one fill per step
+        if self._ws_fill:
+            self.rnn_ws_all.zero_()  # every layer's forward AND BPTT hand-off workspaces, one fill per step
         self._weights_to_bf16()
-        self._to_bf16_rows(x, self.xb0)
+        if not self._xb0_ok:
+            self._to_bf16_rows(x, self.xb0)
         xb = self.xb0[:, :x.shape[1]]
         self._mean_done = False
         for l in range(net.L):
@@ -448,6 +482,9 @@ class SepTrainer:
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         x = (self.mag_mix if feats is None else feats).reshape(BT, -1)
+        # the STFT of this step already wrote x's bf16 rows (self.xb0) unless the features came from elsewhere
+        self._xb0_ok = feats is None and getattr(self, "_xb0_fresh", False)
+        self._xb0_fresh = False
         st = _lib.stream_ptr()
         cell = CELLS[net.cell]
         if self.fast:
@@ -549,19 +586,20 @@ class SepTrainer:
         self.dw_splits = (s_lin, s_ih, s_hh)
         probs = [] if (self.buckets or self.side) else [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H],
                                               out=net.view("mix.Linear.weight", g), transA=True, transB=False,
-                                              beta=1.0, splitk=s_lin)]
+                                              beta=self._gbeta, splitk=s_lin)]
         # longest k-ranges first (dW_lin 63 k-tiles per workgroup, dW_ih 32, dW_hh 16): the short
         # ones fill the tail
         for l in range(net.L - 1, -1, -1):
             xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
             probs.append(dict(A=self.dGb_l[l], B=xb, out=net.cat_view("weight_ih", l, g), transA=True, transB=False,
-                              beta=1.0, splitk=s_ih))
+                              beta=self._gbeta, splitk=s_ih))
         for l in range(net.L - 1, -1, -1):
             src = self.dGhb_l[l] if gru else self.dGb_l[l]
             whh = net.cat_view("weight_hh", l, g)
             for d in range(2):
                 probs.append(dict(A=src[:, d * ldgh:d * ldgh + NGH], B=self.hprevb[l][:, d * hp8:d * hp8 + H],
-                                  out=whh[d * NGH:(d + 1) * NGH], transA=True, transB=False, beta=1.0, splitk=s_hh))
+                                  out=whh[d * NGH:(d + 1) * NGH], transA=True, transB=False, beta=self._gbeta,
+                                  splitk=s_hh))
         self._dw_group = ops.GroupedGemm(probs, net.device)
         return self._dw_group
 
@@ -582,11 +620,11 @@ class SepTrainer:
         ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], splitk=self.dh_split, ws=self.gl_ws)
         if (not grouped or self.buckets) and not self.side:  # (bitwise the grouped launch's dW_lin at the same split)
             ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
-                             beta=1.0, splitk=2, ws=self.gl_ws)
+                             beta=self._gbeta, splitk=2, ws=self.gl_ws)
         if not self.side:
-            _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
+            _lib.call("dl4ss_colsum_bf16_det_ex", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                       _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
-                      self.colsum_part.numel() * 4, st)
+                      self.colsum_part.numel() * 4, self._gbeta, st)
         elif not self.buckets:  # (bucketed: _early_bucket forks it, with the early all-reduce)
             self._side_launch()
 
@@ -607,15 +645,15 @@ class SepTrainer:
             self._side_stream = torch.cuda.Stream(device=net.device)
             self._side_gemm = ops.GroupedGemm(
                 [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H], out=net.view("mix.Linear.weight", g),
-                      transA=True, transB=False, beta=1.0, splitk=split,
+                      transA=True, transB=False, beta=self._gbeta, splitk=split,
                       rowsum=net.view("mix.Linear.bias", g) if split == 1 else None)],
                 net.device, grid=grid, cfg=cfg, one_per_cu=one)
         self._side_stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._side_stream):
             if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
-                _lib.call("dl4ss_colsum_bf16_det", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
+                _lib.call("dl4ss_colsum_bf16_det_ex", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
                           _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
-                          self.colsum_part.numel() * 4, _lib.stream_ptr())
+                          self.colsum_part.numel() * 4, self._gbeta, _lib.stream_ptr())
             self._side_gemm.run()
 
     def _side_join(self):
@@ -663,11 +701,16 @@ class SepTrainer:
                                  strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT, ws=self.gl_ws)
             if l > 0:
                 dH = dH_next
+        # the side stream joins before the bias reduce (it ends inside the last BPTT): a join after the
+        # grouped launch cost ~9 us more per step (the cross-queue wait in front of Adam; A/B x3, round 5)
+        early_join = self.side and not self.buckets and os.environ.get("DL4SS_SIDE_JOIN", "early") == "early"
+        if early_join:
+            self._side_join()
         if self.defer_bias:
             self._bias_reduce()
         if grouped:
             dwg.run()
-        if self.side and not self.buckets:  # dW_lin's side stream joins at the end of the backward
+        if self.side and not self.buckets and not early_join:  # dW_lin's side stream joins at the end of the backward
             self._side_join()
 
     def _bias_reduce(self):
@@ -679,7 +722,8 @@ class SepTrainer:
             self._bias_args = (n, (P * n)(*[self._ws_slot(l, True).data_ptr() for l in range(n)]),
                                (P * n)(*[net.cat_view("bias_ih", l, g).data_ptr() for l in range(n)]),
                                (P * n)(*[net.cat_view("bias_hh", l, g).data_ptr() for l in range(n)]))
-        _lib.call("dl4ss_birnn_bias_reduce", CELLS[net.cell], self.B, net.H, *self._bias_args, _lib.stream_ptr())
+        _lib.call("dl4ss_birnn_bias_reduce_ex", CELLS[net.cell], self.B, net.H, *self._bias_args, self._gbeta,
+                  _lib.stream_ptr())
 
     def backward(self):
         self.backward_early()
@@ -692,7 +736,8 @@ class SepTrainer:
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         g = net.grad
-        g.zero_()
+        if not self.zero_free:
+            g.zero_()
         self._query_bwd()
         if self.fast:
             self._backward_fast_early()
@@ -707,15 +752,16 @@ class SepTrainer:
 
     def _query_bwd(self):
         """SPEECH_EMBEDDING / ADDJUST backward: the embedding and ADDJUST gradients (added into the
-        zeroed flat gradient) and dh_bcast, ADDJUST's share of the last layer's output gradient."""
+        zeroed flat gradient, or written over it when zero_free) and dh_bcast, ADDJUST's share of the
+        last layer's output gradient."""
         net, B, T, H = self.net, self.B, self.T, self.net.H
         g = net.grad
         wadj = net.view("adj.layer.weight") if net.adjust else None
-        _lib.call("dl4ss_query_bwd", _lib.ptr(self.dq), B, T, 2 * H, _lib.ptr(self.spk),
+        _lib.call("dl4ss_query_bwd_ex", _lib.ptr(self.dq), B, T, 2 * H, _lib.ptr(self.spk),
                   _lib.ptr(net.view("emb.layer.weight")), _lib.ptr(wadj), _lib.ptr(self.mean), self.K, net.W,
                   _lib.ptr(net.view("emb.layer.weight", g)),
                   _lib.ptr(net.view("adj.layer.weight", g)) if net.adjust else None,
-                  _lib.ptr(self.dh_bcast) if net.adjust else None, _lib.stream_ptr())
+                  _lib.ptr(self.dh_bcast) if net.adjust else None, net.num_labels, self._gbeta, _lib.stream_ptr())
 
     def backward_late(self):
         """The BPTT chain and the recurrent layers' weight / bias gradients, then the status flag."""
@@ -816,7 +862,8 @@ class SepTrainer:
         self._wait_allreduce()
         self.step_count += 1
         ops.adam_(self.net.flat, self.net.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps,
-                  status=self.status, loss=self.loss, dp_flag=self.net.dp_flag, gscale=1.0 / self.world)
+                  status=self.status, loss=self.loss, dp_flag=self.net.dp_flag, gscale=1.0 / self.world,
+                  shadow=self._shadow if (self._shadow_on and hasattr(self, "_shadow")) else None)
 
     def step(self, raw, gains, spk_idx):
         """One full training step on device-resident inputs; returns the loss tensor (not synced)."""
@@ -894,6 +941,8 @@ class SepTrainer:
             self.capture()
         self.spk.copy_(spk_idx)
         ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
+        if self.fast and self._wb_ver != self.net.flat._version:  # parameters changed outside Adam since the capture
+            self._weights_to_bf16()
         self.graph.replay()
         if self.graph_late is not None:
             self._early_bucket()
@@ -915,6 +964,7 @@ class SepTrainer:
         s, refused = (int(x) for x in self.status.tolist())
         if s or refused:
             self.status.zero_()
+            self.rnn_ws_all.zero_()  # a timed-out launch's half-written hand-offs must not reach the next
             self.step_count -= refused
             where = "on this rank" if s else "on a data-parallel peer"
             raise RuntimeError(f"BiRNN hand-off timed out {where} (status {s}): {refused} update(s) refused")

@@ -23,11 +23,14 @@ def _f32c(t, name):
     return t
 
 
-def stft(x, complex_out=True, mag_out=True, log=False, conj=False, out_c=None, out_mag=None):
+def stft(x, complex_out=True, mag_out=True, log=False, conj=False, out_c=None, out_mag=None, out_bf16=None,
+         n_bf16=0):
     """x (..., N) fp32 -> (X (..., T, F, 2) fp32 [re,im], mag (..., T, F) fp32).
 
     librosa stft(n_fft=256, hop=128) restated (periodic Hann, centre/reflect).
-    ``log`` writes log(|X| + eps) into the magnitude output instead.
+    ``log`` writes log(|X| + eps) into the magnitude output instead.  ``out_bf16`` (rows sig * T + t,
+    row stride >= F): bf16 copies of the magnitudes of the first ``n_bf16`` signals, written by the
+    same launch (dl4ss_stft_fwd_ex; columns >= F untouched).
     """
     _f32c(x, "stft")
     N = x.shape[-1]
@@ -40,6 +43,14 @@ def stft(x, complex_out=True, mag_out=True, log=False, conj=False, out_c=None, o
         out_c = torch.empty(*lead, T, F_BINS, 2, device=x.device, dtype=torch.float32)
     if mag_out and out_mag is None:
         out_mag = torch.empty(*lead, T, F_BINS, device=x.device, dtype=torch.float32)
+    if out_bf16 is not None:
+        if not mag_out or out_bf16.dtype != torch.bfloat16 or out_bf16.stride(-1) != 1 or \
+                out_bf16.shape[0] < n_bf16 * T or out_bf16.stride(0) < F_BINS or n_bf16 > n_sig:
+            raise RuntimeError("stft: out_bf16 must be bf16 rows (>= n_bf16 * T, row stride >= 129) of a magnitude")
+        _lib.call("dl4ss_stft_fwd_ex", _lib.ptr(x), n_sig, N, N_FFT, HOP, flags,
+                  _lib.ptr(out_c) if complex_out else None, _lib.ptr(out_mag), _lib.ptr(out_bf16),
+                  out_bf16.stride(0), n_bf16, _lib.stream_ptr())
+        return out_c, out_mag
     _lib.call("dl4ss_stft_fwd", _lib.ptr(x), n_sig, N, N_FFT, HOP, flags, _lib.ptr(out_c) if complex_out else None,
               _lib.ptr(out_mag) if mag_out else None, _lib.stream_ptr())
     return out_c, out_mag
@@ -295,7 +306,7 @@ class GroupedGemm:
 
     def run(self):
         for c, beta in self._k0:
-            c.mul_(beta)
+            c.zero_() if beta == 0.0 else c.mul_(beta)  # beta 0: C is not read (stale NaN included)
         if self.n == 0:
             return
         if self.grid > 0 or self.cfg != 1 or self.rowsum is not None:
@@ -326,17 +337,25 @@ def colsum(A, out):
     return out
 
 
-def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, loss=None, dp_flag=None, gscale=1.0):
+def adam_(p, g, m, v, step, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, status=None, loss=None, dp_flag=None, gscale=1.0,
+          shadow=None):
     """torch Adam step on flat buffers; with ``status`` (the recurrence hand-off status word,
     2 ints: {timed out, refused-update count}) the update is refused on device when a hand-off
     of this step timed out, loss[0] is set to NaN and status[1] counts the refusal
     (dl4ss_adam_guarded_dp's 2-int status form); with ``dp_flag`` (the all-reduced status flag
     behind the flat gradient) also when a data-parallel peer's hand-off timed out.  ``gscale``: the
-    update uses g * gscale (1 / world_size on a SUM-reduced gradient; 1 is bitwise the unscaled step)."""
+    update uses g * gscale (1 / world_size on a SUM-reduced gradient; 1 is bitwise the unscaled step).
+    ``shadow``: (nseg, seg_off, seg_rows, seg_cols, seg_y, seg_ldy) ctypes arrays -- bf16 copies of the
+    updated parameters written by the same launch (dl4ss_adam_guarded_dp_scaled_bf16)."""
     for t in (p, g, m, v):
         _f32c(t, "adam")
     if status is not None and status.numel() < 2:
         raise ValueError("adam_: the status word needs 2 ints (timed out, refused-update count)")
+    if shadow is not None:
+        _lib.call("dl4ss_adam_guarded_dp_scaled_bf16", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(),
+                  float(lr), float(betas[0]), float(betas[1]), float(eps), int(step), _lib.ptr(status),
+                  _lib.ptr(dp_flag), float(gscale), _lib.ptr(loss), *shadow, _lib.stream_ptr())
+        return
     _lib.call("dl4ss_adam_guarded_dp_scaled", _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(),
               float(lr), float(betas[0]), float(betas[1]), float(eps), int(step), _lib.ptr(status), _lib.ptr(dp_flag),
               float(gscale), _lib.ptr(loss), _lib.stream_ptr())

@@ -37,6 +37,12 @@ enum {
  * TDAA_beta/predata_fromList_cRM_123.py:215-255 (convert2 layout = [re, im]). */
 int dl4ss_stft_fwd(const float* x, long long n_sig, int n_samples, int n_fft, int hop, int flags,
                    float* X_c64, float* mag, void* stream);
+/* dl4ss_stft_fwd that also writes bf16 (round-to-nearest-even) copies of the magnitudes (or log
+ * magnitudes) of the first n_sig_bf16 signals: mag_bf16[(sig * T + t) * ld_bf16 + f], ld_bf16 >= 129,
+ * columns >= 129 untouched -- the bf16 recurrence's first-layer input rows without a conversion pass.
+ * mag_bf16 NULL: dl4ss_stft_fwd. */
+int dl4ss_stft_fwd_ex(const float* x, long long n_sig, int n_samples, int n_fft, int hop, int flags, float* X_c64,
+                      float* mag, void* mag_bf16, long long ld_bf16, long long n_sig_bf16, void* stream);
 
 /* Overlap-add inverse STFT: S (n_sig, T, 129, 2) -> y (n_sig, 128 * (T - 1)).
  * Replaces librosa.core.spectrum.istft(S.T, 128) at
@@ -140,6 +146,9 @@ int dl4ss_colsum_bf16(const void* A, long long lda, int M, int N, float* out, vo
 long long dl4ss_colsum_bf16_part_bytes(int M, int N);
 int dl4ss_colsum_bf16_det(const void* A, long long lda, int M, int N, float* out, float* part, long long part_bytes,
                           void* stream);
+/* dl4ss_colsum_bf16_det with out = beta out + sums (beta 0: out written, not read; beta 1 bitwise _det). */
+int dl4ss_colsum_bf16_det_ex(const void* A, long long lda, int M, int N, float* out, float* part,
+                             long long part_bytes, float beta, void* stream);
 /* n (<= 8) dl4ss_f32_to_bf16_2d conversions in one launch (host arrays of per-segment
  * arguments): the step's bf16 weight copies (W_ih of every layer, the Linear). */
 int dl4ss_f32_to_bf16_2d_multi(int n, const float* const* x, const long long* ldx, const int* rows, const int* cols,
@@ -152,7 +161,10 @@ enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
  * a fixed-order reduce adds into db_ih / db_hh, so the gradients are bitwise reproducible.
  * The launchers zero the workspace themselves (hipMemsetAsync) unless `precision` carries
  * DL4SS_RNN_WS_ZEROED: the caller then guarantees it is zero (e.g. one fill per training
- * step over separate workspaces for every layer and pass). */
+ * step over separate workspaces for every layer and pass) -- or exactly as the previous launch
+ * on it left it, when that launch had the same (cell, B, T, H), T >= 4, and completed without a
+ * timeout: its stale tags cannot match, and the packed kernels reset their start counters and
+ * placement granules themselves (the training step zeroes its workspaces once). */
 #define DL4SS_RNN_WS_ZEROED 0x100
 /* precision flag of dl4ss_birnn_bwd_ex: dGh_bf16 is laid out (B, T, 2, pad8(NGATE*H)) -- each
  * direction's columns start 16-B aligned (the GRU's 900 gate rows -> 904), so both directions'
@@ -165,6 +177,10 @@ enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
 #define DL4SS_RNN_DEFER_BIAS 0x400
 int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
                             float* const* db_hh, void* stream);
+/* dl4ss_birnn_bias_reduce with db = beta db + sums: beta 0 writes db_ih / db_hh without reading them
+ * (the training step then needs no zeroed gradient buffer; beta 1 is bitwise the += form). */
+int dl4ss_birnn_bias_reduce_ex(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
+                               float* const* db_hh, float beta, void* stream);
 long long dl4ss_birnn_workspace_bytes(int cell, int B, int H);
 /* The persistent recurrence's plan under a co-residency budget: every workgroup of a launch
  * (2 directions x nchunk batch chunks x NG units groups) must be resident at once, so the
@@ -301,6 +317,13 @@ int dl4ss_query_fwd(const float* h, int B, int T, int D, const int* idx, const f
 /* d_emb (+=, scatter), d_wadj (+=), dh_bcast (B,D) = W_m^T sum_k dq / T. */
 int dl4ss_query_bwd(const float* dq, int B, int T, int D, const int* idx, const float* emb, const float* w_adj,
                     const float* mean, int K, int W, float* d_emb, float* d_wadj, float* dh_bcast, void* stream);
+/* dl4ss_query_bwd with d_emb / d_wadj = beta (old) + this step's: beta 0 writes them without reading --
+ * every d_wadj element, the embedding rows the batch's speakers own, and zeros in the other rows of
+ * the n_labels-row d_emb (the step's gradient buffer then needs no zeroing pass); beta 1 is bitwise
+ * dl4ss_query_bwd (n_labels unused). */
+int dl4ss_query_bwd_ex(const float* dq, int B, int T, int D, const int* idx, const float* emb, const float* w_adj,
+                       const float* mean, int K, int W, float* d_emb, float* d_wadj, float* dh_bcast, int n_labels,
+                       float beta, void* stream);
 /* out[n] += sum_m A[m*lda + n] (bias gradients). */
 int dl4ss_colsum(const float* A, long long lda, int M, int N, float* out, void* stream);
 /* torch.optim.Adam step on flat fp32 buffers (EvalVer.py:538-544). */
@@ -326,6 +349,16 @@ int dl4ss_adam_guarded_dp(float* p, const float* g, float* m, float* v, long lon
 int dl4ss_adam_guarded_dp_scaled(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1,
                                  float beta2, float eps, int step, int* status, const float* dp_flag, float gscale,
                                  float* loss, void* stream);
+/* dl4ss_adam_guarded_dp_scaled that also writes bf16 (round-to-nearest-even) shadow copies of the
+ * updated parameters: segment s < nseg (<= 8) maps the flat range [seg_off[s], + rows*cols) row-major
+ * onto seg_y[s] (row stride seg_ldy[s] >= cols; columns >= cols untouched).  The bf16 step's weight
+ * operands (W_ih of every layer, the Linear) then need no conversion launch before the next forward:
+ * bitwise dl4ss_f32_to_bf16_2d_multi of the new parameters; a refused update leaves both untouched. */
+int dl4ss_adam_guarded_dp_scaled_bf16(float* p, const float* g, float* m, float* v, long long n, float lr,
+                                      float beta1, float beta2, float eps, int step, int* status, const float* dp_flag,
+                                      float gscale, float* loss, int nseg, const long long* seg_off,
+                                      const int* seg_rows, const int* seg_cols, void* const* seg_y,
+                                      const long long* seg_ldy, void* stream);
 /* flag[0] = status[0] != 0 ? 1 : 0 (one float, written in front of the flat gradient before its all-reduce). */
 int dl4ss_status_flag(const int* status, float* flag, void* stream);
 

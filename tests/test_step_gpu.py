@@ -401,3 +401,126 @@ def test_dp_mean_of_half_batch_gradients_equals_full_batch(dev, precision, mode)
     half = 0.5 * (grads(0, B // 2) + grads(B // 2, B))
     err = float((half - full).abs().max() / full.abs().max())
     assert err < (1e-5 if precision == "fp32" else 1e-3), err
+
+
+@pytest.mark.parametrize("precision,mode,B,cell,K,L,side", [("bf16", "pit", 4, "lstm", 2, 2, "0"),
+                                                         ("bf16", "pit", 4, "gru", 3, 2, "0"),
+                                                         ("bf16s", "label", 4, "lstm", 2, 2, "0"),
+                                                         ("bf16", "pit", 32, "lstm", 2, 4, "1")])
+def test_step_without_gradient_zeroing_bitwise_equals_zeroed(dev, monkeypatch, precision, mode, B, cell, K, L, side):
+    """zero_free (the grouped bf16 backward's writers overwrite their gradient regions: beta-0 GEMMs,
+    bias reduce, colsum / row sums, query backward zeroing the embedding rows no speaker owns) against
+    the zeroed-buffer form (DL4SS_GRAD_ZERO=1) from the same state: bitwise equal losses, gradients and
+    parameters -- with the flat gradient filled with NaN before the zero-free step, so a region read
+    or left unwritten shows.  side "1": the Linear's gradients on the side stream (DL4SS_SIDE_DWLIN)."""
+    N = 8000
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=13)
+    src, spk, u = gen.batch(B)
+    batch = (torch.from_numpy(src.astype(np.float32)).to(dev),
+             torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
+             torch.from_numpy(spk.astype(np.int32)).to(dev))
+    monkeypatch.setenv("DL4SS_SIDE_DWLIN", side)
+    out = {}
+    for zero in ("1", "0"):
+        monkeypatch.setenv("DL4SS_GRAD_ZERO", zero)
+        net = engine.SepNet(cell=cell, num_layers=L, adjust=cell == "lstm", device=dev, seed=17)
+        tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision)
+        assert tr.zero_free == (zero == "0") and bool(tr.side) == (side == "1")
+        for n in net.named_parameters():  # every parameter's region (the 16-B padding between them is
+            net.view(n, net.grad).fill_(float("nan"))  # never written by anyone: it stays zero)
+        loss = tr.step(*batch).clone()
+        tr.check()
+        out[zero] = (loss, net.grad.detach().clone(), net.flat.detach().clone())
+        del tr
+    (l0, g0, p0), (l1, g1, p1) = out["1"], out["0"]
+    bad = [n for n in net.named_parameters() if not torch.isfinite(net.view(n, g1)).all()]
+    assert not bad, bad  # a region no writer covered (or one that read the buffer)
+    diff = [n for n in net.named_parameters() if not torch.equal(net.view(n, g0), net.view(n, g1))]
+    assert not diff, diff
+    assert torch.equal(l0, l1) and torch.equal(g0, g1) and torch.equal(p0, p1)
+
+
+def test_adam_bf16_shadow_copies_equal_fresh_conversion(dev):
+    """The bf16 weight copies the step's forward reads (every layer's W_ih, the Linear) are kept by
+    Adam (dl4ss_adam_guarded_dp_scaled_bf16) instead of a conversion launch per step: after eager and
+    graph steps they are bitwise a fresh dl4ss_f32_to_bf16_2d of the updated parameters (padding
+    columns zero), and a torch in-place change of the parameters (version counter) is picked up."""
+    from dl4ss_amd import _lib
+
+    B, K, N = 4, 2, 8000
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=21)
+    src, spk, u = gen.batch(B)
+    batch = (torch.from_numpy(src.astype(np.float32)).to(dev),
+             torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
+             torch.from_numpy(spk.astype(np.int32)).to(dev))
+    net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=23)
+    tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+    assert tr._shadow_on
+
+    def fresh(x, like):
+        y = torch.empty_like(like)
+        _lib.call("dl4ss_f32_to_bf16_2d", _lib.ptr(x), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(y), y.stride(0),
+                  _lib.stream_ptr())
+        return y
+
+    def check():
+        torch.cuda.synchronize()
+        for l in range(net.L):
+            assert torch.equal(tr.wb_ih[l], fresh(net.cat_view("weight_ih", l), tr.wb_ih[l])), l
+        assert torch.equal(tr.wb_lin, fresh(net.view("mix.Linear.weight"), tr.wb_lin))
+
+    for _ in range(2):
+        tr.step(*batch)
+    tr.check()
+    check()
+    tr.step_graph(*batch)
+    tr.step_graph(*batch)
+    tr.check()
+    check()
+    with torch.no_grad():
+        net.flat.mul_(0.5)  # outside Adam: the next step converts again
+    tr.step_graph(*batch)
+    tr.check()
+    check()
+
+
+@pytest.mark.parametrize("cell,K", [("lstm", 2), ("gru", 3)])
+def test_workspace_reuse_without_fill_bitwise_equals_fill(dev, monkeypatch, cell, K):
+    """The recurrence workspaces are zeroed once and reused as the previous launch left them (no
+    per-step fill; release_start puts the start counters / placement granules back) against a fill
+    before every step (DL4SS_WS_FILL=1): bitwise equal losses, gradients and parameters over eager
+    and graph steps; a forced hand-off timeout in between (check() refills) does not leak into the
+    next step."""
+    B, N = 32, 8000
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=29)
+    batches = []
+    for _ in range(3):
+        src, spk, u = gen.batch(B)
+        batches.append((torch.from_numpy(src.astype(np.float32)).to(dev),
+                        torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
+                        torch.from_numpy(spk.astype(np.int32)).to(dev)))
+    from dl4ss_amd import _lib
+
+    out = {}
+    for fill in ("1", "0"):
+        monkeypatch.setenv("DL4SS_WS_FILL", fill)
+        net = engine.SepNet(cell=cell, num_layers=3, adjust=cell == "lstm", device=dev, seed=31)
+        tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+        assert tr._ws_fill == (fill == "1")
+        losses = [float(tr.step(*b)[0].item()) for b in batches]
+        tr.check()
+        _lib.lib().dl4ss_debug_set_spin_limit(1)  # a timed-out step, refused ...
+        try:
+            tr.step(*batches[0])
+            torch.cuda.synchronize()
+        finally:
+            _lib.lib().dl4ss_debug_set_spin_limit(0)
+        with pytest.raises(RuntimeError, match="timed out"):
+            tr.check()
+        losses += [float(tr.step_graph(*b)[0].item()) for b in batches]  # ... and steps after it
+        tr.check()
+        out[fill] = (losses, net.grad.detach().clone(), net.flat.detach().clone())
+        del tr, net
+    (l0, g0, p0), (l1, g1, p1) = out["1"], out["0"]
+    assert all(np.isfinite(l0)) and l0 == l1
+    assert torch.equal(g0, g1) and torch.equal(p0, p1)

@@ -143,3 +143,25 @@ def test_step_stft_one_launch_equals_two(dev):
     torch.cuda.synchronize()
     assert torch.equal(tr.mag_mix, m_mix)
     assert torch.equal(tr.mag_src.reshape(B * K, tr.T, tr.F), m_src)
+
+
+@pytest.mark.parametrize("N,log", [(32000, False), (8000 + 77, False), (32000, True)])
+def test_stft_bf16_magnitude_copy(dev, N, log):
+    """dl4ss_stft_fwd_ex's bf16 copy of the first n_bf16 signals' (log) magnitudes: bitwise
+    dl4ss_f32_to_bf16_2d of the fp32 output (full and partial frame tiles, the Nyquist bin), the
+    fp32 output unchanged, row padding and the rows of later signals untouched."""
+    from dl4ss_amd import _lib
+
+    g = torch.Generator().manual_seed(3)
+    n_sig, n_bf = 5, 3
+    x = torch.randn(n_sig, N, generator=g).to(dev)
+    T = ops.n_frames(N)
+    _, ref = ops.stft(x, complex_out=False, log=log)
+    mb = torch.full((n_sig * T, 136), 7.0, device=dev, dtype=torch.bfloat16)  # sentinel
+    _, mag = ops.stft(x, complex_out=False, log=log, out_bf16=mb, n_bf16=n_bf)
+    assert torch.equal(mag, ref)
+    want = torch.empty(n_bf * T, 136, device=dev, dtype=torch.bfloat16)
+    src = ref[:n_bf].reshape(n_bf * T, 129)
+    _lib.call("dl4ss_f32_to_bf16_2d", _lib.ptr(src), 129, n_bf * T, 129, _lib.ptr(want), 136, _lib.stream_ptr())
+    assert torch.equal(mb[:n_bf * T, :129], want[:, :129])
+    assert (mb[:n_bf * T, 129:] == 7.0).all() and (mb[n_bf * T:] == 7.0).all()

@@ -30,7 +30,7 @@ def per_step(tr, warmup, steps):
             for r in csv.DictReader(open(tr))]
     rows.sort(key=lambda r: r[1])
     starts = [r[1] for r in rows if r[0] == "source_stats_kernel"]
-    ends = [r[2] for r in rows if r[0] == "adam_kernel"]
+    ends = [r[2] for r in rows if r[0].startswith("adam_kernel")]
     if len(starts) < warmup + steps or len(ends) < warmup + steps:
         return []
     t0, t1 = starts[warmup], ends[warmup + steps - 1]

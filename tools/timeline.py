@@ -20,7 +20,7 @@ def main(path, back=1):
             for r in csv.DictReader(open(path))]
     rows.sort(key=lambda r: r[1])
     starts = [r[1] for r in rows if r[0] == "source_stats_kernel"]
-    ends = [r[2] for r in rows if r[0] == "adam_kernel"]
+    ends = [r[2] for r in rows if r[0].startswith("adam_kernel")]
     t0 = starts[-back]
     t1 = min(e for e in ends if e > t0)
     print(f"step: {(t1 - t0) / 1e3:.1f} us")
