@@ -347,16 +347,23 @@ __device__ __forceinline__ float quad_xor2(float v) {
 typedef __attribute__((address_space(3))) void attn_lds_void;
 __device__ __attribute__((aligned(16))) const unsigned g_attn_zero[4] = {0u, 0u, 0u, 0u};
 
-template <int E, int K, bool GRAD>
-__global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(AttnArgs a) {
+// VF (round 5): fp32 V (the split-precision "bf16s" steps keep V = tanh(Linear) in fp32): the tile
+// arrives as fp32 words (a pair = 8 B, read as one float2), the bf16 dPre pairs go to a separate LDS
+// image (sdp) for the same copy-out; everything else -- the quad's arithmetic and summation order,
+// the bf16 dPre, dq -- as in the bf16-V form.  The generic attn_kernel ran this step at ~2 TB/s
+// (C4 bf16s: 156 us per step for its one GRAD launch).
+template <int E, int K, bool GRAD, bool VF = false>
+__global__ __launch_bounds__(NT, (K == 3 && GRAD) || VF ? 2 : 4) void attn_q4_kernel(AttnArgs a) {
   static_assert(E % 2 == 0, "bf16 pairs");
   constexpr int EP = E / 2;              // bf16 pairs per row
   constexpr int NWL = (EP + 3) / 4;      // pairs per lane
   constexpr int NQ = NT / 4;             // quads per block
   constexpr int RPQ = TILE / NQ;         // rows per quad per tile
-  constexpr int NCH = (TILE * EP + 3) / 4 + 1;  // 16-B chunks of a tile, misaligned start included
+  constexpr int WPR = VF ? E : EP;       // 4-B words of V per row
+  constexpr int NCH = (TILE * WPR + 3) / 4 + 1;  // 16-B chunks of a tile, misaligned start included
   constexpr int NCHP = (NCH + 63) / 64 * 64;     // whole 1-KB DMA instructions
   __shared__ __attribute__((aligned(16))) unsigned sv[NCHP * 4];
+  __shared__ __attribute__((aligned(16))) unsigned sdp[VF && GRAD ? TILE * EP : 1];
   __shared__ float sred[NT / 64][K * K + 1];
   __shared__ float sdq[GRAD ? NT / 64 * K * E : 1];
 
@@ -389,8 +396,8 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(A
 #pragma unroll
       for (int i = 0; i < NWL; ++i) dq[k][i][0] = dq[k][i][1] = 0.f;
   }
-  const unsigned* Vw = reinterpret_cast<const unsigned*>(a.Vb);
-  const long long totw = (long long)a.B * a.rows_per_b * EP;
+  const unsigned* Vw = VF ? reinterpret_cast<const unsigned*>(a.V) : reinterpret_cast<const unsigned*>(a.Vb);
+  const long long totw = (long long)a.B * a.rows_per_b * WPR;
 
   for (int r0 = rbeg; r0 < rend; r0 += TILE) {
     const int nr = min(TILE, rend - r0);
@@ -404,10 +411,10 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(A
 #pragma unroll
       for (int k = 0; k < K; ++k) yr[s][k] = a.Y[(long long)b * a.ys + (long long)k * a.yks + row];
     }
-    const long long w0 = ((long long)b * a.rows_per_b + r0) * EP;
-    const int off = (int)(w0 & 3);
+    const long long w0 = ((long long)b * a.rows_per_b + r0) * WPR;
+    const int off = (int)(w0 & 3);  // (VF: even -- E is -- so every pair is an aligned float2)
     const long long wa = w0 - off;
-    const int nch = (off + nr * EP + 3) >> 2;
+    const int nch = (off + nr * WPR + 3) >> 2;
     __syncthreads();  // the previous tile's rows and dPre copy-out are done with sv
     // V by LDS-DMA: wave instruction p moves chunks 64p .. 64p + 63 (1 KB) into sv + 256p words
     int tail = -1;
@@ -430,16 +437,30 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(A
       const int r = qd + NQ * s;
       if (r < nr) {  // quad-uniform
         const int row = r0 + r;
-        unsigned* v = sv + off + r * EP + j;
-        unsigned wv[NWL];
+        unsigned* v = VF ? sdp + r * EP + j : sv + off + r * EP + j;  // (VF: the dPre pairs' LDS words)
+        float vxs[NWL], vys[NWL];
+        if constexpr (VF) {
+          const float2* vf = reinterpret_cast<const float2*>(sv + off + r * E) + j;
 #pragma unroll
-        for (int i = 0; i < NWL; ++i) wv[i] = (j + 4 * i < EP) ? v[4 * i] : 0u;
+          for (int i = 0; i < NWL; ++i) {
+            const float2 p = (j + 4 * i < EP) ? vf[4 * i] : make_float2(0.f, 0.f);
+            vxs[i] = p.x;
+            vys[i] = p.y;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NWL; ++i) {
+            const unsigned w = (j + 4 * i < EP) ? v[4 * i] : 0u;
+            vxs[i] = __uint_as_float(w << 16);
+            vys[i] = __uint_as_float(w & 0xFFFF0000u);
+          }
+        }
         float lg[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) lg[k] = 0.f;
 #pragma unroll
         for (int i = 0; i < NWL; ++i) {
-          const float vx = __uint_as_float(wv[i] << 16), vy = __uint_as_float(wv[i] & 0xFFFF0000u);
+          const float vx = vxs[i], vy = vys[i];
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             lg[k] = fmaf(vx, qv[k][i][0], lg[k]);
@@ -489,7 +510,7 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(A
           // dq_k[e] += dl_k V[e]
 #pragma unroll
           for (int i = 0; i < NWL; ++i) {
-            const float vx = __uint_as_float(wv[i] << 16), vy = __uint_as_float(wv[i] & 0xFFFF0000u);
+            const float vx = vxs[i], vy = vys[i];
             float g0 = 0.f, g1 = 0.f;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -521,13 +542,14 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) ? 2 : 4) void attn_q4_kernel(A
         const int lead = (int)((4 - (((uintptr_t)(dst + sw)) >> 2)) & 3);  // words before the first aligned one
         const int i0 = min(ew, sw + lead);
         const int nq = (ew - i0) >> 2;
+        const unsigned* so = VF ? sdp : sv + off;  // the tile's dPre words
         for (int q = tid; q < nq; q += NT) {
           const int i = i0 + 4 * q;
-          *reinterpret_cast<uint4*>(dst + i) = make_uint4(sv[off + i], sv[off + i + 1], sv[off + i + 2], sv[off + i + 3]);
+          *reinterpret_cast<uint4*>(dst + i) = make_uint4(so[i], so[i + 1], so[i + 2], so[i + 3]);
         }
         const int te = i0 + 4 * nq;  // tail words [te, ew), head words [sw, i0)
-        if (tid < i0 - sw) dst[sw + tid] = sv[off + sw + tid];
-        if (tid >= 4 && tid - 4 < ew - te) dst[te + tid - 4] = sv[off + te + tid - 4];
+        if (tid < i0 - sw) dst[sw + tid] = so[sw + tid];
+        if (tid >= 4 && tid - 4 < ew - te) dst[te + tid - 4] = so[te + tid - 4];
         sw = ew;
       }
     }
@@ -651,12 +673,15 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
 template <int E, int K, bool CRM, bool VB>
 int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
   dim3 grid(a.nblk, a.B);
-  if constexpr (VB && !CRM) {  // the throughput step's bf16-V magnitude path (16-B aligned V)
-    if ((a.dPreB || !grad) && ((uintptr_t)a.Vb & 15) == 0) {
+  if constexpr (!CRM) {  // the throughput steps' magnitude path (16-B aligned V; bf16 dPre)
+    // fp32 V: only for a bf16-dPre caller (which passes dPre_bf16 to its COST pass too, so both passes
+    // of a PIT step sum the logits alike); the fp32 parity step keeps attn_kernel
+    const bool q4 = VB ? (a.dPreB || !grad) : a.dPreB != nullptr;
+    if (q4 && ((uintptr_t)(VB ? (const void*)a.Vb : (const void*)a.V) & 15) == 0) {
       if (grad)
-        hipLaunchKernelGGL((attn_q4_kernel<E, K, true>), grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((attn_q4_kernel<E, K, true, !VB>), grid, dim3(NT), 0, st, a);
       else
-        hipLaunchKernelGGL((attn_q4_kernel<E, K, false>), grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((attn_q4_kernel<E, K, false, !VB>), grid, dim3(NT), 0, st, a);
       DL4SS_CHECK_LAUNCH();
       return 0;
     }

@@ -287,7 +287,10 @@ int dl4ss_mask_attn_loss(int pass, int crm, int B, int K, int T, int F, int E, c
                          float* part_dq, float* mask_out, float* pred_out, void* stream);
 /* dl4ss_mask_attn_loss with a bf16 GRAD output: dPre_bf16 row (b*T + t) holds the F*E
  * values of frame t at stride dpre_bf16_ld (even, >= F*E: 16-B rows for the Linear's
- * backward GEMMs); dPre may then be NULL. */
+ * backward GEMMs); dPre may then be NULL.  A non-NULL dPre_bf16 on the magnitude path (also
+ * given to the COST pass, which does not write it) selects the quad-per-row kernel for the fp32
+ * V as well -- logits summed as quad partials, as the bf16-V kernel does; NULL keeps the
+ * row-per-lane kernel of the fp32 parity step. */
 int dl4ss_mask_attn_loss_ex(int pass, int crm, int B, int K, int T, int F, int E, const float* V, const float* q,
                             const float* X, long long x_bstride, const float* Y, long long y_bstride,
                             long long y_kstride, const int* perm, float s1, float s2, float* dPre, void* dPre_bf16,

@@ -200,7 +200,7 @@ def test_step_c2_full_size_fp32_masked_magnitude(dev):
     _compare_step(dev, "lstm", 4, 32, 2, 32000, "label")
 
 
-@pytest.mark.parametrize("precision,mode", [("bf16", "pit"), ("fp32", "label"), ("bf16s", "pit")])
+@pytest.mark.parametrize("precision,mode", [("bf16", "pit"), ("fp32", "label"), ("bf16s", "pit"), ("bf16s2", "pit")])
 def test_graph_step_matches_eager(dev, precision, mode):
     """SepTrainer.step_graph (STFT -> forward -> loss -> backward replayed as one HIP graph,
     mixing / Adam eager) against step() from the same state on three changing batches: for
@@ -228,7 +228,7 @@ def test_graph_step_matches_eager(dev, precision, mode):
         net.flat.copy_(state[0]); tr.m.copy_(state[1]); tr.v.copy_(state[2]); tr.step_count = state[3]
         lg = float(tr.step_graph(*b)[0].item())
         tr.check()
-        if precision in ("bf16", "bf16s"):  # the throughput steps are bitwise reproducible: so must the replay be
+        if precision in ("bf16", "bf16s", "bf16s2"):  # the throughput steps are bitwise reproducible: so must the replay be
             assert lg == le and torch.equal(net.grad, ge) and torch.equal(net.flat, pe), (lg, le)
         assert abs(lg - le) <= 1e-6 * abs(le), (lg, le)
         assert float((net.grad - ge).abs().max()) <= 1e-5 * float(ge.abs().max())
@@ -241,7 +241,7 @@ def test_graph_step_matches_eager(dev, precision, mode):
 @pytest.mark.parametrize("precision,mode,B,cell,K", [("bf16", "pit", 4, "lstm", 2), ("bf16", "label", 4, "lstm", 2),
                                                      ("bf16s", "pit", 4, "gru", 3), ("bf16s", "label", 4, "lstm", 2),
                                                      ("bf16", "pit", 32, "lstm", 2), ("bf16", "pit", 4, "gru", 2),
-                                                     ("bf16", "pit", 32, "gru", 3)])
+                                                     ("bf16", "pit", 32, "gru", 3), ("bf16s2", "pit", 4, "gru", 3)])
 def test_step_bitwise_reproducible(dev, precision, mode, B, cell, K):
     """The bf16 throughput step: two steps from the same saved state on the same batch give
     bit-identical losses, gradients and parameters (every reduction has a fixed order; the
@@ -339,7 +339,7 @@ def test_step_c2_full_size_pit_indices(dev, precision):
 
 # (precision, rnn_precision): fp32 parity mode; the mixed mode (fp32 GEMMs, bf16 MFMA recurrent
 # matvec) that C1 / C3 / C4 throughput is quoted in; the all-bf16 operand mode
-C4_MODES = [("fp32", "fp32"), ("fp32", "bf16"), ("bf16s", None),
+C4_MODES = [("fp32", "fp32"), ("fp32", "bf16"), ("bf16s", None), ("bf16s2", None),
             pytest.param("bf16", "bf16", marks=pytest.mark.xfail(
                 strict=True, reason="bf16 GEMM operands on the BiGRU nets: 2.2e-3 > the 1e-3 bar "
                                     "(tests/test_bf16_budget_cpu.py reproduces it by emulation)"))]
