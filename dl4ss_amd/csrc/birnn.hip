@@ -853,6 +853,18 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #pragma unroll
   for (int q = 0; q < NGATE; ++q) bh[q] = cval ? a.bhh[(long long)d * GH + q * H + cj] : 0.0f;
   float hst = 0.0f, cst = 0.0f, hsum = 0.0f;
+#ifndef FWD_STORE_WAVES
+#define FWD_STORE_WAVES 0
+#endif
+  // FWD_STORE_WAVES (experiment, off): the saved-state stores of step s leave from waves 2-3
+  // (matvec-only, idle after B2) during step s+1 instead of from the cell lanes after their publish:
+  // the cell lanes stage {act, c, h_{t-1}, h} in LDS (double buffered by step parity), the last step
+  // stores directly.  Measured round 5 (A/B x3, gpurun_out/r05sw): 3.522 vs 3.466 ms per step, ~14 us
+  // SLOWER per forward launch -- the stores issued right behind the publish pace the polling sweeps
+  // (the round-4 observation); moved off the cell lanes they no longer do.
+  constexpr bool SW = FWD_STORE_WAVES && BC * 32 <= 128;
+  __shared__ float4 s_sta[SW ? 2 * BC * 20 : 1];   // act (4 gates) per cell
+  __shared__ float4 s_stb[SW ? 2 * BC * 20 : 1];   // {c, h_{t-1}, h, -} per cell
 
   // granules of this group: [2 slots][hand-off, spare][BC][NG][8] x 8 B; the spare copy of
   // slot 1 holds the placement granules
@@ -1209,6 +1221,31 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
     STAMP(2)
     __syncthreads();  // B2
     STAMP(3)
+    if constexpr (SW) {
+      // waves 2-3: step s-1's saved state (staged before B1(s); its slot is rewritten only after B2(s+1))
+      const int i = tid - BC * 32;
+      if (s > 0 && i >= 0 && i < BC * J) {
+        const int sb = (s - 1) & 1, ib = b0 + i / J, ij = j0 + i % J;
+        if (ij < H && ib < a.B) {
+          const int tp = d == 0 ? s - 1 : T - s;
+          const long long bt = (long long)ib * T + tp;
+          const float4 ac = s_sta[sb * BC * 20 + i], cb4 = s_stb[sb * BC * 20 + i];
+          if (a.act_cm) {
+            *reinterpret_cast<float4*>(a.act + ((bt * 2 + d) * H + ij) * 4) = ac;
+          } else {
+            float* actp = a.act + (bt * 2 + d) * (4 * H) + ij;
+            actp[0] = ac.x; actp[H] = ac.y; actp[2 * H] = ac.z; actp[3 * H] = ac.w;
+          }
+          if constexpr (CELL == CELL_LSTM) a.cs[(bt * 2 + d) * H + ij] = cb4.x;
+          const long long ho = bt * 2 * H + d * H + ij;
+          if (a.hprev) a.hprev[ho] = cb4.y;
+          if (a.out) a.out[ho] = cb4.z;
+          const int hp8 = (H + 7) & ~7, op8 = (2 * H + 7) & ~7;
+          if (a.outb) a.outb[bt * op8 + d * H + ij] = bf16_rne(cb4.z);
+          if (a.hprevb) a.hprevb[bt * 2 * hp8 + d * hp8 + ij] = bf16_rne(cb4.y);
+        }
+      }
+    }
     if (tid < BC * 32) {
       float hn = 0.0f, st[4] = {0.f, 0.f, 0.f, 0.f};
       if (cval) {
@@ -1266,7 +1303,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_EXP_SKIP
 #define FWD_EXP_SKIP 0  // timing experiments only (results wrong): skip saved-state stores, bits 1 act, 2 cs, 4 out, 8 outb, 16 hprevb, 32 hprev
 #endif
-      if (cval) {
+      if (SW && cval && s < T - 1) {  // staged: waves 2-3 store it during step s+1
+        const int sb = (s & 1) * BC * 20 + cb * J + cu;
+        s_sta[sb] = make_float4(st[0], st[1], st[2], st[3]);
+        s_stb[sb] = make_float4(cst, hst, hn, 0.0f);
+        hsum += hn;
+      } else if (cval) {
         const long long bt = (long long)bg * T + t;
         if (FWD_EXP_SKIP & 1) {
         } else if (a.act_cm) {
