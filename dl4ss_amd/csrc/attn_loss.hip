@@ -352,9 +352,15 @@ __device__ __attribute__((aligned(16))) const unsigned g_attn_zero[4] = {0u, 0u,
 // image (sdp) for the same copy-out; everything else -- the quad's arithmetic and summation order,
 // the bf16 dPre, dq -- as in the bf16-V form.  The generic attn_kernel ran this step at ~2 TB/s
 // (C4 bf16s: 156 us per step for its one GRAD launch).
-template <int E, int K, bool GRAD, bool VF = false>
-__global__ __launch_bounds__(NT, (K == 3 && GRAD) || VF ? 2 : 4) void attn_q4_kernel(AttnArgs a) {
+template <int E, int K, bool GRAD, bool VF = false, bool CRM = false>
+__global__ __launch_bounds__(NT, (K == 3 && GRAD) || VF || CRM ? 2 : 4) void attn_q4_kernel(AttnArgs a) {
   static_assert(E % 2 == 0, "bf16 pairs");
+  // CRM (round 5): the complex-ratio-mask path (cRM_EvalVer.py:259-271, 688, 720-743) -- each row
+  // has NC = 2 logits per query (the re / im halves of the 2E-wide query), the inverse-compressed mask
+  // M, the complex prediction P = M (x) X and its squared error, as attn_kernel computes them (the same
+  // fp32 tanhf / logf chain) -- on the quad layout; only the logits' summation order differs.
+  constexpr int NC = CRM ? 2 : 1;        // logits per (row, query)
+  constexpr int QW = NC * E;             // query width
   constexpr int EP = E / 2;              // bf16 pairs per row
   constexpr int NWL = (EP + 3) / 4;      // pairs per lane
   constexpr int NQ = NT / 4;             // quads per block
@@ -365,21 +371,24 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) || VF ? 2 : 4) void attn_q4_ke
   __shared__ __attribute__((aligned(16))) unsigned sv[NCHP * 4];
   __shared__ __attribute__((aligned(16))) unsigned sdp[VF && GRAD ? TILE * EP : 1];
   __shared__ float sred[NT / 64][K * K + 1];
-  __shared__ float sdq[GRAD ? NT / 64 * K * E : 1];
+  __shared__ float sdq[GRAD ? NT / 64 * K * QW : 1];
 
   const int b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = tid & 3, qd = tid >> 2;
   // this lane's q values (zero for the pair slots past EP)
-  float qv[K][NWL][2];
+  float qv[K][NC][NWL][2];
 #pragma unroll
   for (int k = 0; k < K; ++k)
 #pragma unroll
-    for (int i = 0; i < NWL; ++i) {
-      const int w = j + 4 * i;
-      qv[k][i][0] = w < EP ? a.q[((long long)b * K + k) * E + 2 * w] : 0.f;
-      qv[k][i][1] = w < EP ? a.q[((long long)b * K + k) * E + 2 * w + 1] : 0.f;
-    }
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < NWL; ++i) {
+        const int w = j + 4 * i;
+        const float* qk = a.q + ((long long)b * K + k) * QW + c * E;
+        qv[k][c][i][0] = w < EP ? qk[2 * w] : 0.f;
+        qv[k][c][i][1] = w < EP ? qk[2 * w + 1] : 0.f;
+      }
   const int per = (a.rows_per_b + a.nblk - 1) / a.nblk;
   const int rbeg = blockIdx.x * per;
   const int rend = min(a.rows_per_b, rbeg + per);
@@ -389,27 +398,32 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) || VF ? 2 : 4) void attn_q4_ke
   float cost[K * K + 1];
 #pragma unroll
   for (int i = 0; i < K * K + 1; ++i) cost[i] = 0.f;
-  float dq[GRAD ? K : 1][GRAD ? NWL : 1][2];
+  float dq[GRAD ? K : 1][GRAD ? NC : 1][GRAD ? NWL : 1][2];
   if constexpr (GRAD) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
-      for (int i = 0; i < NWL; ++i) dq[k][i][0] = dq[k][i][1] = 0.f;
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < NWL; ++i) dq[k][c][i][0] = dq[k][c][i][1] = 0.f;
   }
   const unsigned* Vw = VF ? reinterpret_cast<const unsigned*>(a.V) : reinterpret_cast<const unsigned*>(a.Vb);
   const long long totw = (long long)a.B * a.rows_per_b * WPR;
 
   for (int r0 = rbeg; r0 < rend; r0 += TILE) {
     const int nr = min(TILE, rend - r0);
-    // issue this tile's loads: |X| and targets of the quad's rows, then V by 16-B chunks
-    float xr[RPQ], yr[RPQ][K];
+    // issue this tile's loads: X and the targets of the quad's rows (cRM: [re, im]), then V by 16-B chunks
+    float xr[RPQ][NC], yr[RPQ][K][NC];
 #pragma unroll
     for (int s = 0; s < RPQ; ++s) {
       const int r = qd + NQ * s;
       const int row = r0 + (r < nr ? r : 0);
-      xr[s] = a.X[(long long)b * a.xs + row];
 #pragma unroll
-      for (int k = 0; k < K; ++k) yr[s][k] = a.Y[(long long)b * a.ys + (long long)k * a.yks + row];
+      for (int c = 0; c < NC; ++c) xr[s][c] = a.X[((long long)b * a.xs + row) * NC + c];
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) yr[s][k][c] = a.Y[((long long)b * a.ys + (long long)k * a.yks + row) * NC + c];
     }
     const long long w0 = ((long long)b * a.rows_per_b + r0) * WPR;
     const int off = (int)(w0 & 3);  // (VF: even -- E is -- so every pair is an aligned float2)
@@ -455,70 +469,125 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) || VF ? 2 : 4) void attn_q4_ke
             vys[i] = __uint_as_float(w & 0xFFFF0000u);
           }
         }
-        float lg[K];
+        float lg[K][NC];
 #pragma unroll
-        for (int k = 0; k < K; ++k) lg[k] = 0.f;
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) lg[k][c] = 0.f;
 #pragma unroll
         for (int i = 0; i < NWL; ++i) {
           const float vx = vxs[i], vy = vys[i];
 #pragma unroll
-          for (int k = 0; k < K; ++k) {
-            lg[k] = fmaf(vx, qv[k][i][0], lg[k]);
-            lg[k] = fmaf(vy, qv[k][i][1], lg[k]);
-          }
-        }
+          for (int k = 0; k < K; ++k)
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          lg[k] += quad_xor1(lg[k]);
-          lg[k] += quad_xor2(lg[k]);
-        }
-        const float x = xr[s];
-        float m[K], msum = 0.f;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          m[k] = sigmoidf_(lg[k]);
-          msum += m[k];
+            for (int c = 0; c < NC; ++c) {
+              lg[k][c] = fmaf(vx, qv[k][c][i][0], lg[k][c]);
+              lg[k][c] = fmaf(vy, qv[k][c][i][1], lg[k][c]);
+            }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
-          for (int jj = 0; jj < K; ++jj) {
-            const float dd = m[k] * x - yr[s][jj];
-            cost[k * K + jj] = fmaf(dd, dd, cost[k * K + jj]);
+          for (int c = 0; c < NC; ++c) {
+            lg[k][c] += quad_xor1(lg[k][c]);
+            lg[k][c] += quad_xor2(lg[k][c]);
           }
-        const float ds = msum - 1.0f;
-        cost[K * K] = fmaf(ds, ds, cost[K * K]);
-        if ((a.mask_out || a.pred_out) && j == 0) {
+        float dl[K][NC];  // dL/dlogit (GRAD)
+        if constexpr (!CRM) {
+          const float x = xr[s][0];
+          float m[K], msum = 0.f;
 #pragma unroll
           for (int k = 0; k < K; ++k) {
-            const long long o = ((long long)b * K + k) * a.rows_per_b + row;
-            if (a.mask_out) a.mask_out[o] = m[k];
-            if (a.pred_out) a.pred_out[o] = m[k] * x;
+            m[k] = sigmoidf_(lg[k][0]);
+            msum += m[k];
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj) {
+              const float dd = m[k] * x - yr[s][jj][0];
+              cost[k * K + jj] = fmaf(dd, dd, cost[k * K + jj]);
+            }
+          const float ds = msum - 1.0f;
+          cost[K * K] = fmaf(ds, ds, cost[K * K]);
+          if ((a.mask_out || a.pred_out) && j == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              const long long o = ((long long)b * K + k) * a.rows_per_b + row;
+              if (a.mask_out) a.mask_out[o] = m[k];
+              if (a.pred_out) a.pred_out[o] = m[k] * x;
+            }
+          }
+          if constexpr (GRAD) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              float yp = yr[s][0][0];
+#pragma unroll
+              for (int jj = 1; jj < K; ++jj) yp = pm[k] == jj ? yr[s][jj][0] : yp;
+              const float dm = 2.f * a.s1 * (m[k] * x - yp) * x + 2.f * a.s2 * ds;
+              dl[k][0] = dm * m[k] * (1.f - m[k]);
+            }
+          }
+        } else {
+          const float2 x = make_float2(xr[s][0], xr[s][1]);
+          float2 p[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            // cRM_EvalVer.py:269 (10 tanh) and :688 (inverse compression), fp32 as the reference
+            const float mcr = 10.f * tanhf(lg[k][0]);
+            const float mci = 10.f * tanhf(lg[k][1]);
+            const float mr = -10.f * logf((10.f - mcr) / (10.f + mcr));
+            const float mi = -10.f * logf((10.f - mci) / (10.f + mci));
+            p[k] = make_float2(mr * x.x - mi * x.y, mr * x.y + mi * x.x);
+            if (j == 0) {
+              const long long o = 2 * (((long long)b * K + k) * a.rows_per_b + row);
+              if (a.mask_out) { a.mask_out[o] = mr; a.mask_out[o + 1] = mi; }
+              if (a.pred_out) { a.pred_out[o] = p[k].x; a.pred_out[o + 1] = p[k].y; }
+            }
+            if constexpr (GRAD) {
+              // d(M)/d(logit) through the same fp32 chain: dM/dMc * dMc/dl
+              const float dmc_r = 10.f * (1.f / (10.f - mcr) + 1.f / (10.f + mcr));
+              const float dmc_i = 10.f * (1.f / (10.f - mci) + 1.f / (10.f + mci));
+              dl[k][0] = dmc_r * (10.f * (1.f - (mcr * 0.1f) * (mcr * 0.1f)));
+              dl[k][1] = dmc_i * (10.f * (1.f - (mci * 0.1f) * (mci * 0.1f)));
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj) {
+              const float dr = p[k].x - yr[s][jj][0], di = p[k].y - yr[s][jj][1];
+              cost[k * K + jj] = fmaf(dr, dr, fmaf(di, di, cost[k * K + jj]));
+            }
+          if constexpr (GRAD) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              float2 yp = make_float2(yr[s][0][0], yr[s][0][1]);
+#pragma unroll
+              for (int jj = 1; jj < K; ++jj) yp = pm[k] == jj ? make_float2(yr[s][jj][0], yr[s][jj][1]) : yp;
+              const float gr = 2.f * a.s1 * (p[k].x - yp.x), gi = 2.f * a.s1 * (p[k].y - yp.y);
+              // P = M (x) X: dMr = gr xr + gi xi ; dMi = -gr xi + gi xr
+              dl[k][0] *= gr * x.x + gi * x.y;
+              dl[k][1] *= -gr * x.y + gi * x.x;
+            }
           }
         }
         if constexpr (GRAD) {
-          float dl[K];
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            float yp = yr[s][0];
-#pragma unroll
-            for (int jj = 1; jj < K; ++jj) yp = pm[k] == jj ? yr[s][jj] : yp;
-            const float dm = 2.f * a.s1 * (m[k] * x - yp) * x + 2.f * a.s2 * ds;
-            dl[k] = dm * m[k] * (1.f - m[k]);
-          }
-          // dV[e] = sum_k dl_k q_k[e]; dPre = dV (1 - V^2) as bf16 over the lane's own words;
-          // dq_k[e] += dl_k V[e]
+          // dV[e] = sum_{k,c} dl_kc q_kc[e]; dPre = dV (1 - V^2) as bf16 over the lane's own words;
+          // dq_kc[e] += dl_kc V[e]
 #pragma unroll
           for (int i = 0; i < NWL; ++i) {
             const float vx = vxs[i], vy = vys[i];
             float g0 = 0.f, g1 = 0.f;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-              g0 = fmaf(dl[k], qv[k][i][0], g0);
-              g1 = fmaf(dl[k], qv[k][i][1], g1);
-              dq[k][i][0] = fmaf(dl[k], vx, dq[k][i][0]);
-              dq[k][i][1] = fmaf(dl[k], vy, dq[k][i][1]);
-            }
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+              for (int c = 0; c < NC; ++c) {
+                g0 = fmaf(dl[k][c], qv[k][c][i][0], g0);
+                g1 = fmaf(dl[k][c], qv[k][c][i][1], g1);
+                dq[k][c][i][0] = fmaf(dl[k][c], vx, dq[k][c][i][0]);
+                dq[k][c][i][1] = fmaf(dl[k][c], vy, dq[k][c][i][1]);
+              }
             __hip_bfloat162 o2 = __float22bfloat162_rn(make_float2(g0 * (1.f - vx * vx), g1 * (1.f - vy * vy)));
             if (j + 4 * i < EP) v[4 * i] = *reinterpret_cast<unsigned*>(&o2);
           }
@@ -566,23 +635,25 @@ __global__ __launch_bounds__(NT, (K == 3 && GRAD) || VF ? 2 : 4) void attn_q4_ke
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
-      for (int i = 0; i < NWL; ++i)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          float s = dq[k][i][c];
+        for (int i = 0; i < NWL; ++i)
 #pragma unroll
-          for (int o = 4; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
-          const int w = lane + 4 * i;  // lanes 0..3 hold the wave's sums of pairs j + 4i
-          if (lane < 4 && w < EP) sdq[(wave * K + k) * E + 2 * w + c] = s;
-        }
+          for (int h = 0; h < 2; ++h) {
+            float s = dq[k][c][i][h];
+#pragma unroll
+            for (int o = 4; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+            const int w = lane + 4 * i;  // lanes 0..3 hold the wave's sums of pairs j + 4i
+            if (lane < 4 && w < EP) sdq[(wave * K + k) * QW + c * E + 2 * w + h] = s;
+          }
   }
   __syncthreads();
   float* pl = a.part_loss + ((long long)b * a.nblk + blockIdx.x) * (K * K + 1);
   if (tid < K * K + 1) pl[tid] = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
   if constexpr (GRAD) {
-    float* pd = a.part_dq + ((long long)b * a.nblk + blockIdx.x) * K * E;
-    for (int i = tid; i < K * E; i += NT)
-      pd[i] = sdq[0 * K * E + i] + sdq[1 * K * E + i] + sdq[2 * K * E + i] + sdq[3 * K * E + i];
+    float* pd = a.part_dq + ((long long)b * a.nblk + blockIdx.x) * K * QW;
+    for (int i = tid; i < K * QW; i += NT)
+      pd[i] = sdq[0 * K * QW + i] + sdq[1 * K * QW + i] + sdq[2 * K * QW + i] + sdq[3 * K * QW + i];
   }
 }
 
@@ -673,15 +744,16 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
 template <int E, int K, bool CRM, bool VB>
 int launch_attn(bool grad, const AttnArgs& a, hipStream_t st) {
   dim3 grid(a.nblk, a.B);
-  if constexpr (!CRM) {  // the throughput steps' magnitude path (16-B aligned V; bf16 dPre)
-    // fp32 V: only for a bf16-dPre caller (which passes dPre_bf16 to its COST pass too, so both passes
-    // of a PIT step sum the logits alike); the fp32 parity step keeps attn_kernel
-    const bool q4 = VB ? (a.dPreB || !grad) : a.dPreB != nullptr;
+  if constexpr (!(CRM && K == 3)) {  // the throughput steps' path (16-B aligned V; bf16 dPre), magnitude and
+                                     // cRM (K = 3 cRM: the quad kernel's 2 x 3 query halves spill; attn_kernel)
+    // fp32 V or cRM: only for a bf16-dPre caller (which passes dPre_bf16 to its COST pass too, so both
+    // passes of a PIT step sum the logits alike); the fp32 parity step keeps attn_kernel
+    const bool q4 = (VB && !CRM) ? (a.dPreB || !grad) : a.dPreB != nullptr;
     if (q4 && ((uintptr_t)(VB ? (const void*)a.Vb : (const void*)a.V) & 15) == 0) {
       if (grad)
-        hipLaunchKernelGGL((attn_q4_kernel<E, K, true, !VB>), grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((attn_q4_kernel<E, K, true, !VB, CRM>), grid, dim3(NT), 0, st, a);
       else
-        hipLaunchKernelGGL((attn_q4_kernel<E, K, false, !VB>), grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((attn_q4_kernel<E, K, false, !VB, CRM>), grid, dim3(NT), 0, st, a);
       DL4SS_CHECK_LAUNCH();
       return 0;
     }
