@@ -577,6 +577,8 @@ def train_main(args, cfg, dev, world, rank, pg):
     T = tr.T
     stft_ms = stft_instep_graph(tr, B, K, N)
     stft_bytes = B * (K + 1) * (4 * N + 4 * T * 129)  # mag-only STFT of mixture + K sources
+    if getattr(tr, "fast", False):
+        stft_bytes += B * T * 129 * 2  # + the mixtures' bf16 magnitudes (the recurrence's input rows, round 5)
     # the MFMA rooflines, each GEMM timed in isolation with the step's own kernel on the step's
     # operands (HIP events around 20 launches on the launch stream):
     #  * Linear + tanh -> bf16 V (M = B*T, N = F*E = 6450, K = 600, bias + tanh fused): the largest
