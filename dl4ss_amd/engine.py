@@ -361,6 +361,12 @@ class SepTrainer:
         _lib.call("dl4ss_f32_to_bf16_2d", _lib.ptr(x, True), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(out),
                   out.stride(0), _lib.stream_ptr())
 
+    def params_changed(self):
+        """Tell the trainer that net.flat was rewritten by means that may bypass torch's version
+        counter (a raw-pointer kernel, a collective, `.data`): the next step re-derives the bf16
+        weight copies instead of trusting the ones Adam keeps."""
+        self._wb_ver = None
+
     def _weights_to_bf16(self, force=False):
         """The bf16 copies of every layer's W_ih and the Linear weight, one launch
         (dl4ss_f32_to_bf16_2d_multi) -- only when the parameters changed by other means than this
@@ -383,7 +389,7 @@ class SepTrainer:
             assert all(x.is_contiguous() for x, _ in pairs)
             self._shadow = (n, (ctypes.c_longlong * n)(*[(x.data_ptr() - base) // 4 for x, _ in pairs]),
                             self._cvt_args[3], self._cvt_args[4], self._cvt_args[5], self._cvt_args[6])
-        if not force and self._shadow_on and self._wb_ver == net.flat._version:
+        if not force and self._shadow_on and self._wb_ver is not None and self._wb_ver == net.flat._version:
             return
         _lib.call("dl4ss_f32_to_bf16_2d_multi", *self._cvt_args, _lib.stream_ptr())
         self._wb_ver = net.flat._version
@@ -961,7 +967,8 @@ class SepTrainer:
             self.capture()
         self.spk.copy_(spk_idx)
         ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
-        if self.fast and self._wb_ver != self.net.flat._version:  # parameters changed outside Adam since the capture
+        if self.fast and (self._wb_ver is None or self._wb_ver != self.net.flat._version):
+            # parameters changed outside Adam since the capture
             self._weights_to_bf16()
         self.graph.replay()
         if self.graph_late is not None:
