@@ -252,6 +252,9 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
   const bool vec_c = (ldo % 4 == 0) && ((((uintptr_t)out) & 15) == 0) && col + 4 <= N;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+#ifdef GGL_NO_STORE  // diagnostic builds only (results wrong): the k-loop without the epilogue
+    if (M > 0) break;
+#endif
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
 #pragma unroll

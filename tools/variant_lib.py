@@ -22,9 +22,13 @@ def main(tag, defs):
     minimal = "--minimal" in defs
     if minimal:
         defs = [d for d in defs if d != "--minimal"] + ["-DRNN_EXP_MINIMAL"]
+    # --only=a.hip,b.hip: recompile just those sources, link the shipped build's other objects
+    only = [d.split("=", 1)[1].split(",") for d in defs if d.startswith("--only=")]
+    only = only[0] if only else (["birnn.hip"] if minimal else None)
+    defs = [d for d in defs if not d.startswith("--only=")]
 
     def comp(f):
-        if minimal and f != "birnn.hip":
+        if only is not None and f not in only:
             return os.path.join(B.OBJ, f[:-4] + ".o")
         o = f"{od}/{f[:-4]}.o"
         subprocess.run([B.HIPCC, *B.FLAGS, *B.FILE_FLAGS.get(f, []), *defs, "-I", B.CSRC, "-c",
