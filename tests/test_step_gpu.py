@@ -403,11 +403,14 @@ def test_dp_mean_of_half_batch_gradients_equals_full_batch(dev, precision, mode)
     assert err < (1e-5 if precision == "fp32" else 1e-3), err
 
 
-@pytest.mark.parametrize("precision,mode,B,cell,K,L,side", [("bf16", "pit", 4, "lstm", 2, 2, "0"),
-                                                         ("bf16", "pit", 4, "gru", 3, 2, "0"),
-                                                         ("bf16s", "label", 4, "lstm", 2, 2, "0"),
-                                                         ("bf16", "pit", 32, "lstm", 2, 4, "1")])
-def test_step_without_gradient_zeroing_bitwise_equals_zeroed(dev, monkeypatch, precision, mode, B, cell, K, L, side):
+@pytest.mark.parametrize("precision,mode,B,cell,K,L,side,lc", [("bf16", "pit", 4, "lstm", 2, 2, "0", None),
+                                                            ("bf16", "pit", 4, "gru", 3, 2, "0", None),
+                                                            ("bf16s", "label", 4, "lstm", 2, 2, "0", None),
+                                                            ("bf16s", "crm", 4, "gru", 2, 2, "0", None),
+                                                            ("bf16s", "label", 1, "gru", 2, 2, "0", 101),
+                                                            ("bf16", "pit", 32, "lstm", 2, 4, "1", None)])
+def test_step_without_gradient_zeroing_bitwise_equals_zeroed(dev, monkeypatch, precision, mode, B, cell, K, L, side,
+                                                             lc):
     """zero_free (the grouped bf16 backward's writers overwrite their gradient regions: beta-0 GEMMs,
     bias reduce, colsum / row sums, query backward zeroing the embedding rows no speaker owns) against
     the zeroed-buffer form (DL4SS_GRAD_ZERO=1) from the same state: bitwise equal losses, gradients and
@@ -423,8 +426,10 @@ def test_step_without_gradient_zeroing_bitwise_equals_zeroed(dev, monkeypatch, p
     out = {}
     for zero in ("1", "0"):
         monkeypatch.setenv("DL4SS_GRAD_ZERO", zero)
-        net = engine.SepNet(cell=cell, num_layers=L, adjust=cell == "lstm", device=dev, seed=17)
-        tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision)
+        net = engine.SepNet(cell=cell, num_layers=L, adjust=cell == "lstm", crm=mode == "crm", device=dev, seed=17)
+        if mode == "crm":  # logits below the cRM saturation (the reference's N(0,1) embedding saturates at once)
+            net.view("emb.layer.weight").mul_(0.1)
+        tr = engine.SepTrainer(net, B, K, N, mode=mode, precision=precision, loss_channels=lc)
         assert tr.zero_free == (zero == "0") and bool(tr.side) == (side == "1")
         for n in net.named_parameters():  # every parameter's region (the 16-B padding between them is
             net.view(n, net.grad).fill_(float("nan"))  # never written by anyone: it stays zero)
