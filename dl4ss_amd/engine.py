@@ -253,9 +253,12 @@ class SepTrainer:
         self.xw_split0 = self.split and xw != "0"
         # data parallel, bf16 step: the gradient leaves in two buckets ("can
         # overlap with BPTT of the lower layers").  The Linear / embedding / ADDJUST gradients are
-        # complete before the first BPTT (dW_lin then runs on its own, not in the grouped launch) and
-        # their all-reduce runs beside the BPTT chain; the recurrent layers' bucket follows the last
-        # BPTT.  DL4SS_DP_BUCKETS=0: one flat all-reduce after the step's backward.
+        # complete at the end of the BPTT chain (dW_lin on the side stream beside it, or on its own
+        # before it) and their all-reduce runs beside the recurrent layers' grouped weight-gradient
+        # launch; the recurrent layers' bucket follows that launch.  (Round 5 first started the side
+        # GEMM and the early all-reduce eagerly between two graph replays: the side GEMM then shared a
+        # hardware queue with the replayed BPTT chain and ran before it, 4.91 vs 3.51 ms per step.)
+        # DL4SS_DP_BUCKETS=0: one flat all-reduce after the step's backward.
         self.buckets = (process_group is not None and self.fast and net.L <= 5
                         and os.environ.get("DL4SS_DP_BUCKETS", "1") != "0")
         self._works = []
@@ -662,7 +665,7 @@ class SepTrainer:
             _lib.call("dl4ss_colsum_bf16_det_ex", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                       _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
                       self.colsum_part.numel() * 4, self._gbeta, st)
-        elif not self.buckets:  # (bucketed: _early_bucket forks it, with the early all-reduce)
+        else:
             self._side_launch()
 
     def _side_launch(self):
@@ -697,9 +700,12 @@ class SepTrainer:
         """Join: the current stream waits for the side stream's work."""
         torch.cuda.current_stream().wait_stream(self._side_stream)
 
-    def _backward_fast(self):
-        """The bf16 backward from the first BPTT on: the BPTT / dX chain down the layers, the bias
-        reduce and the grouped weight-gradient launch."""
+    def _backward_fast(self, part="all"):
+        """The bf16 backward from the first BPTT on: the BPTT / dX chain down the layers (part
+        "chain", the side stream joined at its end), then the bias reduce and the grouped
+        weight-gradient launch (part "wgrad")."""
+        if part == "wgrad":
+            return self._backward_wgrad()
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         NGH = _ngate(net.cell) * H
@@ -742,17 +748,19 @@ class SepTrainer:
                                  strideB=hp8, strideC=NGH * H, M=NGH, N=H, K=BT, ws=self.gl_ws)
             if l > 0:
                 dH = dH_next
-        # the side stream joins before the bias reduce (it ends inside the last BPTT): a join after the
+        # the side stream joins at the end of the chain (it ends inside the last BPTT): a join after the
         # grouped launch cost ~9 us more per step (the cross-queue wait in front of Adam; A/B x3, round 5)
-        early_join = self.side and not self.buckets and os.environ.get("DL4SS_SIDE_JOIN", "early") == "early"
-        if early_join:
+        if self.side:
             self._side_join()
+        if part == "all":
+            self._backward_wgrad()
+
+    def _backward_wgrad(self):
+        """The recurrent layers' bias reduce and grouped weight-gradient launch (after the chain)."""
         if self.defer_bias:
             self._bias_reduce()
-        if grouped:
-            dwg.run()
-        if self.side and not self.buckets and not early_join:  # dW_lin's side stream joins at the end of the backward
-            self._side_join()
+        if self.net.L <= 5:
+            self._weight_grad_group().run()
 
     def _bias_reduce(self):
         """Every layer's BPTT bias partials (DL4SS_RNN_DEFER_BIAS) into db_ih / db_hh, one launch."""
@@ -871,14 +879,10 @@ class SepTrainer:
         self._works.append(dp.allreduce_sum_async(self.net.grad_ext[self.net.bucket_split():], self.pg))
 
     def _early_bucket(self):
-        """Bucketed data parallel: the side stream's dW_lin (when on) and then, behind it on the same
-        stream, the early bucket's all-reduce -- both beside the BPTT chain that follows."""
-        if self.side:
-            self._side_launch()
-            with torch.cuda.stream(self._side_stream):
-                self.allreduce_early()
-        else:
-            self.allreduce_early()
+        """Bucketed data parallel: the early bucket's all-reduce (Linear -- formed on the side stream,
+        joined at the end of the chain --, embedding, ADDJUST), started after the BPTT chain and
+        running beside the recurrent layers' weight-gradient launch."""
+        self.allreduce_early()
 
     def allreduce_late(self):
         """Start the SUM all-reduce of the late bucket (the status flag and every recurrent layer)."""
@@ -914,11 +918,11 @@ class SepTrainer:
         loss = self.loss_and_grad()
         if self.buckets:
             self.backward_early()
+            self._backward_fast("chain")
             self._early_bucket()
-            self.backward_late()
+            self._backward_fast("wgrad")
+            self._status_flag()
             self.allreduce_late()
-            if self.side:
-                self._side_join()
         else:
             self.backward()
             self.allreduce()
@@ -946,7 +950,9 @@ class SepTrainer:
         step_graph().  The mixing kernel (its input pointer changes per batch), the RCCL
         all-reduce and Adam (its bias correction is a per-step host scalar) stay eager launches
         around the replay.  Bucketed data parallel: two graphs, split where the early bucket's
-        all-reduce starts (after backward_early).  Call after at least one eager step(), so every
+        all-reduce starts -- after the BPTT chain, which the side-stream dW_lin (forked and joined
+        inside the first graph) runs beside; the second graph (the recurrent layers' weight-gradient
+        launch) then runs beside that all-reduce.  Call after at least one eager step(), so every
         workspace exists before the capture."""
         import gc
 
@@ -965,9 +971,11 @@ class SepTrainer:
                     self.backward()
                 else:
                     self.backward_early()
+                    self._backward_fast("chain")
             if g2 is not None:
                 with torch.cuda.graph(g2, pool=g.pool()):
-                    self.backward_late()
+                    self._backward_fast("wgrad")
+                    self._status_flag()
         finally:
             if was_enabled:
                 gc.enable()
@@ -990,8 +998,6 @@ class SepTrainer:
             self._early_bucket()
             self.graph_late.replay()
             self.allreduce_late()
-            if self.side:
-                self._side_join()
         else:
             self.allreduce()
         self.optimizer_step()
