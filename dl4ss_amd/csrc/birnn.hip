@@ -2567,13 +2567,27 @@ DL4SS_API int dl4ss_birnn_plan_info(int cell, int B, int H, int precision, int m
   return 0;
 }
 
-// the larger of the fp32 and bf16 plans' needs (either precision may use the buffer);
-// -1 when neither plan exists
+// Sub-batch of a forward whose plan does not fit the co-residency budget at B: the fp32 VALU
+// plan of a wide layer (H = 600, the classifier: J <= 12, 50 workgroups per group) fits at most
+// B = 16 on a full part.  Rows never interact, so dl4ss_birnn_fwd_mean runs such a batch as
+// consecutive launches of (near-)equal sub-batches.  0 when no sub-batch fits either.
+static int split_batch(int cell, int B, int H, bool mf, Plan& ps) {
+  int fit = 0;
+  for (int b = B - 1; b >= 1 && !fit; --b)
+    if (make_plan(cell, b, H, ps, mf)) fit = b;
+  if (!fit) return 0;
+  const int n = (B + fit - 1) / fit;
+  const int bs = (B + n - 1) / n;
+  return make_plan(cell, bs, H, ps, mf) ? bs : 0;
+}
+
+// the larger of the fp32 and bf16 plans' needs (either precision may use the buffer; an fp32
+// forward planned as sub-batches counts its sub-batch plan); -1 when neither plan exists
 DL4SS_API long long dl4ss_birnn_workspace_bytes(int cell, int B, int H) {
   long long best = -1;
   for (bool mf : {false, true}) {
     Plan p;
-    if (!make_plan(cell, B, H, p, mf)) continue;
+    if (!make_plan(cell, B, H, p, mf) && (mf || split_batch(cell, B, H, mf, p) == 0)) continue;
     const long long n = workspace_bytes(p, H);
     if (n > best) best = n;
   }
@@ -2618,6 +2632,22 @@ DL4SS_API int dl4ss_birnn_fwd_mean(int cell, int precision, int B, int T, int H,
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && G && W_hh && b_hh && (out || out_bf16) && act && workspace && status);
   DL4SS_REQUIRE(cell == CELL_GRU || cs);
   Plan p;
+  if (precision == 0 && !make_plan(cell, B, H, p, false)) {
+    // the fp32 plan does not fit at this batch: consecutive sub-batch launches (split_batch),
+    // each zeroing the shared hand-off workspace itself (stream order keeps them apart)
+    const int bs = split_batch(cell, B, H, false, p);
+    DL4SS_REQUIRE(bs > 0 && out && !h_mean && !out_bf16 && !hprev_bf16);
+    const long long GH = (cell == CELL_LSTM ? 4LL : 3LL) * H;
+    for (int b0 = 0; b0 < B; b0 += bs) {
+      const long long r = (long long)b0 * T;  // (b, t) rows before the sub-batch
+      const int rc = dl4ss_birnn_fwd_mean(cell, 0, B - b0 < bs ? B - b0 : bs, T, H, G + r * 2 * GH, W_hh, b_hh,
+                                          out + r * 2 * H, hprev ? hprev + r * 2 * H : nullptr, act + r * 2 * 4 * H,
+                                          cs ? cs + r * 2 * H : nullptr, nullptr, nullptr, nullptr, workspace,
+                                          ws_bytes, status, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   DL4SS_REQUIRE(make_plan(cell, B, H, p, precision == 1));
   DL4SS_REQUIRE(ws_bytes >= workspace_bytes(p, H));
   hipStream_t st = as_stream(stream);

@@ -216,7 +216,10 @@ void dl4ss_debug_set_rnn_max_wg(int max_wg);
  * (every C2 / C4 step at B = 32): there it is cell-major (B,T,2,H,4), one 16-B record per cell,
  * written by the forward and read by dl4ss_birnn_bwd[_ex] of the same precision and shape.
  * precision 0: exact fp32 recurrent matvec (VALU); 1: bf16 operands on MFMA with fp32
- * accumulate (cell state, gates and all outputs stay fp32).
+ * accumulate (cell state, gates and all outputs stay fp32).  A precision-0 plan that does not
+ * fit the co-residency budget at B (H = 600: 50 workgroups per group, B <= 16 on a full part)
+ * runs as consecutive near-equal sub-batch launches on the same workspace (rows never interact;
+ * dl4ss_birnn_workspace_bytes sizes the workspace for the sub-batch plan).
  * *status != 0 after the call means a hand-off timed out (results invalid).
  * Replaces the cuDNN recurrence of nn.LSTM / nn.GRU(batch_first, bidirectional)
  * at TDAA_beta/main_run_sstune_EvalVer.py:282-293, Torch_multi/main_run.py:263-273. */

@@ -155,8 +155,13 @@ def test_c3_finite_window_matches_oracle(dev):
     assert first_ours is None and first_ref is None, (first_ours, first_ref)
 
 
-def test_c5_full_length_recursive(dev):
-    B, n, seed = 1, 32000, 7
+@pytest.mark.parametrize("B", [1, 32])
+def test_c5_full_length_recursive(dev, B):
+    """C5 in fp32 at T = 251: speaker ids, probabilities (2e-5 abs) and masks (1e-4 abs) against
+    oracle/recursive.py.  At B = 32 the H = 600 classifier's fp32 forward runs as two B = 16
+    launches (its plan needs 50 workgroups per group); ids are compared on every decision whose
+    probability gap exceeds 1e-4 (5x the fp32 bound), and must agree on at least 60 of the 64."""
+    n, seed = 32000, 7
     mix, cls, emb = _models(seed)
     X = _feats(B, n, seed)
     T = X.shape[1]
@@ -165,10 +170,27 @@ def test_c5_full_length_recursive(dev):
         ref = orc.recursive_extract(lambda x: mix(x), cls, emb.weight, X)
     out = _ours(dev, mix, cls, emb, B, T, "fp32").run(X.to(dev))
     torch.cuda.synchronize()
-    assert torch.equal(out["spk"].cpu().long(), ref["spk"]), (out["spk"], ref["spk"])
     for s in range(2):
         assert (out["probs"][s].cpu() - ref["probs"][s]).abs().max() < 2e-5
-    assert (out["masks"].cpu() - ref["masks"]).abs().max() < 1e-4
+    spk, rspk = out["spk"].cpu().long(), ref["spk"]
+    if B == 1:
+        assert torch.equal(spk, rspk), (spk, rspk)
+        assert (out["masks"].cpu() - ref["masks"]).abs().max() < 1e-4
+        return
+    agree = 0
+    for b in range(B):
+        seen = []
+        for s in range(2):
+            order = ref["probs"][s][b].sort(descending=True, stable=True).indices.tolist()
+            rank = next(i for i, k in enumerate(order) if k not in seen)
+            seen.append(order[rank])
+            p = ref["probs"][s][b].sort(descending=True).values
+            if bool((p[:rank + 1] - p[1:rank + 2]).min() > 1e-4):
+                assert int(spk[b, s]) == int(rspk[b, s]), (b, s, spk[b], rspk[b])
+            agree += int(spk[b, s]) == int(rspk[b, s])
+    assert agree >= 60, agree
+    rows = (spk == rspk).all(dim=1)
+    assert (out["masks"][rows].cpu() - ref["masks"][rows]).abs().max() < 1e-4
 
 
 # bf16 C5: the classifier probabilities' measured bf16 error is <= 9e-5 (B = 32, T = 251,
