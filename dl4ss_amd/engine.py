@@ -275,6 +275,14 @@ class SepTrainer:
         self.side = None
         self._side_stream = None
         self._side_gemm = None
+        # The side launch is enqueued after the first BPTT, its fork still at the dH GEMM (an event): the
+        # captured graph then keeps the chain on the main queue and puts the side GEMM on the second --
+        # the first-enqueued child of the fork stays on the parent's queue.  Enqueued before the BPTT
+        # the side GEMM kept it and the chain paid a cross-queue wait at the fork (11 vs 5 us) and at
+        # the join (9.5 vs 6 us): 3.457-3.463 vs 3.463-3.469 ms per step (A/B x3,
+        # profiles/r05_side_late_ab.txt).  DL4SS_SIDE_LATE=0 restores the early enqueue (A/B).
+        self._side_late = os.environ.get("DL4SS_SIDE_LATE", "1") != "0"
+        self._fork_ev = None
         side = os.environ.get("DL4SS_SIDE_DWLIN", "")
         if self.fast and net.L <= 5 and side != "0" and dev.type == "cuda":
             if side and side != "1":
@@ -665,6 +673,10 @@ class SepTrainer:
             _lib.call("dl4ss_colsum_bf16_det_ex", _lib.ptr(self.dPreb), self.dPreb.stride(0), BT, FE,
                       _lib.ptr(net.view("mix.Linear.bias", g)), _lib.ptr(self.colsum_part),
                       self.colsum_part.numel() * 4, self._gbeta, st)
+        elif self._side_late:
+            if self._fork_ev is None:
+                self._fork_ev = torch.cuda.Event()
+            self._fork_ev.record()  # the fork point; the side launch follows the first BPTT
         else:
             self._side_launch()
 
@@ -688,7 +700,10 @@ class SepTrainer:
                       transA=True, transB=False, beta=self._gbeta, splitk=split,
                       rowsum=net.view("mix.Linear.bias", g) if split == 1 else None)],
                 net.device, grid=grid, cfg=cfg, one_per_cu=one)
-        self._side_stream.wait_stream(torch.cuda.current_stream())
+        if self._side_late:
+            self._side_stream.wait_event(self._fork_ev)
+        else:
+            self._side_stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._side_stream):
             if self.side[2] != 1:  # split dW_lin: no row sums, the bias gradient by colsum
                 _lib.call("dl4ss_colsum_bf16_det_ex", _lib.ptr(self.dPreb), self.dPreb.stride(0), B * T, FE,
@@ -731,6 +746,8 @@ class SepTrainer:
                       _lib.ptr(dGb), _lib.ptr(dGhb) if gru else None, _lib.ptr(net.cat_view("bias_ih", l, g)),
                       _lib.ptr(net.cat_view("bias_hh", l, g)), _lib.ptr(self._ws_slot(l, True)), self.ws_bytes,
                       _lib.ptr(self.status), st)
+            if self.side and self._side_late and l == net.L - 1:
+                self._side_launch()
             if l > 0:  # the input gradient: all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
                 if self.dx_sk:
