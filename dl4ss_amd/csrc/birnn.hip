@@ -856,6 +856,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_STORE_WAVES
 #define FWD_STORE_WAVES 0
 #endif
+// The forward's saved gate activations and cell states (read back only by the BPTT, after the
+// rest of the forward, the loss and the Linear's backward) leave with non-temporal stores: C2
+// 3.438-3.449 vs 3.452-3.472 ms per step (A/B x3 twice, profiles/r05_nt_saves_ab.txt).  Measured
+// and not kept: the bf16 layer output / h_{t-1} copies non-temporal too (the next GEMMs read them
+// soon: 3.496-3.508 ms), and the BPTT's bf16 dG as well (3.529-3.532 ms).  0: plain stores (A/B).
+#ifndef FWD_NT_SAVES
+#define FWD_NT_SAVES 1
+#endif
   // FWD_STORE_WAVES (experiment, off): the saved-state stores of step s leave from waves 2-3
   // (matvec-only, idle after B2) during step s+1 instead of from the cell lanes after their publish:
   // the cell lanes stage {act, c, h_{t-1}, h} in LDS (double buffered by step parity), the last step
@@ -1312,12 +1320,22 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         const long long bt = (long long)bg * T + t;
         if (FWD_EXP_SKIP & 1) {
         } else if (a.act_cm) {
+#if FWD_NT_SAVES
+          typedef float nt_f4 __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(nt_f4{st[0], st[1], st[2], st[3]},
+                                      reinterpret_cast<nt_f4*>(a.act + ((bt * 2 + d) * H + cj) * 4));
+#else
           *reinterpret_cast<float4*>(a.act + ((bt * 2 + d) * H + cj) * 4) = make_float4(st[0], st[1], st[2], st[3]);
+#endif
         } else {
           float* actp = a.act + (bt * 2 + d) * (4 * H) + cj;
           actp[0] = st[0]; actp[H] = st[1]; actp[2 * H] = st[2]; actp[3 * H] = st[3];
         }
+#if FWD_NT_SAVES
+        if constexpr (CELL == CELL_LSTM) __builtin_nontemporal_store(cst, a.cs + (bt * 2 + d) * H + cj);
+#else
         if constexpr (CELL == CELL_LSTM) if (!(FWD_EXP_SKIP & 2)) a.cs[(bt * 2 + d) * H + cj] = cst;
+#endif
         const long long ho = bt * 2 * H + d * H + cj;
         if (a.hprev && !(FWD_EXP_SKIP & 32)) a.hprev[ho] = hst;
         if (a.out && !(FWD_EXP_SKIP & 4)) a.out[ho] = hn;
