@@ -864,6 +864,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_NT_SAVES
 #define FWD_NT_SAVES 1
 #endif
+// The bf16 h_{t-1} copy (read only by the weight-gradient launch at the end of the backward)
+// non-temporal too: 3.440-3.447 vs 3.449-3.454 ms per step (A/B x3, profiles/r05_nt_saves_ab.txt)
+#ifndef FWD_NT_HPREVB
+#define FWD_NT_HPREVB 1
+#endif
   // FWD_STORE_WAVES (experiment, off): the saved-state stores of step s leave from waves 2-3
   // (matvec-only, idle after B2) during step s+1 instead of from the cell lanes after their publish:
   // the cell lanes stage {act, c, h_{t-1}, h} in LDS (double buffered by step parity), the last step
@@ -1345,7 +1350,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         // direction's block 16-B aligned (the per-direction dW_hh operand)
         const int hp8 = (H + 7) & ~7, op8 = (2 * H + 7) & ~7;
         if (a.outb && !(FWD_EXP_SKIP & 8)) a.outb[bt * op8 + d * H + cj] = bf16_rne(hn);
+#if FWD_NT_HPREVB
+        if (a.hprevb) __builtin_nontemporal_store((unsigned short)bf16_rne(hst), a.hprevb + bt * 2 * hp8 + d * hp8 + cj);
+#else
         if (a.hprevb && !(FWD_EXP_SKIP & 16)) a.hprevb[bt * 2 * hp8 + d * hp8 + cj] = bf16_rne(hst);
+#endif
       }
       hst = hn;
     }
