@@ -403,7 +403,11 @@ def standin_main(args, world, rank):
         mask, _, _, _ = model(f, sp)
         loss, _ = om.loss_label_ordered(mask, f, Yt)
         loss.backward()
-        g = dp.allreduce_mean_(torch.cat([p.grad.reshape(-1) for p in params]), pg)
+        g = torch.cat([p.grad.reshape(-1) for p in params])
+        work = dp.allreduce_sum_async(g, pg)  # SUM, then the mean's 1 / world (as the trainer's Adam)
+        if work is not None:
+            work.wait()
+            g.mul_(1.0 / dp.world(pg))
         o = 0
         for p in params:
             p.grad.copy_(g[o:o + p.numel()].view_as(p))

@@ -5,6 +5,14 @@
 
 #define DL4SS_API extern "C" __attribute__((visibility("default")))
 
+// Timing-experiment macros that drop stores (results wrong) are accepted only in the experiment
+// variant libraries tools/variant_lib.py builds (it defines DL4SS_VARIANT_BUILD): a stray -D in a
+// product build stops the compile instead of shipping a library that silently skips work.
+#if !defined(DL4SS_VARIANT_BUILD) && (defined(FWD_EXP_SKIP) || defined(BWD_EXP_NO_DG) || defined(GGL_NO_STORE) || \
+                                      defined(RNN_EXP_MINIMAL))
+#error "FWD_EXP_SKIP / BWD_EXP_NO_DG / GGL_NO_STORE / RNN_EXP_MINIMAL are for tools/variant_lib.py builds only"
+#endif
+
 #define DL4SS_CHECK_LAUNCH()                        \
   do {                                              \
     hipError_t _e = hipGetLastError();              \

@@ -1,5 +1,6 @@
 """Data-parallel host logic: one process per GPU, the utterance
-batch sharded across ranks, one flat-gradient all-reduce per step.
+batch sharded across ranks, the flat gradient SUM-all-reduced once per step (flat, or in
+buckets), the mean's 1 / world applied inside the HIP Adam (dl4ss_adam_guarded_dp_scaled).
 
 Kept free of HIP calls so the multi-rank behaviour is testable with the ``gloo``
 backend on CPU (``tests/test_dp_cpu.py``); on the GPU box the same calls run over
@@ -17,19 +18,6 @@ def broadcast_params_(flat, pg=None, src=0):
     """Identical initial weights on every rank (rank `src`'s)."""
     if world(pg) > 1:
         dist.broadcast(flat, src, group=pg)
-    return flat
-
-
-def allreduce_mean_(flat, pg=None):
-    """grad <- mean over ranks of the per-rank grads.  Every rank's loss is a mean
-    over its own equal-sized shard, so the mean of the per-rank gradients is the
-    gradient of the global-batch mean loss (the single-GPU reference's objective)."""
-    if not (dist.is_available() and dist.is_initialized()):
-        return flat
-    n = world(pg)
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=pg)  # also at world size 1 (bench --dist)
-    if n > 1:
-        flat.mul_(1.0 / n)
     return flat
 
 

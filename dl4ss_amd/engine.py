@@ -71,7 +71,17 @@ class SepNet:
         self.grad_ext = torch.zeros(off + 4, device=self.device, dtype=torch.float32)
         self.grad = self.grad_ext[4:]
         self.dp_flag = self.grad_ext[0:1]
+        # generation of `flat` for writers torch's version counter does not see (the device-side
+        # Adam of any trainer on this net, a raw-pointer kernel, a collective): every such write
+        # bumps it (params_changed()), and a trainer trusts its bf16 weight copies only while
+        # (generation, flat._version) is what it was when the copies were made
+        self.generation = 0
         self.reset_parameters(seed)
+
+    def params_changed(self):
+        """Declare that `flat` was rewritten by means that may bypass torch's version counter:
+        every trainer on this net re-derives its bf16 weight copies on its next step."""
+        self.generation += 1
 
     def view(self, name, buf=None):
         off, shape = self.offsets[name]
@@ -262,6 +272,7 @@ class SepTrainer:
         self.buckets = (process_group is not None and self.fast and net.L <= 5
                         and os.environ.get("DL4SS_DP_BUCKETS", "1") != "0")
         self._works = []
+        self._in_chain = False
         # The Linear's weight and bias gradients on a SIDE STREAM beside the BPTT chain (round 5): the
         # persistent recurrence keeps its grid within the CUs minus 1/16 (dl4ss_birnn_plan_info), so
         # `free` CUs idle through the chain.  dW_lin (and the bias gradient as the row sums of the same
@@ -381,16 +392,24 @@ class SepTrainer:
 
     def params_changed(self):
         """Tell the trainer that net.flat was rewritten by means that may bypass torch's version
-        counter (a raw-pointer kernel, a collective, `.data`): the next step re-derives the bf16
-        weight copies instead of trusting the ones Adam keeps."""
+        counter (a raw-pointer kernel, a collective, `.data`): the next step of every trainer on
+        this net re-derives the bf16 weight copies instead of trusting the ones Adam keeps."""
+        self.net.params_changed()
         self._wb_ver = None
+
+    def _wb_key(self):
+        return (self.net.generation, self.net.flat._version)
+
+    def _wb_stale(self):
+        return self._wb_ver is None or self._wb_ver != self._wb_key()
 
     def _weights_to_bf16(self, force=False):
         """The bf16 copies of every layer's W_ih and the Linear weight, one launch
         (dl4ss_f32_to_bf16_2d_multi) -- only when the parameters changed by other means than this
         trainer's Adam, which writes the copies itself (dl4ss_adam_guarded_dp_scaled_bf16, round 5):
         a torch in-place op on net.flat (a checkpoint load, the DP broadcast, a test's state restore)
-        bumps its version counter, the device-side Adam does not."""
+        bumps its version counter, the device-side Adam does not -- it bumps the net's generation,
+        so another trainer on the same net sees the change."""
         net = self.net
         if not hasattr(self, "_cvt_args"):
             pairs = [(net.cat_view("weight_ih", l), self.wb_ih[l]) for l in range(net.L)]
@@ -407,10 +426,10 @@ class SepTrainer:
             assert all(x.is_contiguous() for x, _ in pairs)
             self._shadow = (n, (ctypes.c_longlong * n)(*[(x.data_ptr() - base) // 4 for x, _ in pairs]),
                             self._cvt_args[3], self._cvt_args[4], self._cvt_args[5], self._cvt_args[6])
-        if not force and self._shadow_on and self._wb_ver is not None and self._wb_ver == net.flat._version:
+        if not force and self._shadow_on and not self._wb_stale():
             return
         _lib.call("dl4ss_f32_to_bf16_2d_multi", *self._cvt_args, _lib.stream_ptr())
-        self._wb_ver = net.flat._version
+        self._wb_ver = self._wb_key()
 
     @staticmethod
     def _hilo(x, y, segw, pattern, nseg=3):
@@ -721,6 +740,16 @@ class SepTrainer:
         weight-gradient launch (part "wgrad")."""
         if part == "wgrad":
             return self._backward_wgrad()
+        self._in_chain = True
+        try:
+            self._backward_chain()
+        finally:
+            self._in_chain = False
+        if part == "all":
+            self._backward_wgrad()
+
+    def _backward_chain(self):
+        """The BPTT / dX chain down the layers, the side stream joined at its end."""
         net, B, T, H = self.net, self.B, self.T, self.net.H
         BT = B * T
         NGH = _ngate(net.cell) * H
@@ -769,8 +798,6 @@ class SepTrainer:
         # grouped launch cost ~9 us more per step (the cross-queue wait in front of Adam; A/B x3, round 5)
         if self.side:
             self._side_join()
-        if part == "all":
-            self._backward_wgrad()
 
     def _backward_wgrad(self):
         """The recurrent layers' bias reduce and grouped weight-gradient launch (after the chain)."""
@@ -875,17 +902,31 @@ class SepTrainer:
             _lib.call("dl4ss_status_flag", _lib.ptr(self.status), _lib.ptr(self.net.dp_flag), _lib.stream_ptr())
 
     def allreduce(self):
-        """The RCCL all-reduce (SUM) of the whole flat gradient; Adam applies the 1 / world of the
-        mean (no separate pass over the buffer).  The slot in front of the gradient carries this
-        rank's hand-off status flag (dl4ss_status_flag, written at the end of backward()): after
-        the sum it is non-zero on every rank iff a hand-off timed out on any rank, and the guarded
-        Adam reads it (a timed-out rank's incomplete gradient must not reach the healthy
-        ranks' weights either).  Bucketed steps (self.buckets) use allreduce_early / _late."""
+        """START the RCCL all-reduce (SUM) of the whole flat gradient, asynchronously; Adam applies
+        the 1 / world of the mean (no separate pass over the buffer).  The slot in front of the
+        gradient carries this rank's hand-off status flag (dl4ss_status_flag, written at the end of
+        backward()): after the sum it is non-zero on every rank iff a hand-off timed out on any
+        rank, and the guarded Adam reads it (a timed-out rank's incomplete gradient must
+        not reach the healthy ranks' weights either).  Bucketed steps (self.buckets) use
+        allreduce_early / _late.
+
+        Contract: net.grad is complete only after wait_allreduce() (optimizer_step()
+        calls it), and it then holds the SUM over ranks, not the mean -- grad_mean() is the mean."""
         if self.pg is None:
             return
         from . import dp
 
+        self._no_collective_in_chain()
         self._works.append(dp.allreduce_sum_async(self.net.grad_ext, self.pg))
+
+    def _no_collective_in_chain(self):
+        """Invariant: no collective starts while the BPTT chain is being enqueued.  The
+        persistent recurrence needs all its workgroups co-resident, and the side-stream dW_lin holds
+        every CU the recurrence plan leaves free for the whole chain; a collective kernel placed
+        beside the chain could keep a recurrence workgroup off the device (a hand-off timeout, then a
+        refused step).  Every all-reduce of the step therefore starts after the chain."""
+        if self._in_chain:
+            raise RuntimeError("a gradient all-reduce was started inside the BPTT chain")
 
     def allreduce_early(self):
         """Start the SUM all-reduce of the early bucket (Linear, embedding, ADDJUST gradients):
@@ -893,6 +934,7 @@ class SepTrainer:
         BPTT chain that follows."""
         from . import dp
 
+        self._no_collective_in_chain()
         self._works.append(dp.allreduce_sum_async(self.net.grad_ext[self.net.bucket_split():], self.pg))
 
     def _early_bucket(self):
@@ -905,14 +947,25 @@ class SepTrainer:
         """Start the SUM all-reduce of the late bucket (the status flag and every recurrent layer)."""
         from . import dp
 
+        self._no_collective_in_chain()
         self._works.append(dp.allreduce_sum_async(self.net.grad_ext[:self.net.bucket_split()], self.pg))
 
-    def _wait_allreduce(self):
-        """The current stream waits for every all-reduce started this step (before Adam)."""
+    def wait_allreduce(self):
+        """The current stream waits for every all-reduce started this step: net.grad then holds the
+        gradient SUM over ranks (for callers that inspect or clip it before optimizer_step(), which
+        calls this itself; grad_mean() gives the mean)."""
         for w in self._works:
             if w is not None:
                 w.wait()
         self._works = []
+
+    _wait_allreduce = wait_allreduce
+
+    def grad_mean(self):
+        """The global-batch mean gradient (a new tensor): the all-reduced SUM x 1 / world, the
+        arithmetic the guarded Adam applies (gscale)."""
+        self.wait_allreduce()
+        return self.net.grad * (1.0 / self.world)
 
     def optimizer_step(self):
         """Adam on device; refused (parameters untouched, loss[0] = NaN) when a recurrence
@@ -923,9 +976,16 @@ class SepTrainer:
         parallel: the gradient is the SUM over ranks, scaled by 1 / world inside the update."""
         self._wait_allreduce()
         self.step_count += 1
+        shadow = self._shadow if (self._shadow_on and hasattr(self, "_shadow")) else None
         ops.adam_(self.net.flat, self.net.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps,
                   status=self.status, loss=self.loss, dp_flag=self.net.dp_flag, gscale=1.0 / self.world,
-                  shadow=self._shadow if (self._shadow_on and hasattr(self, "_shadow")) else None)
+                  shadow=shadow)
+        # the update bypasses torch's version counter: a new generation of the parameters, whose bf16
+        # copies only this trainer holds (written by the same launch), and only if they were current
+        # before it -- copies stale before the update stay stale after it
+        fresh = shadow is not None and not self._wb_stale()
+        self.net.params_changed()
+        self._wb_ver = self._wb_key() if fresh else None
 
     def step(self, raw, gains, spk_idx):
         """One full training step on device-resident inputs; returns the loss tensor (not synced)."""
@@ -1007,7 +1067,7 @@ class SepTrainer:
             self.capture()
         self.spk.copy_(spk_idx)
         ops.mix_sources(raw, gains, out_src=self.src, out_mix=self.mix, stats_ws=self.stats)
-        if self.fast and (self._wb_ver is None or self._wb_ver != self.net.flat._version):
+        if self.fast and self._wb_stale():
             # parameters changed outside Adam since the capture
             self._weights_to_bf16()
         self.graph.replay()

@@ -104,12 +104,18 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
     assert not bad, (bad, errs)
     if precision != "fp32" or tr.rnn_precision != "fp32":
         return {"masked_rel_l2": rel}  # a first Adam step is ~lr*sign(g): not comparable where bf16 moved a small gradient's sign
-    # Adam-updated parameters: first step moves each weight by ~lr*sign(g); allow sign
-    # disagreements only where the gradient itself is at rounding level
+    _assert_adam_params_close(net, ref, grads_ref, errs)
+    return {"masked_rel_l2": rel}
+
+
+def _assert_adam_params_close(net, ref, grads_ref, errs, lr=2e-4, eps=1e-8):
+    """The HIP Adam-updated parameters (net) against the oracle's torch.optim.Adam step (ref) after a
+    first step, which moves each weight by ~lr*sign(g): a disagreeing weight must be explained by that
+    tensor's measured gradient error errs[name] (relative to its largest reference gradient)."""
     for name, p in ref.named_parameters():
         ours = net.view(name).cpu()
         diff = (ours - p.detach()).abs()
-        assert diff.max().item() <= 2.1 * 2e-4, name
+        assert diff.max().item() <= 2.1 * lr, name
         moved = diff > 1e-6
         if moved.any():
             # Adam's first step is lr*g/(|g|+eps): sign-sensitive, and steep near |g| ~ eps
@@ -118,12 +124,10 @@ def _compare_step(dev, cell, L, B, K, N, mode, tol_loss=1e-4, tol_grad=2e-3, los
             # flip (|g| <= err), or a step change within 4 lr*err*eps/(|g|+eps)^2; and rare
             gr = grads_ref[name]
             err_abs = errs[name] * max(gr.abs().max().item(), 1e-30)
-            lr, eps = 2e-4, 1e-8
             ga = gr.abs()
             ok = (ga <= err_abs) | (diff <= 4 * lr * err_abs * eps / (ga + eps) ** 2)
             assert bool(ok[moved].all()), (name, int(moved.sum()), gr[moved & ~ok][:8])
             assert moved.float().mean().item() < 1e-2, name
-    return {"masked_rel_l2": rel}
 
 
 def test_step_bilstm_label_order(dev):
@@ -371,36 +375,134 @@ def test_step_c4_pit_3spk_gradients(dev):
     _compare_step(dev, "gru", 2, 4, 3, 8000, "pit", adjust=False)
 
 
-@pytest.mark.parametrize("precision,mode", [("fp32", "label"), ("bf16", "pit")])
-def test_dp_mean_of_half_batch_gradients_equals_full_batch(dev, precision, mode):
-    """The data-parallel arithmetic of SepTrainer (dp.allreduce_mean_ of per-rank flat
-    gradients, each rank scaling its loss by its LOCAL batch: s1 = 1/(B_local K T F),
-    s2 = 0.5/(B_local T F)) at world size 1: the mean of the flat net.grad of two half-batch
-    steps equals the full-batch step's net.grad -- fused bias gradients, query / ADDJUST
-    gradients and the sum-to-one term included."""
-    B, K, N = 4, 2, 4000
+@pytest.mark.parametrize("precision,mode,cell", [("fp32", "label", "lstm"), ("bf16", "pit", "lstm"),
+                                                 ("bf16", "pit", "gru")])
+def test_dp_scaled_adam_on_summed_half_batches_equals_full_batch_step(dev, precision, mode, cell):
+    """The data-parallel step's N > 1 arithmetic through the shipped kernels, on one GPU: two
+    "ranks" take half-batch steps on the same weights (each scaling its loss by its LOCAL batch,
+    s1 = 1/(B_local K T F), s2 = 0.5/(B_local T F)) and write their status flag into the slot in front
+    of the flat gradient (dl4ss_status_flag); the element-wise sum of the two extended gradients is
+    what the SUM all-reduce leaves on every rank; SepTrainer.optimizer_step at world 2 applies it with
+    gscale = 1/2 inside the guarded Adam (dl4ss_adam_guarded_dp_scaled[_bf16]).  Checked against
+      - the same Adam at world 1 on the pre-halved gradient: bitwise parameters, moments and (bf16)
+        the Adam-kept bf16 weight copies, themselves bitwise a fresh conversion of the new weights;
+      - the full-batch step at world 1: gradient, first moment and parameters (first Adam step);
+      - fp32: the oracle's global-batch torch.optim.Adam step (the reference's objective, the mean
+        loss over the whole batch: TDAA_beta/main_run_sstune_EvalVer.py:641,673-675);
+    and a summed flag of 1 (one peer's hand-off timed out) refuses the update on every rank."""
+    from dl4ss_amd import _lib
+
+    B, K, N, L, seed = 4, 2, 8000, 2, 13
+    adjust = cell == "lstm"
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=21)
     src, spk, u = gen.batch(B)
     gains = synth.gains_for(u, K)
     raw = torch.from_numpy(src.astype(np.float32)).to(dev)
     g = torch.from_numpy(gains.astype(np.float32)).to(dev)
     sp = torch.from_numpy(spk.astype(np.int32)).to(dev)
-    net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=13)
 
-    def grads(lo, hi):
+    def new_net():
+        return engine.SepNet(cell=cell, num_layers=L, adjust=adjust, device=dev, seed=seed)
+
+    def grad_step(net, lo, hi):
+        """One rank's forward + backward on utterances [lo, hi); returns (trainer, its grad_ext)."""
         tr = engine.SepTrainer(net, hi - lo, K, N, mode=mode, precision=precision)
         tr.spk.copy_(sp[lo:hi])
         tr.features(raw[lo:hi].contiguous(), g[lo:hi].contiguous())
         tr.forward()
         tr.loss_and_grad()
         tr.backward()
+        # the rank's status flag in front of its gradient (the trainer writes it only with a process group)
+        _lib.call("dl4ss_status_flag", _lib.ptr(tr.status), _lib.ptr(net.dp_flag), _lib.stream_ptr())
+        torch.cuda.synchronize()
         tr.check()
-        return net.grad.detach().clone()
+        return tr, net.grad_ext.detach().clone()
 
-    full = grads(0, B)
-    half = 0.5 * (grads(0, B // 2) + grads(B // 2, B))
-    err = float((half - full).abs().max() / full.abs().max())
+    # --- two ranks, one SUM all-reduce, Adam at world 2 (gscale 1/2)
+    net = new_net()
+    tr0, g0 = grad_step(net, 0, B // 2)
+    _, g1 = grad_step(net, B // 2, B)
+    summed = g0 + g1
+    assert float(summed[0]) == 0.0  # no rank timed out
+    net.grad_ext.copy_(summed)
+    tr0.world = 2
+    tr0.optimizer_step()
+    tr0.check()
+    assert tr0.step_count == 1
+
+    # --- the same Adam at world 1 on the pre-halved sum: bitwise (x 0.5 is exact in fp32)
+    netx = new_net()
+    trx, _ = grad_step(netx, 0, B // 2)
+    netx.grad_ext.copy_(summed * 0.5)
+    trx.optimizer_step()
+    trx.check()
+    torch.cuda.synchronize()
+    assert torch.equal(net.flat, netx.flat)
+    assert torch.equal(tr0.m, trx.m) and torch.equal(tr0.v, trx.v)
+    if tr0.fast:
+        assert tr0._shadow_on and not tr0._wb_stale()  # the copies Adam kept are trusted ...
+
+        def fresh(x, like):
+            y = torch.zeros_like(like)
+            _lib.call("dl4ss_f32_to_bf16_2d", _lib.ptr(x), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(y),
+                      y.stride(0), _lib.stream_ptr())
+            return y
+
+        torch.cuda.synchronize()
+        for l in range(L):  # ... and are bitwise a fresh conversion of the updated weights
+            w = net.cat_view("weight_ih", l)
+            assert torch.equal(tr0.wb_ih[l][:, :w.shape[1]], fresh(w, tr0.wb_ih[l])[:, :w.shape[1]]), l
+            assert torch.equal(tr0.wb_ih[l], trx.wb_ih[l]), l
+        assert torch.equal(tr0.wb_lin, trx.wb_lin)
+
+    # --- the full-batch step at world 1
+    netf = new_net()
+    trf, gf = grad_step(netf, 0, B)
+    trf.optimizer_step()
+    trf.check()
+    mean = 0.5 * summed
+    err = float((mean[4:] - gf[4:]).abs().max() / gf[4:].abs().max())
     assert err < (1e-5 if precision == "fp32" else 1e-3), err
+    merr = float((tr0.m - trf.m).abs().max() / trf.m.abs().max())
+    assert merr < (1e-5 if precision == "fp32" else 1e-3), merr
+    dpar = (net.flat - netf.flat).abs()
+    assert float(dpar.max()) <= 2.1 * tr0.lr
+    # a first Adam step moves each weight by ~lr sign(g): disagreements only where g is at rounding level
+    flip = dpar > 1e-6
+    tiny = gf[4:].abs() <= (1e-5 if precision == "fp32" else 1e-3) * gf[4:].abs().max()
+    assert bool(tiny[flip].all()), int((flip & ~tiny).sum())
+
+    # --- fp32: against the oracle's global-batch Adam step
+    if precision == "fp32":
+        ref = om.SepModel(cell=cell, num_layers=L, adjust=adjust)
+        ref.load_state_dict({k: v.cpu() for k, v in new_net().state_dict().items()})
+        feats, X, Y = _oracle_features(src, gains, False)
+        opt = om.make_adam(ref)
+        opt.zero_grad()
+        mask, _, _, _ = ref(feats, torch.from_numpy(spk))
+        loss_ref, _ = om.loss_label_ordered(mask, X, Y)
+        loss_ref.backward()
+        grads_ref = {n: p.grad.detach().clone() for n, p in ref.named_parameters()}
+        opt.step()
+        errs = {}
+        for name, gr in grads_ref.items():
+            ours = net.view(name, mean[4:]).cpu()
+            errs[name] = (ours - gr).abs().max().item() / max(gr.abs().max().item(), 1e-30)
+        assert max(errs.values()) < 2e-3, errs
+        _assert_adam_params_close(net, ref, grads_ref, errs)
+
+    # --- one peer's hand-off timed out: its flag sums to 1 and every rank refuses the update
+    before = net.flat.detach().clone()
+    m_before = tr0.m.detach().clone()
+    net.grad_ext.copy_(summed)
+    net.grad_ext[0] = 1.0
+    tr0.optimizer_step()
+    torch.cuda.synchronize()
+    assert torch.equal(net.flat, before) and torch.equal(tr0.m, m_before)
+    assert torch.isnan(tr0.loss[0]).item() and int(tr0.status[1]) == 1
+    with pytest.raises(RuntimeError, match="peer"):
+        tr0.check()
+    assert tr0.step_count == 1  # the refused step is taken back out of the bias corrections
 
 
 @pytest.mark.parametrize("precision,mode,B,cell,K,L,side,lc", [("bf16", "pit", 4, "lstm", 2, 2, "0", None),
@@ -487,6 +589,43 @@ def test_adam_bf16_shadow_copies_equal_fresh_conversion(dev):
     tr.step_graph(*batch)
     tr.check()
     check()
+
+
+def test_two_trainers_on_one_net_never_read_stale_bf16_copies(dev, monkeypatch):
+    """the bf16 weight copies a trainer's Adam keeps are trusted only while the net's
+    (generation, version) is what that Adam left -- another trainer's Adam on the same SepNet (which
+    bypasses torch's version counter) bumps the generation.  Two trainers (different batch sizes)
+    stepping one net alternately, eager and graph steps, are bitwise the same run with a conversion
+    every step (DL4SS_ADAM_SHADOW=0)."""
+    B, K, N = 4, 2, 8000
+    gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=37)
+    batches = []
+    for _ in range(3):
+        src, spk, u = gen.batch(B)
+        batches.append((torch.from_numpy(src.astype(np.float32)).to(dev),
+                        torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
+                        torch.from_numpy(spk.astype(np.int32)).to(dev)))
+    half = [tuple(t[:2].contiguous() for t in b) for b in batches]
+    out = {}
+    for shadow in ("0", "1"):
+        monkeypatch.setenv("DL4SS_ADAM_SHADOW", shadow)
+        net = engine.SepNet(cell="lstm", num_layers=2, device=dev, seed=41)
+        ta = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
+        tb = engine.SepTrainer(net, 2, K, N, mode="pit", precision="bf16")
+        assert ta._shadow_on == tb._shadow_on == (shadow == "1")
+        losses = []
+        for i in range(3):
+            losses.append(ta.step(*batches[i]).clone())
+            losses.append(tb.step(*half[i]).clone())
+        for i in range(3):
+            losses.append(ta.step_graph(*batches[i]).clone())
+            losses.append(tb.step_graph(*half[i]).clone())
+        ta.check()
+        tb.check()
+        out[shadow] = (torch.stack(losses), net.flat.detach().clone())
+        del ta, tb
+    assert torch.equal(out["0"][0], out["1"][0])
+    assert torch.equal(out["0"][1], out["1"][1])
 
 
 @pytest.mark.parametrize("cell,K", [("lstm", 2), ("gru", 3)])

@@ -25,7 +25,7 @@ def main(tag, defs):
     # --only=a.hip,b.hip: recompile just those sources, link the shipped build's other objects
     only = [d.split("=", 1)[1].split(",") for d in defs if d.startswith("--only=")]
     only = only[0] if only else (["birnn.hip"] if minimal else None)
-    defs = [d for d in defs if not d.startswith("--only=")]
+    defs = [d for d in defs if not d.startswith("--only=")] + ["-DDL4SS_VARIANT_BUILD"]
 
     def comp(f):
         if only is not None and f not in only:
