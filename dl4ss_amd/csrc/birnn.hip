@@ -773,8 +773,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
   constexpr int NXQ = xw_nxq(BC);       // DMA pieces per prefetch wave and step
   constexpr int XSL = xw_slot(BC);      // bf16 per step slot
   constexpr int NSLOT = 3 * SPB;
-  unsigned short* sxb = reinterpret_cast<unsigned short*>(
-      (reinterpret_cast<uintptr_t>(spub + BC * PKU) + 255) & ~static_cast<uintptr_t>(255));
+  // (advanced from spub by element arithmetic, not through an integer cast: the cast lost the LDS
+  //  address space and every read of the ring (the projection's B fragments) compiled to a FLAT load,
+  //  counted in vmcnt as well as lgkmcnt -- 120 per fused kernel, round 6)
+  unsigned short* const sx0 = spub + BC * PKU;
+  const unsigned sxpad = (256u - ((unsigned)reinterpret_cast<uintptr_t>(sx0) & 255u)) & 255u;
+  unsigned short* sxb = sx0 + sxpad / 2;
 
   // ---- W_hh tile of this wave as bf16 A fragments: lane holds A[row tile*16 + (lane&15)][k]
   bf16x8 afrag[KSMAX];
