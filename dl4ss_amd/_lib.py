@@ -36,8 +36,6 @@ SIGNATURES = {
     "dl4ss_colsum_bf16_det": [P, LL, I, I, P, P, LL, P],
     "dl4ss_colsum_bf16_det_ex": [P, LL, I, I, P, P, LL, F, P],
     "dl4ss_gemm_bf16_gl_ws_bytes": [I, I, I, I, I],
-    "dl4ss_gemm_bf16_gl_streamk_ws_bytes": [I, I, I, I],
-    "dl4ss_gemm_bf16_gl_streamk": [I, I, I, I, I, P, LL, P, LL, P, LL, F, I, P, LL, P],
     "dl4ss_gemm_gl_set_config": [I],
     "dl4ss_gemm_bf16_gl": [I, I, I, I, I, P, LL, P, LL, P, LL, P, I, F, I, I, LL, LL, LL, P, LL, P],
     "dl4ss_gemm_bf16_gl_grouped_ws_bytes": [I, P, P, P, P],
@@ -91,7 +89,6 @@ SIGNATURES = {
 # entry points that return a value rather than a hipError_t
 RESTYPES = {"dl4ss_birnn_workspace_bytes": ctypes.c_longlong, "dl4ss_colsum_bf16_part_bytes": ctypes.c_longlong,
             "dl4ss_gemm_bf16_gl_ws_bytes": ctypes.c_longlong,
-            "dl4ss_gemm_bf16_gl_streamk_ws_bytes": ctypes.c_longlong,
             "dl4ss_gemm_bf16_gl_grouped_ws_bytes": ctypes.c_longlong, "dl4ss_attn_nblk": ctypes.c_int,
             "dl4ss_attn_dot_nblk": ctypes.c_int, "dl4ss_debug_set_spin_limit": None,
             "dl4ss_debug_set_place_force": None, "dl4ss_debug_set_rnn_max_wg": None}

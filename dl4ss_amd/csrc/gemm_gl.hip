@@ -658,106 +658,6 @@ __global__ __launch_bounds__(256) void gemm_gl_reduce_kernel(int M, int N, int S
 }
 
 // ---------------------------------------------------------------------------------------------
-// Stream-K (round 5): the tiles x k-tiles iterations of ONE GEMM dealt in equal contiguous ranges to a
-// fixed grid (two workgroups per CU), tile-major, so every workgroup runs the same number of k-tiles
-// whatever the tile count.  The step's dX (315 tiles on 512 workgroup slots: the CUs holding two tiles
-// set the time) and dH are the shapes it is for.  A tile whose iterations one workgroup covers is
-// written directly (beta as gemm_gl_kernel); a tile split across workgroups leaves one fp32 partial per
-// segment (segment s = this workgroup's rank among the tile's owners) in slab s, and
-// gemm_gl_sk_fixup_kernel adds the segments in order: deterministic, bitwise reproducible.
-__device__ __forceinline__ long long sk_begin(int g, long long iters, int G) { return (long long)g * iters / G; }
-// the workgroup whose range holds iteration x
-__device__ __forceinline__ int sk_owner(long long x, long long iters, int G) {
-  int g = (int)(x * G / iters);
-  while (g + 1 < G && sk_begin(g + 1, iters, G) <= x) ++g;
-  while (g > 0 && sk_begin(g, iters, G) > x) --g;
-  return g;
-}
-// tile index <-> (tm, tn): the GROUP-of-8 M swizzle of gemm_gl_kernel
-__device__ __forceinline__ void sk_tile_mn(int tile, int gm, int gn, int& tm, int& tn) {
-  constexpr int GROUP = 8;
-  const int gsize = GROUP * gn;
-  const int first_m = (tile / gsize) * GROUP;
-  const int gm_here = min(gm - first_m, GROUP);
-  tm = first_m + (tile % gsize) % gm_here;
-  tn = (tile % gsize) / gm_here;
-}
-template <bool A_KC, bool B_KC, class CF>
-__global__ __launch_bounds__(CF::NT, 2) void gemm_gl_sk_kernel(int M, int N, int K, const unsigned short* __restrict__ A,
-                                                               long long lda, const unsigned short* __restrict__ B,
-                                                               long long ldb, float* __restrict__ C, long long ldc,
-                                                               float beta, int gm, int gn, int nk, long long iters,
-                                                               float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
-  const int G = gridDim.x;
-  // XCD-major order (gemm_gl_kernel's remap): consecutive ranges -- neighbouring tiles -- on one XCD
-  const int L = blockIdx.x;
-  const int xcd = L % 8, q8 = G / 8, r8 = G % 8;
-  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + L / 8;
-  const long long it1 = sk_begin(g + 1, iters, G);
-  bool first = true;
-  for (long long it = sk_begin(g, iters, G); it < it1;) {
-    const int tile = (int)(it / nk);
-    const int ka = (int)(it - (long long)tile * nk);
-    const int kb = (int)min((long long)nk, ka + (it1 - it));
-    const long long t0 = (long long)tile * nk;
-    const int own0 = sk_owner(t0, iters, G), own1 = sk_owner(t0 + nk - 1, iters, G);
-    int tm, tn;
-    sk_tile_mn(tile, gm, gn, tm, tn);
-    const int kbeg = ka * BK, kspan = min(K, kb * BK) - kbeg;
-    if (!first) __syncthreads();  // the previous segment's epilogue is done with the LDS
-    first = false;
-    if (own0 == own1)
-      gl_tile<A_KC, B_KC, EPI_NONE, false, CF>(smem, M, N, A, lda, B, ldb, C, ldc, nullptr, beta, tm * CF::BM, tn * BN,
-                                              kbeg, kspan, nullptr);
-    else
-      gl_tile<A_KC, B_KC, EPI_NONE, true, CF>(smem, M, N, A, lda, B, ldb, C, ldc, nullptr, 0.0f, tm * CF::BM, tn * BN,
-                                             kbeg, kspan, part + (long long)(g - own0) * M * N);
-    it += kb - ka;
-  }
-}
-// C = beta C + sum_s slab[s] (s in order) over the tiles split across workgroups; four columns per thread
-template <int BM>
-__global__ __launch_bounds__(256) void gemm_gl_sk_fixup_kernel(int M, int N, int gm, int gn, int nk, long long iters,
-                                                               int G, const float* __restrict__ part,
-                                                               float* __restrict__ C, long long ldc, float beta) {
-  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
-  const long long mn = (long long)M * N;
-  if (i >= mn) return;
-  const int r = (int)(i / N), c = (int)(i - (long long)r * N);
-  constexpr int GROUP = 8;
-  const int tm = r / BM, tn = c / BN;
-  const int first_m = (tm / GROUP) * GROUP, gm_here = min(gm - first_m, GROUP);
-  const int tile = (tm / GROUP) * (GROUP * gn) + tn * gm_here + (tm - first_m);
-  const long long t0 = (long long)tile * nk;
-  const int own0 = sk_owner(t0, iters, G), own1 = sk_owner(t0 + nk - 1, iters, G);
-  if (own0 == own1) return;  // written directly by its one workgroup
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int sgi = 0; sgi <= own1 - own0; ++sgi) {
-    const float4 v = *reinterpret_cast<const float4*>(part + (long long)sgi * mn + i);
-    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-  }
-  float* cp = C + (long long)r * ldc + c;
-  if (beta != 0.0f) {
-    const float4 o = *reinterpret_cast<const float4*>(cp);
-    a.x += beta * o.x; a.y += beta * o.y; a.z += beta * o.z; a.w += beta * o.w;
-  }
-  *reinterpret_cast<float4*>(cp) = a;
-}
-// CUs of the current device (0 when none is visible)
-inline int gl_cu_count() {
-  int dev = 0, cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  return cu;
-}
-// segments a tile can span at most: ceil(nk / min range) + 1
-inline int sk_max_segments(long long iters, int G, int nk) {  // G <= iters: every range non-empty
-  const long long per = std::max<long long>(1, iters / G);
-  return (int)std::min<long long>(G, (nk + per - 1) / per + 1);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Grouped launch: up to GMAXP independent GEMMs (the step's weight gradients: dW_lin and every
 // layer's dW_ih / dW_hh, each its own M x N x K and split-K factor) as ONE grid.  One by one they
 // under-fill the chip (dW_ih: 95 tiles x 4 splits; dW_hh: 2 x 30 tiles x 8 splits) and each pays its
@@ -1050,58 +950,6 @@ DL4SS_API int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, co
   if (!a_kc && b_kc) return launch<false, true>(GGL_ARGS);
   return launch<false, false>(GGL_ARGS);
 #undef GGL_ARGS
-}
-
-// Stream-K form of dl4ss_gemm_bf16_gl (EPI_NONE, no bias, batch 1): C = op(A) op(B) + beta C over a
-// fixed grid of `grid` workgroups (<= 0: two per CU) dealt equal ranges of the tiles x k-tiles
-// iterations; split tiles' partials in ws (dl4ss_gemm_bf16_gl_streamk_ws_bytes) and one fixed-order
-// fixup launch.  Needs N % 4 == 0, ldc % 4 == 0 and a 16-B aligned C.
-DL4SS_API long long dl4ss_gemm_bf16_gl_streamk_ws_bytes(int M, int N, int K, int grid) {
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
-  if (grid <= 0) grid = 2 * std::max(1, gl_cu_count());
-  const long long tiles = (long long)((M + 127) / 128) * ((N + BN - 1) / BN);
-  const int nk = (K + BK - 1) / BK;
-  grid = (int)std::min<long long>(grid, tiles * nk);
-  return (long long)sk_max_segments(tiles * nk, grid, nk) * M * N * 4;
-}
-
-DL4SS_API int dl4ss_gemm_bf16_gl_streamk(int transA, int transB, int M, int N, int K, const void* A, long long lda,
-                                         const void* B, long long ldb, float* C, long long ldc, float beta, int grid,
-                                         void* ws, long long ws_bytes, void* stream) {
-  DL4SS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && A && B && C);
-  if (M == 0 || N == 0) return 0;
-  DL4SS_REQUIRE(K > 0 && lda % 8 == 0 && ldb % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0);
-  DL4SS_REQUIRE(N % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)C & 15) == 0 && ldc >= N);
-  const bool a_kc = !transA, b_kc = transB;
-  const int k8 = (K + 7) & ~7;
-  DL4SS_REQUIRE(!a_kc || lda >= k8);
-  DL4SS_REQUIRE(!b_kc || ldb >= k8);
-  DL4SS_REQUIRE(a_kc || lda >= ((M + 7) & ~7));
-  DL4SS_REQUIRE(b_kc || ldb >= ((N + 7) & ~7));
-  if (grid <= 0) grid = 2 * std::max(1, gl_cu_count());
-  const int gm = (M + C128::BM - 1) / C128::BM, gn = (N + BN - 1) / BN, nk = (K + BK - 1) / BK;
-  const long long iters = (long long)gm * gn * nk;
-  // at most one workgroup per iteration: every range is then non-empty, so a split tile's owners are
-  // consecutive workgroups and segment s = g - (first owner) indexes its slab
-  grid = (int)std::min<long long>(grid, iters);
-  DL4SS_REQUIRE(ws && ws_bytes >= (long long)sk_max_segments(iters, grid, nk) * M * N * 4);
-  hipStream_t st = as_stream(stream);
-  const auto* a = reinterpret_cast<const unsigned short*>(A);
-  const auto* b = reinterpret_cast<const unsigned short*>(B);
-  float* w = reinterpret_cast<float*>(ws);
-#define GSK(AK, BKC) \
-  hipLaunchKernelGGL((gemm_gl_sk_kernel<AK, BKC, C128>), dim3(grid), dim3(C128::NT), 0, st, M, N, K, a, lda, b, ldb, C, \
-                     ldc, beta, gm, gn, nk, iters, w)
-  if (a_kc && b_kc) GSK(true, true);
-  else if (a_kc) GSK(true, false);
-  else if (b_kc) GSK(false, true);
-  else GSK(false, false);
-#undef GSK
-  DL4SS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gemm_gl_sk_fixup_kernel<C128::BM>, dim3((unsigned)cdiv((long long)M * N / 4, 256)), dim3(256), 0,
-                     st, M, N, gm, gn, nk, iters, grid, w, C, ldc, beta);
-  DL4SS_CHECK_LAUNCH();
-  return 0;
 }
 
 // Workspace bytes of dl4ss_gemm_bf16_gl_grouped: the split-K slabs of every problem, each at a

@@ -240,10 +240,6 @@ class SepTrainer:
         self.fast = precision in ("bf16", "bf16s", "bf16s2") and self.rnn_precision == "bf16"
         self.dh_split = int(os.environ.get("DL4SS_DH_SPLIT", "3"))  # dH split-K (tuning knob, A/B runs)
         self.dx_split = int(os.environ.get("DL4SS_DX_SPLIT", "1"))  # dX split-K (tuning knob, A/B runs)
-        # stream-K dX / dH (dl4ss_gemm_bf16_gl_streamk; A/B knobs, round 5)
-        self.dx_sk = os.environ.get("DL4SS_DX_SK", "0") == "1"
-        self.dh_sk = os.environ.get("DL4SS_DH_SK", "0") == "1"
-        self.sk_grid = int(os.environ.get("DL4SS_SK_GRID", "0"))  # stream-K workgroups (0: two per CU)
         # BPTT bias partials reduced once after the last BPTT instead of after each (A/B knob)
         self.defer_bias = os.environ.get("DL4SS_DEFER_BIAS", "1") != "0"
         # Forward input projections x W_ih^T + b_ih formed inside the packed recurrence kernel
@@ -343,10 +339,7 @@ class SepTrainer:
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, 2 * NGH, max(1, self.dx_split), 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", FE_, 2 * H, BT, 2, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", 2 * NGH, 2 * H, BT, 4, 1),
-                          _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", NGH, H, BT, 8, 2),
-                          _lib.query("dl4ss_gemm_bf16_gl_streamk_ws_bytes", BT, 2 * H, FE_, self.sk_grid) if self.dh_sk else 0,
-                          _lib.query("dl4ss_gemm_bf16_gl_streamk_ws_bytes", BT, 2 * H, 2 * NGH, self.sk_grid)
-                          if self.dx_sk else 0)
+                          _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", NGH, H, BT, 8, 2))
             self.gl_ws = torch.empty(max(gl_need, 1), device=dev, dtype=torch.uint8)
             # partial sums of the deterministic Linear-bias colsum (dl4ss_colsum_bf16_det)
             pb = _lib.query("dl4ss_colsum_bf16_part_bytes", BT, F * net.E)
@@ -663,7 +656,9 @@ class SepTrainer:
                 probs.append(dict(A=src[:, d * ldgh:d * ldgh + NGH], B=self.hprevb[l][:, d * hp8:d * hp8 + H],
                                   out=whh[d * NGH:(d + 1) * NGH], transA=True, transB=False, beta=self._gbeta,
                                   splitk=s_hh))
-        self._dw_group = ops.GroupedGemm(probs, net.device)
+        # DL4SS_DW_CFG (A/B knob): the grouped launch's tile configuration (1: 128 x 128, two workgroups
+        # per CU; 2: 256 x 128 three-stage, one per CU)
+        self._dw_group = ops.GroupedGemm(probs, net.device, cfg=int(os.environ.get("DL4SS_DW_CFG", "1")))
         return self._dw_group
 
     def _backward_fast_early(self):
@@ -680,11 +675,7 @@ class SepTrainer:
         # gemm_gl split-K factors, measured per shape at C2 (tools/gemm_gl_bench.py --sweep): dH
         # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
         # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
-        if self.dh_sk:
-            ops.gemm_bf16_gl_streamk(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], ws=self.gl_ws,
-                                     grid=self.sk_grid)
-        else:
-            ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], splitk=self.dh_split, ws=self.gl_ws)
+        ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], splitk=self.dh_split, ws=self.gl_ws)
         if (not grouped or self.buckets) and not self.side:  # (bitwise the grouped launch's dW_lin at the same split)
             ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
                              beta=self._gbeta, splitk=2, ws=self.gl_ws)
@@ -779,11 +770,7 @@ class SepTrainer:
                 self._side_launch()
             if l > 0:  # the input gradient: all the next BPTT waits on
                 dH_next = self.dH[1] if dH is self.dH[0] else self.dH[0]
-                if self.dx_sk:
-                    ops.gemm_bf16_gl_streamk(dGb, self.wb_ih[l][:, :2 * H], out=dH_next, ws=self.gl_ws,
-                                             grid=self.sk_grid)
-                else:
-                    ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk=self.dx_split, ws=self.gl_ws)
+                ops.gemm_bf16_gl(dGb, self.wb_ih[l][:, :2 * H], out=dH_next, splitk=self.dx_split, ws=self.gl_ws)
             if not grouped:
                 xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
                 ops.gemm_bf16_gl(dGb, xb, transA=True, out=net.cat_view("weight_ih", l, g), beta=1.0, splitk=4,

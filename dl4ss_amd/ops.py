@@ -220,28 +220,6 @@ def gemm_bf16_gl(A, B, transA=False, transB=False, bias=None, epilogue=EPI_NONE,
     return out
 
 
-def gemm_bf16_gl_streamk(A, B, out, transA=False, transB=False, beta=0.0, grid=0, ws=None):
-    """out (fp32) = op(A) @ op(B) + beta*out through the stream-K form (dl4ss_gemm_bf16_gl_streamk):
-    a fixed grid (0: two workgroups per CU) dealt equal ranges of tiles x k-tiles, split tiles'
-    partials added in order by one fixup launch (deterministic).  ws: a uint8 workspace of at least
-    dl4ss_gemm_bf16_gl_streamk_ws_bytes, else a per-device one."""
-    _mat_bf16(A, "gemm_bf16_gl_streamk(A)")
-    _mat_bf16(B, "gemm_bf16_gl_streamk(B)")
-    _mat(out, "gemm_bf16_gl_streamk(out)")
-    M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
-    Kb, N = (B.shape[1], B.shape[0]) if transB else (B.shape[0], B.shape[1])
-    if K != Kb or tuple(out.shape) != (M, N):
-        raise RuntimeError(f"gemm_bf16_gl_streamk: shapes {tuple(A.shape)} {tuple(B.shape)} -> {tuple(out.shape)}")
-    nb = _lib.query("dl4ss_gemm_bf16_gl_streamk_ws_bytes", M, N, K, int(grid))
-    if ws is not None and ws.numel() < nb:
-        raise RuntimeError(f"gemm_bf16_gl_streamk: workspace of {ws.numel()} bytes < {nb}")
-    ws = ws if ws is not None else _gl_workspace(A.device, nb)
-    _lib.call("dl4ss_gemm_bf16_gl_streamk", int(transA), int(transB), M, N, K, _lib.ptr(A, True), A.stride(0),
-              _lib.ptr(B, True), B.stride(0), _lib.ptr(out, True), out.stride(0), float(beta), int(grid),
-              _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
-    return out
-
-
 class GroupedGemm:
     """A fixed list of bf16 GEMM problems C_i = op(A_i) @ op(B_i) + beta_i C_i run as ONE grouped
     launch (dl4ss_gemm_bf16_gl_grouped; + one split-K combine launch).  Each problem is a dict

@@ -107,15 +107,6 @@ int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, const void* 
                        long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta,
                        int splitk, int batch, long long strideA, long long strideB, long long strideC, void* ws,
                        long long ws_bytes, void* stream);
-/* Stream-K form (EPI_NONE, no bias, batch 1): C = op(A) op(B) + beta C on a fixed grid of `grid`
- * workgroups (<= 0: two per CU), each dealt an equal contiguous range of the tiles x 64-deep k-tiles
- * iterations (tile-major); a tile split across workgroups leaves fp32 partials in ws
- * (dl4ss_gemm_bf16_gl_streamk_ws_bytes) that one fixup launch adds in order (deterministic).
- * N % 4 == 0, ldc % 4 == 0, C 16-B aligned; the operand rules of dl4ss_gemm_bf16_gl. */
-long long dl4ss_gemm_bf16_gl_streamk_ws_bytes(int M, int N, int K, int grid);
-int dl4ss_gemm_bf16_gl_streamk(int transA, int transB, int M, int N, int K, const void* A, long long lda,
-                               const void* B, long long ldb, float* C, long long ldc, float beta, int grid, void* ws,
-                               long long ws_bytes, void* stream);
 /* Grouped form: n <= 16 independent problems C_i = op(A_i) op(B_i) + beta_i C_i (same transA /
  * transB for all, no bias, EPI_NONE, per-problem split-K factor) as ONE GEMM launch plus one
  * split-K combine launch; each C_i bitwise equal to dl4ss_gemm_bf16_gl with the same split factor.
