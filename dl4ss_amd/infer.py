@@ -28,6 +28,40 @@ from . import _lib, ops
 from .engine import CELLS, _ngate
 
 
+# split-precision operand images (dl4ss_f32_to_bf16_hilo): [x_hi | x_lo | x_hi] . [w_hi | w_hi | w_lo]
+A_SPLIT, W_SPLIT = 0b010, 0b100
+
+
+def _p8(n):
+    return (n + 7) // 8 * 8
+
+
+def _hilo(x, y, segw, pattern):
+    """y = the three-segment split image of the fp32 rows x (segments of segw, hi / lo by pattern)."""
+    _lib.call("dl4ss_f32_to_bf16_hilo", _lib.ptr(x, True), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(y),
+              y.stride(0), segw, 3, pattern, _lib.stream_ptr())
+
+
+class _SplitWeights:
+    """The [w_hi | w_hi | w_lo] images of a net's weights for the "bf16s" GEMMs, converted once per
+    parameter generation: reused while (net.generation, net.flat._version) is what it was when they
+    were made (engine.SepNet's contract for writes that bypass torch's version counter)."""
+
+    def __init__(self, net):
+        self.net, self.key, self.img = net, None, {}
+
+    def get(self, name, w):
+        key = (getattr(self.net, "generation", 0), self.net.flat._version)
+        if key != self.key:
+            self.img, self.key = {}, key
+        if name not in self.img:
+            seg = _p8(w.shape[1])
+            y = torch.empty(w.shape[0], 3 * seg, device=w.device, dtype=torch.bfloat16)
+            _hilo(w, y, seg, W_SPLIT)
+            self.img[name] = y
+        return self.img[name]
+
+
 class _BiRNNStack:
     """Forward-only stacked bidirectional LSTM / GRU (input GEMM + persistent recurrence per
     layer) with its buffers for one (B, T)."""
@@ -49,19 +83,28 @@ class _BiRNNStack:
         self.ws = torch.empty((wsn + 7) // 8, dtype=torch.int64, device=device)
         self.status = torch.zeros(1, dtype=torch.int32, device=device)
 
-    def run(self, x2d, cat_view, precision, rnn_precision=None):
+    def run(self, x2d, cat_view, precision, rnn_precision=None, split_w=None):
         """x2d (B*T, D0) fp32 -> (B, T, 2H); cat_view(kind, l) gives the [fwd; reverse]
         parameter of layer l (``weight_ih`` / ``weight_hh`` / ``bias_ih`` / ``bias_hh``).
-        ``precision``: the input-projection GEMMs; ``rnn_precision`` (default: the same) the
-        recurrent matvec."""
+        ``precision``: the input-projection GEMMs -- "fp32", "bf16", or "bf16s": one bf16 LDS-DMA
+        GEMM over split operands (K' = 3 K, fp32-accurate to ~2^-16; the training step's bf16s
+        forward GEMMs), with ``split_w`` (a _SplitWeights) holding the weight images;
+        ``rnn_precision`` (default: the same; "bf16" for bf16s) the recurrent matvec."""
         B, T, H = self.B, self.T, self.H
-        rnn_precision = rnn_precision or precision
+        rnn_precision = rnn_precision or ("bf16" if precision == "bf16s" else precision)
         st = _lib.stream_ptr()
         x = x2d
         out = None
         for l in range(self.L):
-            ops.gemm(x, cat_view("weight_ih", l), transB=True, bias=cat_view("bias_ih", l), out=self.G,
-                     precision=precision)
+            if precision == "bf16s":
+                seg = _p8(x.shape[1])
+                xs = self._xs(B * T, 3 * seg, x.device)
+                _hilo(x, xs, seg, A_SPLIT)
+                ops.gemm_bf16_gl(xs, split_w.get(f"weight_ih_l{l}", cat_view("weight_ih", l)), transB=True,
+                                 bias=cat_view("bias_ih", l), out=self.G)
+            else:
+                ops.gemm(x, cat_view("weight_ih", l), transB=True, bias=cat_view("bias_ih", l), out=self.G,
+                         precision=precision)
             out = self.out[l % 2]
             _lib.call("dl4ss_birnn_fwd", CELLS[self.cell], ops.PREC[rnn_precision], B, T, H, _lib.ptr(self.G),
                       _lib.ptr(cat_view("weight_hh", l)), _lib.ptr(cat_view("bias_hh", l)), _lib.ptr(out),
@@ -69,6 +112,13 @@ class _BiRNNStack:
                       _lib.ptr(self.ws), self.wsn, _lib.ptr(self.status), st)
             x = out.view(B * T, 2 * H)
         return out
+
+    def _xs(self, rows, cols, device):
+        """the split image of a layer input, (rows, cols) bf16 (one buffer, grown to the widest layer)"""
+        buf = getattr(self, "_xs_buf", None)
+        if buf is None or buf.numel() < rows * cols:
+            buf = self._xs_buf = torch.empty(rows * cols, device=device, dtype=torch.bfloat16)
+        return buf[:rows * cols].view(rows, cols)
 
     def check(self):
         s = int(self.status.item())
@@ -162,18 +212,29 @@ class ClassifierForward:
 
 class MaskNetForward:
     """MIX_SPEECH forward on a SepNet: V (B*T, F*E) = tanh(Linear(BiRNN(X))).  ``precision``: the
-    GEMMs (input projections, Linear); ``rnn_precision`` (default: the same): the recurrence."""
+    GEMMs (input projections, Linear; "fp32", "bf16" or the split-operand "bf16s");
+    ``rnn_precision`` (default: the same, "bf16" for bf16s): the recurrence."""
 
     def __init__(self, net, B, T, precision="fp32", rnn_precision=None):
         self.net, self.B, self.T, self.precision = net, B, T, precision
-        self.rnn_precision = rnn_precision or precision
+        self.rnn_precision = rnn_precision or ("bf16" if precision == "bf16s" else precision)
         self.stack = _BiRNNStack(net.cell, net.H, net.L, B, T, net.device)
+        self.split_w = _SplitWeights(net) if precision == "bf16s" else None
         self.h = None
 
     def __call__(self, feats, out):
         B, T, net = self.B, self.T, self.net
-        self.h = self.stack.run(feats.reshape(B * T, -1), net.cat_view, self.precision, self.rnn_precision)
-        ops.gemm(self.h.view(B * T, 2 * net.H), net.view("mix.Linear.weight"), transB=True,
+        self.h = self.stack.run(feats.reshape(B * T, -1), net.cat_view, self.precision, self.rnn_precision,
+                                split_w=self.split_w)
+        h2 = self.h.view(B * T, 2 * net.H)
+        if self.precision == "bf16s":
+            seg = _p8(2 * net.H)
+            hs = self.stack._xs(B * T, 3 * seg, h2.device)
+            _hilo(h2, hs, seg, A_SPLIT)
+            ops.gemm_bf16_gl(hs, self.split_w.get("mix.Linear.weight", net.view("mix.Linear.weight")), transB=True,
+                             bias=net.view("mix.Linear.bias"), epilogue=ops.EPI_TANH, out=out)
+            return out
+        ops.gemm(h2, net.view("mix.Linear.weight"), transB=True,
                  bias=net.view("mix.Linear.bias"), epilogue=ops.EPI_TANH, out=out, precision=self.precision)
         return out
 
@@ -197,15 +258,18 @@ class RecursiveExtractor:
     no ADJUST; its ``emb.layer.weight`` is the speaker embedding); ``cnet``: ClassifierNet.
 
     ``precision``: "fp32" (exact GEMMs and recurrences), "bf16" (bf16 operands everywhere, fp32
-    accumulate and state) or "mixed" -- the mask net's GEMMs (input projections, Linear -> V) in
-    fp32 with its recurrence on bf16 operands, the classifier in bf16.  The masks are sigmoids of
-    V . emb with N(0,1) speaker embeddings and no ADDJUST: every bf16 GEMM operand of the mask net
-    costs ~1e-3 of masked-magnitude error (tools/bf16_budget.py on the same BiGRU-2L net), the
-    recurrence ~0.3e-3, so "mixed" is the mode within the north-star 1e-3 (C5 in DESIGN.md
-    section 6).  The classifier only decides the speaker ids (its bf16 probabilities are within
-    ~1e-4 of fp32)."""
+    accumulate and state), "bf16s" -- the mask net's GEMMs (input projections, Linear -> V) as ONE
+    bf16 GEMM each over split operands (hi + lo bf16, K' = 3 K: fp32-accurate to ~2^-16, at bf16
+    MFMA speed) with its recurrence on bf16 operands, the classifier in bf16 -- or "mixed", the same
+    with the mask net's GEMMs on the exact fp32 MFMA (half the speed of bf16s, round 5).  The masks are
+    sigmoids of V . emb with N(0,1) speaker embeddings and no ADDJUST: every bf16-rounded GEMM operand
+    of the mask net costs ~1e-3 of masked-magnitude error (tools/bf16_budget.py on the same BiGRU-2L
+    net), the recurrence ~0.3e-3, so "bf16s" (and "mixed") are the modes within the north-star 1e-3
+    (C5 in DESIGN.md section 6; quoted in bf16s from round 6).  The classifier only decides the speaker
+    ids (its bf16 probabilities are within ~1e-4 of fp32)."""
 
-    MODES = {"fp32": ("fp32", "fp32", "fp32"), "bf16": ("bf16", "bf16", "bf16"), "mixed": ("fp32", "bf16", "bf16")}
+    MODES = {"fp32": ("fp32", "fp32", "fp32"), "bf16": ("bf16", "bf16", "bf16"), "mixed": ("fp32", "bf16", "bf16"),
+             "bf16s": ("bf16s", "bf16", "bf16")}
 
     def __init__(self, net, cnet, B, T, precision="fp32", alpha=-0.3, top_k=3, max_steps=2):
         if net.E != 50 or net.crm:

@@ -217,14 +217,15 @@ def _masked_rel(out, ref, X, rows):
     return r_fin, r_step
 
 
-# masked-magnitude rel-L2 bar per mode: "mixed" (fp32 mask-net GEMMs, bf16 recurrences, bf16
-# classifier) is the mode C5 is quoted in and must meet the north-star 1e-3; the all-bf16 operand
+# masked-magnitude rel-L2 bar per mode: "bf16s" (split-operand bf16 mask-net GEMMs, bf16 recurrences,
+# bf16 classifier; the mode C5 is quoted in from round 6) and "mixed" (the same with fp32 GEMMs) must
+# meet the north-star 1e-3; the all-bf16 operand
 # mode misses it on this BiGRU net (random-init N(0,1) query embeddings, no ADDJUST) and is held to
 # its own 1e-2 bound and never quoted as in-bar
-C5_BAR = {"mixed": 1e-3, "bf16": 1e-2}
+C5_BAR = {"mixed": 1e-3, "bf16s": 1e-3, "bf16": 1e-2}
 
 
-@pytest.mark.parametrize("precision", ["mixed", "bf16"])
+@pytest.mark.parametrize("precision", ["bf16s", "mixed", "bf16"])
 @pytest.mark.parametrize("B,seed", [(1, 11), (32, 7)])
 def test_c5_full_length_recursive_bf16(dev, B, seed, precision):
     """C5 at T = 251 against oracle/recursive.py in its bf16 modes, with unconditional asserts: at

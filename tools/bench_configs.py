@@ -122,7 +122,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16", "bf16s", "bf16s2", "mixed"],
-                    help="c1/c3/c4: fp32, bf16, bf16s; c5: fp32, bf16, mixed (infer.RecursiveExtractor)")
+                    help="c1/c3/c4: fp32, bf16, bf16s, bf16s2; c5: fp32, bf16, bf16s, mixed (infer.RecursiveExtractor)")
     ap.add_argument("--c5-precision", default=None, help="precision of the c5 configs (default: --precision)")
     ap.add_argument("--rnn-precision", default=None, choices=["fp32", "bf16"],
                     help="recurrent matvec precision (default: --precision)")
