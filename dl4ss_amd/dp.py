@@ -32,11 +32,14 @@ def allreduce_sum_async(t, pg=None):
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg, async_op=True)
 
 
-def allreduce_buckets_(ext, split, pg=None):
-    """The bucketed form of one SUM all-reduce of ``ext``: [split, end) first, then [0, split), both
-    asynchronous, then waited for -- elementwise the same sums as the flat all-reduce
-    (tests/test_dp_cpu.py)."""
-    works = [allreduce_sum_async(ext[split:], pg), allreduce_sum_async(ext[:split], pg)]
+def allreduce_buckets_(ext, splits, pg=None):
+    """The bucketed form of one SUM all-reduce of ``ext``: ``splits`` (an index, or ascending indices)
+    cut it into contiguous buckets, all-reduced asynchronously from the LAST bucket to the first (the
+    order the bucketed step completes them: Linear / embedding / ADDJUST, the upper layers, then the
+    lower layers with the status flag), then waited for -- elementwise the same sums as the flat
+    all-reduce (tests/test_dp_cpu.py)."""
+    cuts = [0] + ([int(splits)] if isinstance(splits, int) else [int(x) for x in splits]) + [ext.numel()]
+    works = [allreduce_sum_async(ext[a:b], pg) for a, b in reversed(list(zip(cuts[:-1], cuts[1:])))]
     for w in works:
         if w is not None:
             w.wait()

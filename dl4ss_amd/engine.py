@@ -101,6 +101,11 @@ class SepNet:
         embedding and ADDJUST (complete before the first BPTT)."""
         return 4 + self.offsets["mix.Linear.weight"][0]
 
+    def bucket_mid(self, layer):
+        """Index into grad_ext where the recurrent layers >= ``layer`` start (layers are contiguous in
+        order): the three-bucket step's middle bucket is [bucket_mid(layer), bucket_split())."""
+        return 4 + self.offsets[f"mix.layer.weight_ih_l{layer}"][0]
+
     def named_parameters(self):
         return {name: self.view(name) for name, _ in self.specs}
 
@@ -265,8 +270,19 @@ class SepTrainer:
         # GEMM and the early all-reduce eagerly between two graph replays: the side GEMM then shared a
         # hardware queue with the replayed BPTT chain and ran before it, 4.91 vs 3.51 ms per step.)
         # DL4SS_DP_BUCKETS=0: one flat all-reduce after the step's backward.
-        self.buckets = (process_group is not None and self.fast and net.L <= 5
-                        and os.environ.get("DL4SS_DP_BUCKETS", "1") != "0")
+        # Three buckets (round 6, DL4SS_DP_BUCKETS=3; L >= 2): the grouped weight-gradient launch is split in
+        # two -- the upper layers (>= dp_layer = L // 2) first, whose all-reduce then runs beside the lower
+        # layers' launch -- and only the lower layers + the status flag follow it.  Measured at world size 1
+        # over RCCL (tools/dist_ab.sh, profiles/r06_dist_buckets_ab.txt): 3.61 ms per step against 3.50 for
+        # two buckets and 3.48 flat -- the two half launches each pay their own ramp, tail and split-K
+        # combine (+~90 us) and the third replay ~20 us, more than the ~0.03 ms of all-reduce the middle
+        # bucket could hide at 8 ranks.  So the default stays "2" (round 5: one grouped
+        # launch, flag + layers behind it); "0": one flat all-reduce.
+        nb = os.environ.get("DL4SS_DP_BUCKETS", "2")
+        if nb not in ("0", "1", "2", "3"):
+            raise ValueError(f"DL4SS_DP_BUCKETS={nb}: expected 0, 2 or 3")
+        self.buckets = process_group is not None and self.fast and net.L <= 5 and nb != "0"
+        self.dp_layer = net.L // 2 if (self.buckets and nb == "3" and net.L >= 2) else None
         self._works = []
         self._in_chain = False
         # The Linear's weight and bias gradients on a SIDE STREAM beside the BPTT chain (round 5): the
@@ -612,7 +628,9 @@ class SepTrainer:
         x 8 splits, each with its own ramp and tail).  Each gradient is bitwise what a single
         launch with the same split factor produces (tests/test_gemm_grouped_gpu.py).  The weight gradients
         accumulate (beta 1) onto the zeroed flat gradient: the reference's loss.backward()
-        (TDAA_beta/main_run_sstune_EvalVer.py:673)."""
+        (TDAA_beta/main_run_sstune_EvalVer.py:673).  Returns the list of launches: one, or with three
+        data-parallel buckets two -- the layers >= dp_layer, then the rest -- each gradient bitwise the
+        one-launch form's (same split factors)."""
         if self._dw_group is not None:
             return self._dw_group
         net, H = self.net, self.net.H
@@ -640,25 +658,36 @@ class SepTrainer:
         if os.environ.get("DL4SS_DW_SPLITS"):  # A/B knob: "lin,ih,hh"
             s_lin, s_ih, s_hh = (int(v) for v in os.environ["DL4SS_DW_SPLITS"].split(","))
         self.dw_splits = (s_lin, s_ih, s_hh)
-        probs = [] if (self.buckets or self.side) else [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H],
-                                              out=net.view("mix.Linear.weight", g), transA=True, transB=False,
-                                              beta=self._gbeta, splitk=s_lin)]
-        # longest k-ranges first (dW_lin 63 k-tiles per workgroup, dW_ih 32, dW_hh 16): the short
-        # ones fill the tail
-        for l in range(net.L - 1, -1, -1):
-            xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
-            probs.append(dict(A=self.dGb_l[l], B=xb, out=net.cat_view("weight_ih", l, g), transA=True, transB=False,
-                              beta=self._gbeta, splitk=s_ih))
-        for l in range(net.L - 1, -1, -1):
-            src = self.dGhb_l[l] if gru else self.dGb_l[l]
-            whh = net.cat_view("weight_hh", l, g)
-            for d in range(2):
-                probs.append(dict(A=src[:, d * ldgh:d * ldgh + NGH], B=self.hprevb[l][:, d * hp8:d * hp8 + H],
-                                  out=whh[d * NGH:(d + 1) * NGH], transA=True, transB=False, beta=self._gbeta,
-                                  splitk=s_hh))
+
+        def layer_probs(layers):
+            # longest k-ranges first (dW_lin 63 k-tiles per workgroup, dW_ih 32, dW_hh 16): the short
+            # ones fill the tail
+            probs = []
+            for l in layers:
+                xb = self.xb0[:, :self.F] if l == 0 else self.outb[l - 1][:, :2 * H]
+                probs.append(dict(A=self.dGb_l[l], B=xb, out=net.cat_view("weight_ih", l, g), transA=True,
+                                  transB=False, beta=self._gbeta, splitk=s_ih))
+            for l in layers:
+                src = self.dGhb_l[l] if gru else self.dGb_l[l]
+                whh = net.cat_view("weight_hh", l, g)
+                for d in range(2):
+                    probs.append(dict(A=src[:, d * ldgh:d * ldgh + NGH], B=self.hprevb[l][:, d * hp8:d * hp8 + H],
+                                      out=whh[d * NGH:(d + 1) * NGH], transA=True, transB=False, beta=self._gbeta,
+                                      splitk=s_hh))
+            return probs
+
+        lin = [] if (self.buckets or self.side) else [dict(A=self.dPreb[:, :FE], B=self.outb[-1][:, :2 * H],
+                                             out=net.view("mix.Linear.weight", g), transA=True, transB=False,
+                                             beta=self._gbeta, splitk=s_lin)]
         # DL4SS_DW_CFG (A/B knob): the grouped launch's tile configuration (1: 128 x 128, two workgroups
         # per CU; 2: 256 x 128 three-stage, one per CU)
-        self._dw_group = ops.GroupedGemm(probs, net.device, cfg=int(os.environ.get("DL4SS_DW_CFG", "1")))
+        cfg = int(os.environ.get("DL4SS_DW_CFG", "1"))
+        if self.dp_layer is not None:
+            Ls = self.dp_layer
+            self._dw_group = [ops.GroupedGemm(lin + layer_probs(range(net.L - 1, Ls - 1, -1)), net.device, cfg=cfg),
+                              ops.GroupedGemm(layer_probs(range(Ls - 1, -1, -1)), net.device, cfg=cfg)]
+        else:
+            self._dw_group = [ops.GroupedGemm(lin + layer_probs(range(net.L - 1, -1, -1)), net.device, cfg=cfg)]
         return self._dw_group
 
     def _backward_fast_early(self):
@@ -729,8 +758,8 @@ class SepTrainer:
         """The bf16 backward from the first BPTT on: the BPTT / dX chain down the layers (part
         "chain", the side stream joined at its end), then the bias reduce and the grouped
         weight-gradient launch (part "wgrad")."""
-        if part == "wgrad":
-            return self._backward_wgrad()
+        if part in ("wgrad", "upper", "lower"):
+            return self._backward_wgrad("all" if part == "wgrad" else part)
         self._in_chain = True
         try:
             self._backward_chain()
@@ -786,12 +815,16 @@ class SepTrainer:
         if self.side:
             self._side_join()
 
-    def _backward_wgrad(self):
-        """The recurrent layers' bias reduce and grouped weight-gradient launch (after the chain)."""
-        if self.defer_bias:
+    def _backward_wgrad(self, which="all"):
+        """The recurrent layers' bias reduce and grouped weight-gradient launch(es) (after the chain).
+        Three data-parallel buckets: "upper" (the bias reduce + the layers >= dp_layer) and "lower"."""
+        if which != "lower" and self.defer_bias:
             self._bias_reduce()
         if self.net.L <= 5:
-            self._weight_grad_group().run()
+            groups = self._weight_grad_group()
+            run = groups if which == "all" else groups[:1] if which == "upper" else groups[1:]
+            for grp in run:
+                grp.run()
 
     def _bias_reduce(self):
         """Every layer's BPTT bias partials (DL4SS_RNN_DEFER_BIAS) into db_ih / db_hh, one launch."""
@@ -930,12 +963,24 @@ class SepTrainer:
         running beside the recurrent layers' weight-gradient launch."""
         self.allreduce_early()
 
-    def allreduce_late(self):
-        """Start the SUM all-reduce of the late bucket (the status flag and every recurrent layer)."""
+    def allreduce_mid(self):
+        """Three buckets: start the SUM all-reduce of the upper recurrent layers (>= dp_layer), complete
+        after the first weight-gradient launch, beside the second."""
         from . import dp
 
         self._no_collective_in_chain()
-        self._works.append(dp.allreduce_sum_async(self.net.grad_ext[:self.net.bucket_split()], self.pg))
+        net = self.net
+        self._works.append(dp.allreduce_sum_async(net.grad_ext[net.bucket_mid(self.dp_layer):net.bucket_split()],
+                                                  self.pg))
+
+    def allreduce_late(self):
+        """Start the SUM all-reduce of the late bucket: the status flag and every recurrent layer (two
+        buckets), or the layers below dp_layer (three)."""
+        from . import dp
+
+        self._no_collective_in_chain()
+        end = self.net.bucket_mid(self.dp_layer) if self.dp_layer is not None else self.net.bucket_split()
+        self._works.append(dp.allreduce_sum_async(self.net.grad_ext[:end], self.pg))
 
     def wait_allreduce(self):
         """The current stream waits for every all-reduce started this step: net.grad then holds the
@@ -984,7 +1029,12 @@ class SepTrainer:
             self.backward_early()
             self._backward_fast("chain")
             self._early_bucket()
-            self._backward_fast("wgrad")
+            if self.dp_layer is not None:
+                self._backward_fast("upper")
+                self.allreduce_mid()
+                self._backward_fast("lower")
+            else:
+                self._backward_fast("wgrad")
             self._status_flag()
             self.allreduce_late()
         else:
@@ -1016,13 +1066,16 @@ class SepTrainer:
         around the replay.  Bucketed data parallel: two graphs, split where the early bucket's
         all-reduce starts -- after the BPTT chain, which the side-stream dW_lin (forked and joined
         inside the first graph) runs beside; the second graph (the recurrent layers' weight-gradient
-        launch) then runs beside that all-reduce.  Call after at least one eager step(), so every
-        workspace exists before the capture."""
+        launch) then runs beside that all-reduce.  Three buckets: a third graph -- the second graph holds
+        the bias reduce and the upper layers' weight gradients, the third the lower layers' and the status
+        flag, with the middle bucket's all-reduce started between them.  Call after at least one eager
+        step(), so every workspace exists before the capture."""
         import gc
 
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         g2 = torch.cuda.CUDAGraph() if self.buckets else None
+        g3 = torch.cuda.CUDAGraph() if (self.buckets and self.dp_layer is not None) else None
         # no garbage collection while the stream is being captured: a collection that frees another
         # object's device memory mid-capture aborted the process (round 4, a dropped trainer's buffers)
         gc.collect()
@@ -1036,20 +1089,27 @@ class SepTrainer:
                 else:
                     self.backward_early()
                     self._backward_fast("chain")
-            if g2 is not None:
+            if g2 is not None and g3 is None:
                 with torch.cuda.graph(g2, pool=g.pool()):
                     self._backward_fast("wgrad")
+                    self._status_flag()
+            elif g3 is not None:
+                with torch.cuda.graph(g2, pool=g.pool()):
+                    self._backward_fast("upper")
+                with torch.cuda.graph(g3, pool=g.pool()):
+                    self._backward_fast("lower")
                     self._status_flag()
         finally:
             if was_enabled:
                 gc.enable()
         torch.cuda.synchronize()
-        self.graph, self.graph_late = g, g2
+        self.graph, self.graph_late, self.graph_lower = g, g2, g3
         return g
 
     def step_graph(self, raw, gains, spk_idx):
         """step() with the captured graph: mixing, graph replay, all-reduce, Adam (bucketed: the
-        early bucket's all-reduce between the two replays)."""
+        early bucket's all-reduce between the first two replays, the middle one's between the second
+        and the third)."""
         if getattr(self, "graph", None) is None:
             self.capture()
         self.spk.copy_(spk_idx)
@@ -1061,6 +1121,9 @@ class SepTrainer:
         if self.graph_late is not None:
             self._early_bucket()
             self.graph_late.replay()
+            if self.graph_lower is not None:
+                self.allreduce_mid()
+                self.graph_lower.replay()
             self.allreduce_late()
         else:
             self.allreduce()

@@ -168,7 +168,9 @@ def _bucket_worker(rank, world, port, out):
     flat = ext.clone()
     dist.all_reduce(flat, op=dist.ReduceOp.SUM)
     buck = dp.allreduce_buckets_(ext.clone(), net.bucket_split())
-    out[rank] = (flat, buck)
+    # three buckets (round 6): layers < L // 2 with the flag, layers >= L // 2, Linear / emb / ADDJUST
+    buck3 = dp.allreduce_buckets_(ext.clone(), [net.bucket_mid(net.L // 2), net.bucket_split()])
+    out[rank] = (flat, buck, buck3)
     dist.destroy_process_group()
 
 
@@ -185,9 +187,14 @@ def test_dp_bucketed_allreduce_equals_flat():
     early = {n for n, (off, _) in net.offsets.items() if off + 4 >= split}
     assert early == {"mix.Linear.weight", "mix.Linear.bias", "emb.layer.weight", "adj.layer.weight"}
     assert net.dp_flag.data_ptr() == net.grad_ext.data_ptr()  # the flag travels with the late bucket
+    mid = net.bucket_mid(net.L // 2)  # the three-bucket step's middle bucket: exactly layers 2 and 3 of C2
+    middle = {n for n, (off, _) in net.offsets.items() if mid <= off + 4 < split}
+    assert middle == {f"mix.layer.{kind}_l{l}{rev}" for kind in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")
+                      for l in (2, 3) for rev in ("", "_reverse")}
     for r in range(world):
-        flat, buck = out[r]
+        flat, buck, buck3 = out[r]
         assert torch.equal(flat, buck)  # bitwise: the same elementwise sums
+        assert torch.equal(flat, buck3)
         assert torch.equal(flat, out[0][0])  # every rank holds the same sums
         assert flat[0] == 1.0  # one rank's timeout reaches every rank through the late bucket
     # (Adam's 1 / world on the SUM, dl4ss_adam_guarded_dp_scaled, runs on the GPU:

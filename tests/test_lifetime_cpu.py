@@ -54,8 +54,10 @@ def test_recursive_extractor_modes():
     cnet = infer.ClassifierNet(129, 600, 3, 101, device="cpu")
     ex = infer.RecursiveExtractor(net, cnet, 1, 9, precision="mixed")
     assert (ex.mask_net.precision, ex.mask_net.rnn_precision, ex.classifier.precision) == ("fp32", "bf16", "bf16")
+    ex = infer.RecursiveExtractor(net, cnet, 1, 9, precision="bf16s")  # round 6: split-operand mask-net GEMMs
+    assert (ex.mask_net.precision, ex.mask_net.rnn_precision, ex.classifier.precision) == ("bf16s", "bf16", "bf16")
     with pytest.raises(ValueError):
-        infer.RecursiveExtractor(net, cnet, 1, 9, precision="bf16s")
+        infer.RecursiveExtractor(net, cnet, 1, 9, precision="bf16s2")
 
 
 def test_step_plan_flags(monkeypatch):

@@ -1,7 +1,7 @@
 """The data-parallel path on the GPU at world size 1 over RCCL: an ``nccl``
 process group with a private TCP rendezvous (as ``bench.py --dist``), and SepTrainer's graph
 step with ``process_group=pg`` -- status flag in front of the flat gradient -> RCCL SUM all-reduce of
-``grad_ext`` (two buckets, or flat) -> ``dl4ss_adam_guarded_dp_scaled`` (x 1 / world) -- beside the
+``grad_ext`` (three buckets, two, or flat) -> ``dl4ss_adam_guarded_dp_scaled`` (x 1 / world) -- beside the
 240-workgroup persistent recurrence and the side-stream dW_lin.
 
 * At world size 1 the all-reduce is an identity, so the pg step must be BITWISE the pg=None step:
@@ -61,11 +61,13 @@ def _trainer(dev, cfg, B, K, N, pg):
     return engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16", process_group=pg)
 
 
-@pytest.mark.parametrize("name,buckets", [("C2", "1"), ("C4", "1"), ("C2", "0")])
+@pytest.mark.parametrize("name,buckets", [("C2", "3"), ("C4", "3"), ("C2", "2"), ("C2", "0")])
 def test_rccl_world1_graph_step_bitwise_equal_to_single_gpu(dev, pg, name, buckets, monkeypatch):
-    """buckets "1" (default): the early bucket (Linear, embedding, ADDJUST) all-reduced behind the
-    side-stream dW_lin beside the BPTT chain, the late one after it, two graph replays; "0": one flat
-    all-reduce after one replay.  Both SUM, with the 1 / world inside Adam."""
+    """buckets "3" (round 6, not the default): the early bucket (Linear, embedding, ADDJUST) all-reduced after
+    the BPTT chain beside the upper layers' weight-gradient launch, the upper layers' bucket beside the
+    lower layers' launch, the lower layers + status flag last, three graph replays; "2" (the default, round 5): the
+    early bucket, then every layer + the flag after one weight-gradient launch, two replays; "0": one
+    flat all-reduce after one replay.  All SUM, with the 1 / world inside Adam."""
     monkeypatch.setenv("DL4SS_DP_BUCKETS", buckets)
     cfg = CFGS[name]
     B, K, N = 32, cfg["K"], 32000
@@ -73,7 +75,8 @@ def test_rccl_world1_graph_step_bitwise_equal_to_single_gpu(dev, pg, name, bucke
     runs = {}
     for tag, group in (("single", None), ("rccl", pg)):
         tr = _trainer(dev, cfg, B, K, N, group)
-        assert tr.buckets == (group is not None and buckets == "1")
+        assert tr.buckets == (group is not None and buckets != "0")
+        assert (tr.dp_layer is not None) == (group is not None and buckets == "3")
         tr.step(*pool[0])  # eager warm-up before the capture
         losses = [float(tr.step_graph(*b)[0].item()) for b in pool]
         tr.check()

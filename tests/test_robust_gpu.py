@@ -190,7 +190,7 @@ def test_captured_trainer_freed_by_refcount(dev):
         tr.step(*batch)
         tr.step_graph(*batch)
         tr.check()
-        refs = [weakref.ref(tr), weakref.ref(tr.graph), weakref.ref(tr._dw_group)]
+        refs = [weakref.ref(tr), weakref.ref(tr.graph)] + [weakref.ref(grp) for grp in tr._dw_group]
         del tr
         torch.cuda.synchronize()
         assert all(r() is None for r in refs), [r() is None for r in refs]
