@@ -76,6 +76,31 @@ def test_gemm_gl_epilogues_and_beta(dev):
     _check(out, ref2 + 0.5 * C0.double().cpu(), mag + 0.5 * C0.double().cpu().abs())
 
 
+@pytest.mark.parametrize("M,N,ld,off", [(8032, 6450, 6450, 0), (8032, 6450, 6450, 2), (700, 452, 458, 4),
+                                          (333, 200, 206, 6), (130, 64, 64, 0)],
+                         ids=["linear", "linear_off4B", "ld458_off8B", "ld206_off12B", "one_block"])
+def test_gemm_gl_bf16_v_epilogue_bitwise(dev, M, N, ld, off):
+    """The Linear's tanh -> bf16 V epilogue (rows staged in LDS shifted by their own 16-B misalignment,
+    written as aligned 16-B chunks + head / tail words): bitwise the RNE bf16 of the fp32 tanh epilogue
+    (same k-loop), for every row misalignment (V rows of 2 ld bytes, V starting off bytes past 16 B),
+    the partial last column block and rows past a 128 multiple; nothing outside V is written."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + off)
+    K = 600
+    Ab = ops.to_bf16(torch.randn(M, K, generator=g).to(dev))
+    Bb = ops.to_bf16(torch.randn(N, K, generator=g).to(dev))
+    bias = torch.randn(N, generator=g).to(dev)
+    ref = ops.gemm_bf16_gl(Ab, Bb, transB=True, bias=bias, epilogue=ops.EPI_TANH).to(torch.bfloat16)
+    buf = torch.full((M * ld + off + 64,), 7.0, device=dev, dtype=torch.bfloat16)
+    V = buf[off:off + M * ld].view(M, ld)[:, :N]
+    ops.gemm_bf16_gl(Ab, Bb, transB=True, bias=bias, epilogue=ops.EPI_TANH_BF16, out=V)
+    torch.cuda.synchronize()
+    assert torch.equal(V.view(torch.int16).cpu(), ref.view(torch.int16).cpu())
+    mask = torch.ones(buf.numel(), dtype=torch.bool)
+    idx = (off + torch.arange(M)[:, None] * ld + torch.arange(N)[None, :]).reshape(-1)
+    mask[idx] = False
+    assert bool((buf.cpu()[mask] == 7.0).all())
+
+
 @pytest.mark.parametrize("ta,tb", [(True, False), (False, False), (True, True)])
 def test_gemm_gl_splitk_deterministic(dev, ta, tb):
     """weight-gradient form (long K, small output): split-K slabs summed in fixed order"""
