@@ -40,18 +40,26 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-constexpr int BN = 128, BK = 64;
+constexpr int BN = 128, BK = 64;  // BK: the split-K quantum and the default k-tile depth
 constexpr int PAN = 128 * BK;  // bf16 elements of one 128-row operand panel image (16 KB)
 
-// Tile configurations: BM x 128 output tile, BM / 32 waves of 64 x 64, STG LDS stages.
+// Tile configurations: BM x 128 output tile, BM / 32 waves of 64 x 64, STG LDS stages of KT-deep
+// k-tiles (KT 64 or 32), WPC workgroups per CU.
 //   Cfg<128, 2>: 256 threads, 64 KB, two workgroups per CU, one k-tile of DMA in flight each
 //   Cfg<256, 3>: 512 threads, 144 KB, one workgroup per CU, two k-tiles in flight (a counted
 //                vmcnt across a raw s_barrier), 25 % fewer operand bytes per MFMA
-template <int BM_, int STG_>
+//   Cfg<128, 5, 32> (round 6, the deep ring): 32-deep k-tiles, five 16-KB stages = 80 KB, two
+//                workgroups per CU (the whole 160 KB), FOUR k-tiles (128 k) in flight during each
+//                k-tile's MFMAs -- twice the bytes in flight of Cfg<128, 2> -- behind the same
+//                counted-vmcnt raw barrier; the same MFMAs in the same k order (bitwise the same C)
+template <int BM_, int STG_, int KT_ = 64>
 struct Cfg {
-  static constexpr int BM = BM_, STG = STG_, NT = 2 * BM_, NW = NT / 64;
-  static constexpr int CPW_A = BM_ / 8 / NW, CPW_B = BN / 8 / NW;  // 1-KB DMAs per wave per k-tile
-  static constexpr int IMG_A = BM_ * BK, IMG_B = BN * BK, STAGE = IMG_A + IMG_B;
+  static constexpr int BM = BM_, STG = STG_, KT = KT_, NT = 2 * BM_, NW = NT / 64;
+  static constexpr int PPP = KT_ / 4;  // 1-KB DMA pieces per 128-row panel per k-tile
+  static constexpr int CPW_A = BM_ / 128 * PPP / NW, CPW_B = BN / 128 * PPP / NW;  // 1-KB DMAs per wave per k-tile
+  static constexpr int IMG_A = BM_ * KT_, IMG_B = BN * KT_, STAGE = IMG_A + IMG_B;
+  static constexpr int WPC = (NT == 256 && STG_ * STAGE * 2 <= 80 * 1024) ? 2 : 1;  // workgroups per CU
+  static_assert(CPW_A >= 1 && CPW_B >= 1, "at least one DMA per wave and operand");
 };
 enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2 };
 
@@ -61,12 +69,19 @@ __device__ __attribute__((aligned(64))) const unsigned g_zero_line[16] = {0};
 __device__ __forceinline__ float ftanh_fast(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
 
 __device__ __forceinline__ int km_xor(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+// KC image swizzle: 16-B chunk c of row r at c ^ kc_swz(r).  KT 64 (128-B rows, 8 chunks): the 16
+// rows of a ds_read_b128 lane group on 16 distinct bank slots by (r >> 1) & 7; KT 32 (64-B rows, 4
+// chunks, four rows per 256-B bank cycle): rows r, r + 4, r + 8, r + 12 apart by (r >> 2) & 3
+template <int KT>
+__device__ __forceinline__ int kc_swz(int r) { return KT == 64 ? (r >> 1) & 7 : (r >> 2) & 3; }
 
 // Per-lane source pointers of one operand's CPW DMA instructions (this wave's share of a
-// ROWS x 64 tile, ROWS / 128 panels of 16 1-KB instructions) at k-tile start kbeg; advanced
-// by `step` elements per k-tile.  Instruction j fills panel j >> 4, piece j & 15.
-template <bool KC, int CPW>
+// ROWS x KT tile, ROWS / 128 panels of PPP = KT / 4 1-KB instructions) at k-tile start kbeg; advanced
+// by `step` elements per k-tile.  Instruction j fills panel j / PPP, piece j % PPP.  KC pieces are
+// 512 / KT rows of KT k (lanes KT / 8 to a row); KM pieces are 4 k-rows of 128 rows.
+template <bool KC, int CPW, int KT = BK>
 struct Stager {
+  static constexpr int PPP = KT / 4, LPR = KT / 8;
   const unsigned short* src[CPW];
   int kpos[CPW];  // k of this lane's chunk (KC) or k-row (KM) relative to the k-tile start
   long long step;
@@ -74,10 +89,10 @@ struct Stager {
                                        int lane) {
 #pragma unroll
     for (int i = 0; i < CPW; ++i) {
-      const int j = wave * CPW + i, pan = j >> 4, jj = j & 15;
+      const int j = wave * CPW + i, pan = j / PPP, jj = j % PPP;
       if (KC) {
-        const int r = 8 * jj + (lane >> 3), cp = lane & 7;  // row within the panel
-        const int c = cp ^ ((r >> 1) & 7);
+        const int r = (512 / KT) * jj + lane / LPR, cp = lane % LPR;  // row within the panel
+        const int c = cp ^ kc_swz<KT>(r);
         const int gr = min(r0 + 128 * pan + r, rmax - 1);
         src[i] = G + (long long)gr * ld + kbeg + 8 * c;
         kpos[i] = 8 * c;
@@ -90,9 +105,9 @@ struct Stager {
         kpos[i] = k;
       }
     }
-    step = KC ? BK : (long long)BK * ld;
+    step = KC ? KT : (long long)KT * ld;
   }
-  // issue this wave's CPW 1-KB DMAs of k-tile t (k0 = kbeg + t * BK) into image dst
+  // issue this wave's CPW 1-KB DMAs of k-tile t (k0 = kbeg + t * KT) into image dst
   __device__ __forceinline__ void issue(unsigned short* dst, int wave, int t, int k0_rel, int kspan) {
 #pragma unroll
     for (int i = 0; i < CPW; ++i) {
@@ -103,14 +118,14 @@ struct Stager {
   }
 };
 
-// fragment (8 k-values of one row) of k-step kk (0, 1) for tile row `row`
-template <bool KC>
+// fragment (8 k-values of one row) of k-step kk (0 .. KT / 32 - 1) for tile row `row`
+template <bool KC, int KT = BK>
 __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int kk, int lane) {
-  img += (row >> 7) * PAN;  // 128-row panel
+  img += (row >> 7) * (128 * KT);  // 128-row panel
   row &= 127;
   if (KC) {
     const int c = 4 * kk + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(img + row * BK + 8 * (c ^ ((row >> 1) & 7)));
+    return *reinterpret_cast<const bf16x8*>(img + row * KT + 8 * (c ^ kc_swz<KT>(row)));
   } else {
     // group g = lane >> 4 reads k-rows 32 kk + 8 g + 4 h + q (q = 0..3) for rows c0 .. c0 + 15,
     // lane 4 q + p of the group addressing columns c0 + 4 p .. + 3 (c0 = row - (lane & 15))
@@ -127,6 +142,24 @@ __device__ __forceinline__ bf16x8 frag(const unsigned short* img, int row, int k
   }
 }
 
+// s_waitcnt vmcnt(N) with N a compile-time count; vm_wait_n: the count a * PW for a runtime a < AMAX
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int PW, int AMAX>
+__device__ __forceinline__ void vm_wait_n(int a) {
+  if constexpr (AMAX > 0) {
+    if (a == AMAX - 1) {
+      vm_wait<(AMAX - 1) * PW>();
+      return;
+    }
+    vm_wait_n<PW, AMAX - 1>(a);
+  } else {
+    vm_wait<0>();
+  }
+}
+
 // One BM x 128 output tile of C (or of split-K slab `slab`, SPLIT) over k in [kbeg, kbeg + kspan):
 // the k-loop and the epilogue of gemm_gl_kernel and gemm_gl_grouped_kernel.  smem: the kernel's
 // one LDS array (CF::STG * CF::STAGE bf16).
@@ -140,8 +173,8 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
                                         float* __restrict__ C, long long ldc, const float* __restrict__ bias,
                                         float beta, int m0, int n0, int kbeg, int kspan, float* __restrict__ slab,
                                         float* __restrict__ rsum = nullptr) {
-  constexpr int STG = CF::STG, IMG_A = CF::IMG_A, STAGE = CF::STAGE;
-  const int nk = (kspan + BK - 1) / BK;
+  constexpr int STG = CF::STG, IMG_A = CF::IMG_A, STAGE = CF::STAGE, KT = CF::KT;
+  const int nk = (kspan + KT - 1) / KT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const bool rs = RS && rsum != nullptr && n0 == 0 && wn == 0;  // wave-uniform
@@ -150,8 +183,8 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
   for (int i = 0; i < 4; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
 
-  Stager<A_KC, CF::CPW_A> sa_;
-  Stager<B_KC, CF::CPW_B> sb_;
+  Stager<A_KC, CF::CPW_A, KT> sa_;
+  Stager<B_KC, CF::CPW_B, KT> sb_;
   sa_.init(A, lda, m0, M, kbeg, wave, lane);
   sb_.init(B, ldb, n0, N, kbeg, wave, lane);
 
@@ -164,12 +197,12 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
   auto compute = [&](const unsigned short* ia) {
     const unsigned short* ib = ia + IMG_A;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KT / 32; ++kk) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<A_KC>(ia, wm + 16 * i + (lane & 15), kk, lane);
+      for (int i = 0; i < 4; ++i) af[i] = frag<A_KC, KT>(ia, wm + 16 * i + (lane & 15), kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag<B_KC>(ib, wn + 16 * j + (lane & 15), kk, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<B_KC, KT>(ib, wn + 16 * j + (lane & 15), kk, lane);
 #ifndef GGL_NO_MFMA  // diagnostic builds: GGL_NO_MFMA (fragments read, no MFMA), GGL_NO_DMA (first tile only)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -189,8 +222,8 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
   };
   auto dma = [&](int t) {  // this wave's DMAs of k-tile t into LDS stage t % STG
     unsigned short* na = smem + (t % STG) * STAGE;
-    sa_.issue(na, wave, t, t * BK, kspan);
-    sb_.issue(na + IMG_A, wave, t, t * BK, kspan);
+    sa_.issue(na, wave, t, t * KT, kspan);
+    sb_.issue(na + IMG_A, wave, t, t * KT, kspan);
   };
   if constexpr (STG == 2) {
     dma(0);
@@ -205,18 +238,20 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
       __syncthreads();  // ... and every wave's; every wave is done reading buffer kt & 1
     }
   } else {
-    dma(0);
-    if (nk > 1) dma(1);
+    // STG - 1 k-tiles issued ahead: at k-tile kt, tiles kt + 1 .. kt + STG - 2 may stay in flight
+    // across the wait (a counted vmcnt), then the raw barrier (every wave's tile kt landed, every
+    // wave is done reading tile kt - 1's stage), then tile kt + STG - 1 into that stage
+    constexpr int PW = CF::CPW_A + CF::CPW_B;  // this wave's DMAs per k-tile
+#pragma unroll
+    for (int t = 0; t < STG - 1; ++t)
+      if (t < nk) dma(t);
     for (int kt = 0; kt < nk; ++kt) {
-      // this wave's DMAs of tile kt landed (tile kt + 1's 8 may stay in flight), then the raw
-      // barrier: every wave's tile kt landed and every wave is done reading tile kt - 1's stage
-      if (kt + 1 < nk)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CF::CPW_A + CF::CPW_B) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ahead = min(STG - 2, nk - 1 - kt);  // tiles issued after kt (wave-uniform)
+      if (ahead >= STG - 2) vm_wait<(STG - 2) * PW>();
+      else vm_wait_n<PW, STG - 2>(ahead);
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < nk) dma(kt + 2);  // into the stage tile kt - 1 used
-      compute(smem + (kt % 3) * STAGE);
+      if (kt + STG - 1 < nk) dma(kt + STG - 1);  // into the stage tile kt - 1 used
+      compute(smem + (kt % STG) * STAGE);
     }
     __syncthreads();  // every wave is done with the stages before the epilogue reuses LDS
   }
@@ -315,7 +350,7 @@ __device__ __forceinline__ void gl_tile(unsigned short* smem, int M, int N, cons
 }
 
 template <bool A_KC, bool B_KC, int EPI, bool SPLIT, class CF>
-__global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) void gemm_gl_kernel(
+__global__ __launch_bounds__(CF::NT, CF::WPC) void gemm_gl_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, long long lda, const unsigned short* __restrict__ B,
     long long ldb, float* __restrict__ C, long long ldc, const float* __restrict__ bias, float beta, int k_per_split,
     int grid_m, int grid_n, long long sa, long long sb, long long sc, float* __restrict__ part) {
@@ -716,7 +751,7 @@ __device__ __forceinline__ void grouped_tile(const GlProb p, int L, unsigned sho
 }
 
 template <bool A_KC, bool B_KC, class CF, bool RS = false>
-__global__ __launch_bounds__(CF::NT, (CF::NT == 256 && CF::STG == 2) ? 2 : 1) void gemm_gl_grouped_kernel(GlGroup g) {
+__global__ __launch_bounds__(CF::NT, CF::WPC) void gemm_gl_grouped_kernel(GlGroup g) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
   // problems by DISPATCH order (so every problem's workgroups are dealt over all 8 XCDs: an
   // XCD-contiguous remap of the whole grid handed one XCD nearly all of dW_lin's long k-ranges,
@@ -791,6 +826,8 @@ __global__ __launch_bounds__(256) void gemm_gl_grouped_reduce_kernel(GlGroup g) 
 typedef Cfg<128, 2> C128;  // 128 x 128, double buffer, two workgroups per CU (the round-2 default)
 typedef Cfg<256, 3> C256;  // 256 x 128, three stages, one workgroup per CU
 typedef Cfg<128, 3> C128S3;  // 128 x 128, three stages (measured slower: A/B knob only)
+typedef Cfg<128, 5, 32> C128D5;  // 128 x 128, five 32-deep stages (80 KB), two per CU: the deep ring
+typedef Cfg<128, 4, 32> C128D4;  // the same with four stages (64 KB): three k-tiles in flight
 // tile configuration: 0 = per shape (gl_cfg_for), 1 = C128, 2 = C256, 3 = C128S3, 4 / 5 = 256 x 256
 // ping-pong with 8 / 10 half-tile slots
 int g_gl_cfg = 0;
@@ -890,6 +927,8 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
   if (cfg == 5) return launch_pp<A_KC, B_KC, 10>(GGL_ARGS);
   if (cfg == 2) return launch_cfg<A_KC, B_KC, C256>(GGL_ARGS);
   if (cfg == 3) return launch_cfg<A_KC, B_KC, C128S3>(GGL_ARGS);
+  if (cfg == 6) return launch_cfg<A_KC, B_KC, C128D5>(GGL_ARGS);
+  if (cfg == 7) return launch_cfg<A_KC, B_KC, C128D4>(GGL_ARGS);
   return launch_cfg<A_KC, B_KC, C128>(GGL_ARGS);
 #undef GGL_ARGS
 }
@@ -898,9 +937,10 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
 
 // Tuning knob (tools/gemm_gl_bench.py): tile configuration of gemm_gl (0 = per shape, 1 =
 // 128 x 128 double buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages, 4 = 256 x
-// 256 ping-pong, 128 KB LDS, 5 = the same with the whole 160 KB: six half-tiles in flight).
+// 256 ping-pong, 128 KB LDS, 5 = the same with the whole 160 KB: six half-tiles in flight, 6 / 7 =
+// 128 x 128 deep ring: five / four 32-deep k-tile stages, four / three k-tiles in flight).
 DL4SS_API int dl4ss_gemm_gl_set_config(int cfg) {
-  DL4SS_REQUIRE(cfg >= 0 && cfg <= 5);
+  DL4SS_REQUIRE(cfg >= 0 && cfg <= 7);
   g_gl_cfg = cfg;
   return 0;
 }
@@ -1056,7 +1096,8 @@ DL4SS_API int dl4ss_gemm_bf16_gl_grouped(int n, int transA, int transB, const in
 
 // The persistent form: `grid` workgroups walk the group's tiles (grid <= 0: one per tile, as
 // dl4ss_gemm_bf16_gl_grouped), in tile configuration cfg (1 = 128 x 128 double buffer; 2 = 256 x
-// 128, three stages, 144 KB LDS: one workgroup per CU); one_per_cu pads cfg 1's LDS so that one
+// 128, three stages, 144 KB LDS: one workgroup per CU; 6 / 7 = 128 x 128 deep ring of five / four
+// 32-deep stages, two workgroups per CU); one_per_cu pads cfg 1's LDS so that one
 // workgroup fills a CU.  rowsum (NULL, or n pointers, each NULL or M_i floats): rowsum_i[m] =
 // beta_i rowsum_i[m] + sum_k op(A_i)(m, k) for unsplit problems with both operands k-major (the
 // Linear's bias gradient beside its weight gradient).  For a side stream beside the persistent recurrence, which leaves the CUs
@@ -1067,8 +1108,14 @@ DL4SS_API int dl4ss_gemm_bf16_gl_grouped_ex(int n, int transA, int transB, const
                                             const float* beta, const int* splitk, void* ws, long long ws_bytes,
                                             int grid, int cfg, int one_per_cu, float* const* rowsum, void* stream) {
   DL4SS_REQUIRE(n >= 1 && n <= GMAXP && M && N && K && A && lda && B && ldb && C && ldc && beta && splitk);
-  DL4SS_REQUIRE(cfg == 1 || cfg == 2);
+  DL4SS_REQUIRE(cfg == 1 || cfg == 2 || cfg == 6 || cfg == 7);
   hipStream_t st = as_stream(stream);
+  if (cfg == 6)
+    return grouped_launch<C128D5>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes,
+                                  grid, 0, rowsum, st);
+  if (cfg == 7)
+    return grouped_launch<C128D4>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes,
+                                  grid, 0, rowsum, st);
   if (cfg == 2)
     return grouped_launch<C256>(n, !transA, transB, M, N, K, A, lda, B, ldb, C, ldc, beta, splitk, ws, ws_bytes, grid,
                                 0, rowsum, st);

@@ -116,7 +116,8 @@ def test_grouped_empty_problems_are_no_ops(dev):
     ops.GroupedGemm([probs[1]], dev).run()  # nothing left to launch
 
 
-@pytest.mark.parametrize("grid,cfg,one", [(16, 1, True), (7, 1, False), (16, 2, False)])
+@pytest.mark.parametrize("grid,cfg,one", [(16, 1, True), (7, 1, False), (16, 2, False), (16, 6, False), (0, 6, False),
+                                          (9, 7, False)])
 def test_grouped_persistent_form_matches(dev, grid, cfg, one):
     """dl4ss_gemm_bf16_gl_grouped_ex: `grid` workgroups walk the tiles (the side-stream form beside
     the recurrence).  Each tile's k-loop and epilogue are the one-tile-per-workgroup launch's, so the
@@ -137,7 +138,7 @@ def test_grouped_persistent_form_matches(dev, grid, cfg, one):
         assert torch.equal(p["out"], q["out"])
 
 
-@pytest.mark.parametrize("cfg", [2, 1])
+@pytest.mark.parametrize("cfg", [2, 1, 6])
 def test_grouped_rowsum_is_the_bias_gradient(dev, cfg):
     """The side-stream dW_lin (engine.SepTrainer.side): the persistent grouped launch also forms
     rowsum[m] = beta rowsum[m] + sum_k op(A)(m, k) -- the Linear's bias gradient, the column sums of
