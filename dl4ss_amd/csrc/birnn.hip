@@ -98,7 +98,12 @@ __device__ __forceinline__ u64 rtc_now() {
 // Gate nonlinearities on the serial critical path: v_exp + v_rcp (1 ulp) instead of
 // the IEEE division / ocml tanh sequences (the cell update runs on one wave).
 __device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
-__device__ __forceinline__ float ftanh(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f; }
+// tanh(x) = 2 / (1 + 2^(x (-2 log2 e))) - 1: the constant folded into ONE multiply (-2 log2e is exact in
+// fp32, so x * (-2 L) rounds the same product as (-2 x) * L did -- bitwise the two-multiply form, one
+// dependent VALU op shorter on the recurrences' critical cell chain)
+__device__ __forceinline__ float ftanh(float x) {
+  return 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -2.88539008177792681472f)) - 1.0f;
+}
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -873,6 +878,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_NT_HPREVB
 #define FWD_NT_HPREVB 1
 #endif
+// The packed forward's publish gathers a granule pair's six bf16 h values by DPP wave shifts
+// (round 6); 0: through an LDS stage and read-back (the round-2..5 form, A/B)
+#ifndef FWD_PUB_DPP
+#define FWD_PUB_DPP 1
+#endif
   // FWD_STORE_WAVES (experiment, off): the saved-state stores of step s leave from waves 2-3
   // (matvec-only, idle after B2) during step s+1 instead of from the cell lanes after their publish:
   // the cell lanes stage {act, c, h_{t-1}, h} in LDS (double buffered by step parity), the last step
@@ -1298,6 +1308,32 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         }
       }
       STAMP(5)
+#if FWD_PUB_DPP
+      // publish: lane cu = 6 k (k < 4) of each row packs the bf16 h of units cu .. cu + 5 (units >=
+      // J and padded rows are zeros) into two tagged granules and stores them with one 16-B
+      // write-through store.  The neighbours' values arrive by five DPP wave shifts (lane i reads
+      // lane i + 1), not through an LDS stage and read-back (round 6: the LDS round trip sat on
+      // every step's critical path)
+      {
+        const int v0 = ct ? (int)bf16_rne(hn) : 0;
+        const int v1 = __builtin_amdgcn_mov_dpp(v0, 0x130, 0xF, 0xF, true);  // wave_shl:1
+        const int v2 = __builtin_amdgcn_mov_dpp(v1, 0x130, 0xF, 0xF, true);
+        const int v3 = __builtin_amdgcn_mov_dpp(v2, 0x130, 0xF, 0xF, true);
+        const int v4 = __builtin_amdgcn_mov_dpp(v3, 0x130, 0xF, 0xF, true);
+        const int v5 = __builtin_amdgcn_mov_dpp(v4, 0x130, 0xF, 0xF, true);
+        const int k6 = cu / 6;
+        if (cu == 6 * k6 && k6 < 4) {
+          const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
+          const u32x4 x = {(unsigned)v0 | ((unsigned)v1 << 16), (unsigned)v2 | (tag << 16),
+                           (unsigned)v3 | ((unsigned)v4 << 16), (unsigned)v5 | (tag << 16)};
+          const int off = ((s & 1) * 2 * slot_g + (cb * NG + w) * 8 + 2 * k6) * 8;
+          if (wt)
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 16);  // sc1 write-through (group spans XCDs)
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);   // plain: stays in the group's L2
+        }
+      }
+#else
       // stage bf16 h (padded rows / units >= H stage zeros) and publish: lanes 0-3 of
       // each row read 6 staged values (LDS is in order within the wave) and store two
       // tagged granules with one 16-B write-through store
@@ -1315,6 +1351,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         else
           __builtin_amdgcn_raw_buffer_store_b128(x, xr, off, 0, 0);   // plain: stays in the group's L2
       }
+#endif
       STAMP(6)
       if (tid == 0) TRACE(0, s);
 #ifndef FWD_EXP_SKIP
@@ -2221,12 +2258,22 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       STAMP(4)
       const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
       constexpr int NQW = BC * WSPAN / 4;  // 16-B quads of this wave
+      constexpr int NQI = (NQW + 63) / 64;
+      // every quad's LDS read issued before the first is used (one LDS round trip, not one per store:
+      // a lane past the wave's quads reads a valid clamped quad and stores nothing)
+      float4 vq[NQI];
+#pragma unroll
+      for (int i = 0; i < NQI; ++i) {
+        const int e = min(64 * i + lane, NQW - 1);
+        const int bb = e / (WSPAN / 4), kl = 4 * (e % (WSPAN / 4));
+        vq[i] = *reinterpret_cast<const float4*>(wsw + bb * WSP + kl);
+      }
 #pragma unroll
       for (int e0 = 0; e0 < NQW; e0 += 64) {
         const int e = e0 + lane;
         const int bb = e / (WSPAN / 4), k = wv * WSPAN + 4 * (e % (WSPAN / 4));
         if ((NQW % 64 == 0 || e < NQW) && k < H) {
-          const float4 v = *reinterpret_cast<const float4*>(wsw + bb * WSP + (k - wv * WSPAN));
+          const float4 v = vq[e0 / 64];
           const unsigned r0 = pack24(v.x), r1 = pack24(v.y), r2 = pack24(v.z), r3 = pack24(v.w);
           const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
           const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules
