@@ -55,6 +55,7 @@ constexpr int HMAX_L = 640;  // largest hidden size of the forward-only (inferen
 constexpr int DL4SS_RNN_WS_ZEROED = 0x100;  // precision flag: workspace already zero (no memset)
 constexpr int DL4SS_RNN_DEFER_BIAS = 0x400;  // BPTT: leave the per-row bias partials for dl4ss_birnn_bias_reduce
 constexpr int DL4SS_RNN_DGH_PAD8 = 0x200;  // precision flag (bwd): dGh_bf16 direction stride padded to 8
+constexpr int DL4SS_RNN_DOUT_SLABS_MASK = 0x3000;  // precision field (bwd): dOut = (S - 1) << 12 split-K slabs
 constexpr unsigned SPIN_LIMIT = 1u << 20;  // ~1 s of polling: a stuck hand-off exits, never hangs
 
 typedef unsigned long long u64;
@@ -190,7 +191,9 @@ struct RnnArgs {
   float* hprev;          // (B,T,2H) h_{t-1} per step (zero at the sequence start)
   float* act;            // (B,T,2,4H) LSTM: i,f,g,o ; GRU: r,z,n,(W_hn h + b_hn)
   float* cs;             // (B,T,2,H) LSTM cell states
-  const float* dOut;     // bwd (B,T,2H)
+  const float* dOut;     // bwd (B,T,2H), or dout_ns split-K slabs of it dout_zs floats apart (summed in order)
+  int dout_ns;
+  long long dout_zs;
   const float* dOutB;    // bwd optional (B,2H) added to dOut at every t (d mean_t h)
   float* dG;             // bwd (B,T,2,NGATE*H) grad wrt input projection (pre-activation)
   float* dGh;            // bwd GRU: grad wrt W_hh h + b_hh (LSTM: == dG, may be null)
@@ -241,22 +244,45 @@ __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& grou
 // p[q][(t + shift[q]) * stride[q]] (0 outside [0, T)), landing in LDS at dst[q].
 // Loads for step s+1 are issued during step s and committed to LDS at step s+1
 // (by then the granule poll has already waited past them).
-template <int NQ>
+// NZ > 1 (the BPTT's dOut, DL4SS_RNN_DOUT_SLABS): an item with nz[q] > 1 is the sum of nz[q] split-K
+// slabs zs floats apart, all loaded at issue and added at commit in slab order from zero -- bitwise the
+// gemm_gl split-K combine it replaces (((0 + s0) + s1) + ...).
+template <int NQ, int NZ = 1>
 struct StepLoader {
   const float* p[NQ];
   int stride[NQ], shift[NQ], dst[NQ];
   float v[NQ];
+  int nz[NQ];
+  long long zs;
+  float vz[NQ][NZ > 1 ? NZ - 1 : 1];
   __device__ __forceinline__ void issue(int t, int T) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int tt = t + shift[q];
-      v[q] = (p[q] != nullptr && tt >= 0 && tt < T) ? p[q][(long long)tt * stride[q]] : 0.0f;
+      const bool ok = p[q] != nullptr && tt >= 0 && tt < T;
+      v[q] = ok ? p[q][(long long)tt * stride[q]] : 0.0f;
+      if constexpr (NZ > 1) {
+#pragma unroll
+        for (int z = 1; z < NZ; ++z)
+          vz[q][z - 1] = (ok && z < nz[q]) ? p[q][(long long)tt * stride[q] + z * zs] : 0.0f;
+      }
     }
   }
   __device__ __forceinline__ void commit(float* lds) const {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      if (dst[q] >= 0) lds[dst[q]] = v[q];
+    for (int q = 0; q < NQ; ++q) {
+      if (dst[q] < 0) continue;
+      float x = v[q];
+      if constexpr (NZ > 1) {
+        if (nz[q] > 1) {
+          x = 0.0f + v[q];
+#pragma unroll
+          for (int z = 1; z < NZ; ++z)
+            if (z < nz[q]) x += vz[q][z - 1];
+        }
+      }
+      lds[dst[q]] = x;
+    }
   }
 };
 
@@ -1880,7 +1906,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   constexpr int NQA = PFF ? (CPWP + 63) / 64 : 1;
   const int ncell = BC * J, cpw = (ncell + 1) / 2, pwi = wv - WPF;
   float* sraw = sop + 2 * 2 * SOPP + (wv >= WPF ? pwi : 0) * NSL * CPWP;
-  StepLoader<NQ> ld;
+  StepLoader<NQ, 4> ld;  // dOut: up to 4 split-K slabs (DL4SS_RNN_DOUT_SLABS)
+  ld.zs = a.dout_zs;
   const float4* ap[NQA];
   float4 av[NQA];
   int ac[NQA];
@@ -1947,6 +1974,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.stride[q] = stride;
     ld.shift[q] = shift;
     ld.dst[q] = !on ? -1 : PFF ? slot * CPWP + c : (slot >> 2) * SOPP + cell * 4 + (slot & 3);
+    ld.nz[q] = slot == 0 ? a.dout_ns : 1;
   }
   if (wv >= WPF) {
     ld.issue(d == 0 ? T - 1 : 0, T);
@@ -2860,7 +2888,8 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   const bool prezeroed = precision & DL4SS_RNN_WS_ZEROED;
   const bool dgh_pad8 = precision & DL4SS_RNN_DGH_PAD8;
   const bool defer_bias = precision & DL4SS_RNN_DEFER_BIAS;
-  precision &= ~(DL4SS_RNN_WS_ZEROED | DL4SS_RNN_DGH_PAD8 | DL4SS_RNN_DEFER_BIAS);
+  const int dout_ns = ((precision & DL4SS_RNN_DOUT_SLABS_MASK) >> 12) + 1;
+  precision &= ~(DL4SS_RNN_WS_ZEROED | DL4SS_RNN_DGH_PAD8 | DL4SS_RNN_DEFER_BIAS | DL4SS_RNN_DOUT_SLABS_MASK);
   DL4SS_REQUIRE(precision == 0 || precision == 1);
   DL4SS_REQUIRE(B > 0 && T > 0 && H > 0 && dOut && W_hh && act && workspace && status);
   DL4SS_REQUIRE(dG || dG_bf16);
@@ -2883,10 +2912,14 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   }
   // bf16 gradient copies, dropping the fp32 ones and the fused bias sums need the packed kernel
   DL4SS_REQUIRE(pk || (!dG_bf16 && !dGh_bf16 && !db_ih && !db_hh && dG && (cell == CELL_LSTM || dGh)));
+  // split-K dOut slabs: the packed BPTT's step-factor prefetch (batch chunks >= 4) sums them
+  DL4SS_REQUIRE(dout_ns == 1 || (pk && p.BC >= 4));
   RnnArgs a{};
   fill_args(a, p, B, T, H);
   a.Whh = W_hh; a.act = const_cast<float*>(act); a.cs = const_cast<float*>(cs);
   a.hprev = const_cast<float*>(hprev); a.dOut = dOut; a.dOutB = dOut_bcast; a.dG = dG; a.dGh = dGh;
+  a.dout_ns = dout_ns;
+  a.dout_zs = (long long)B * T * 2 * H;
   a.dGb = reinterpret_cast<unsigned short*>(dG_bf16); a.dGhb = reinterpret_cast<unsigned short*>(dGh_bf16);
   const int GHc = (cell == CELL_LSTM ? 4 : 3) * H;
   a.ghb = dgh_pad8 ? (GHc + 7) / 8 * 8 : GHc;

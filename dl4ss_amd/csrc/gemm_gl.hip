@@ -61,7 +61,7 @@ struct Cfg {
   static constexpr int WPC = (NT == 256 && STG_ * STAGE * 2 <= 80 * 1024) ? 2 : 1;  // workgroups per CU
   static_assert(CPW_A >= 1 && CPW_B >= 1, "at least one DMA per wave and operand");
 };
-enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2 };
+enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2, EPI_SPLIT_SLABS = 3 };
 
 // 64 zero bytes every out-of-range k chunk is loaded from (16 B per lane)
 __device__ __attribute__((aligned(64))) const unsigned g_zero_line[16] = {0};
@@ -848,12 +848,13 @@ int launch_cfg(int M, int N, int K, const unsigned short* A, long long lda, cons
   const int ntiles = gm * gn;
   dim3 grid(ntiles, batch, splitk);
   if (splitk > 1) {
-    if (epi != EPI_NONE) return (int)hipErrorInvalidValue;
+    if (epi != EPI_NONE && epi != EPI_SPLIT_SLABS) return (int)hipErrorInvalidValue;
     const long long need = (long long)batch * splitk * M * N * 4;
     if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL((gemm_gl_kernel<A_KC, B_KC, EPI_NONE, true, CF>), grid, dim3(CF::NT), 0, st, M, N, K, A, lda, B,
                        ldb, C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
     DL4SS_CHECK_LAUNCH();
+    if (epi == EPI_SPLIT_SLABS) return 0;  // the slabs stay in ws for their consumer
     if (N % 4 == 0 && ldc % 4 == 0 && sc % 4 == 0 && ((uintptr_t)C & 15) == 0)
       hipLaunchKernelGGL(gemm_gl_reduce_kernel<true>, dim3(cdiv((long long)M * N / 4, 256), batch), dim3(256), 0, st, M,
                          N, splitk, ws, C, ldc, sc, bias, beta);
@@ -898,12 +899,13 @@ int launch_pp(int M, int N, int K, const unsigned short* A, long long lda, const
   splitk = (K + kps - 1) / kps;
   dim3 grid(gm * gn, batch, splitk);
   if (splitk > 1) {
-    if (epi != EPI_NONE) return (int)hipErrorInvalidValue;
+    if (epi != EPI_NONE && epi != EPI_SPLIT_SLABS) return (int)hipErrorInvalidValue;
     const long long need = (long long)batch * splitk * M * N * 4;
     if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL((gemm_pp_kernel<A_KC, B_KC, EPI_NONE, true, SL>), grid, dim3(pp::NT), 0, st, M, N, K, A, lda, B,
                        ldb, C, ldc, nullptr, 0.0f, kps, gm, gn, sa, sb, sc, ws);
     DL4SS_CHECK_LAUNCH();
+    if (epi == EPI_SPLIT_SLABS) return 0;
     return launch_reduce(M, N, splitk, batch, C, ldc, sc, bias, beta, ws, st);
   }
 #define GPP_LAUNCH(EPI_)                                                                                            \
@@ -980,6 +982,10 @@ DL4SS_API int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, co
   DL4SS_REQUIRE(b_kc || ldb >= ((N + 7) & ~7));
   if (epilogue == EPI_TANH_BF16)
     DL4SS_REQUIRE(beta == 0.0f && splitk == 1 && (ldc & 1) == 0 && ((uintptr_t)C & 3) == 0);
+  // split slabs only: the effective split (after the 64-k rounding) must still be > 1, no bias / beta
+  if (epilogue == EPI_SPLIT_SLABS)
+    DL4SS_REQUIRE(bias == nullptr && beta == 0.0f && dl4ss_gemm_bf16_gl_ws_bytes(M, N, K, splitk, batch) > 0);
+  DL4SS_REQUIRE(epilogue >= EPI_NONE && epilogue <= EPI_SPLIT_SLABS);
   hipStream_t st = as_stream(stream);
   const auto* a = reinterpret_cast<const unsigned short*>(A);
   const auto* b = reinterpret_cast<const unsigned short*>(B);

@@ -29,6 +29,10 @@ DGH_PAD8 = 0x200  # DL4SS_RNN_DGH_PAD8
 DEFER_BIAS = 0x400  # DL4SS_RNN_DEFER_BIAS
 
 
+def DOUT_SLABS(n):  # DL4SS_RNN_DOUT_SLABS(S): the BPTT sums dOut's S split-K slabs itself
+    return ((n - 1) & 3) << 12
+
+
 def _ngate(cell):
     return 4 if cell == "lstm" else 3
 
@@ -244,6 +248,11 @@ class SepTrainer:
             raise ValueError(f"precision '{precision}' runs the bf16 recurrence (rnn_precision bf16)")
         self.fast = precision in ("bf16", "bf16s", "bf16s2") and self.rnn_precision == "bf16"
         self.dh_split = int(os.environ.get("DL4SS_DH_SPLIT", "3"))  # dH split-K (tuning knob, A/B runs)
+        # dH's split-K slabs summed by the top layer's BPTT as it loads dOut (DL4SS_RNN_DOUT_SLABS, round 6):
+        # no combine launch between the dH GEMM and the first BPTT.  Set per trainer in the bf16 step
+        # when the BPTT plan has batch chunks >= 4 (the packed loader that sums them); DL4SS_DH_SLABS=0: the
+        # combine launch (A/B)
+        self.dh_slabs = 1
         self.dx_split = int(os.environ.get("DL4SS_DX_SPLIT", "1"))  # dX split-K (tuning knob, A/B runs)
         # BPTT bias partials reduced once after the last BPTT instead of after each (A/B knob)
         self.defer_bias = os.environ.get("DL4SS_DEFER_BIAS", "1") != "0"
@@ -357,6 +366,14 @@ class SepTrainer:
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", 2 * NGH, 2 * H, BT, 4, 1),
                           _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", NGH, H, BT, 8, 2))
             self.gl_ws = torch.empty(max(gl_need, 1), device=dev, dtype=torch.uint8)
+            plan = ops.birnn_plan(net.cell, B, H) if dev.type == "cuda" else None
+            nsl = _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, F * net.E, max(1, self.dh_split), 1) // \
+                (BT * 2 * H * 4)
+            if os.environ.get("DL4SS_DH_SLABS", "1") != "0" and plan is not None and plan["BC"] >= 4 and 2 <= nsl <= 4:
+                self.dh_slabs = int(nsl)
+                # the slabs' own workspace: other split-K GEMMs between dH and the BPTT (dW_lin off the side
+                # stream) must not overwrite them
+                self.dh_ws = torch.empty(nsl * BT * 2 * H * 4, device=dev, dtype=torch.uint8)
             # partial sums of the deterministic Linear-bias colsum (dl4ss_colsum_bf16_det)
             pb = _lib.query("dl4ss_colsum_bf16_part_bytes", BT, F * net.E)
             self.colsum_part = torch.empty(max(1, pb // 4), device=dev, dtype=torch.float32)
@@ -704,7 +721,11 @@ class SepTrainer:
         # gemm_gl split-K factors, measured per shape at C2 (tools/gemm_gl_bench.py --sweep): dH
         # 8032x600x6450 -> 3, dW_lin 6450x600x8032 -> 2, dX 8032x600x2400 -> 1, dW_ih
         # 2400x600x8032 -> 4, dW_hh 2 x 1200x300x8032 -> 8 (slabs + a fixed-order reduce)
-        ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], splitk=self.dh_split, ws=self.gl_ws)
+        if self.dh_slabs > 1:  # the slabs stay in dh_ws: the top layer's BPTT sums them (DL4SS_RNN_DOUT_SLABS)
+            ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], splitk=self.dh_split, ws=self.dh_ws,
+                             epilogue=ops.EPI_SPLIT_SLABS)
+        else:
+            ops.gemm_bf16_gl(dPreb, self.wb_lin[:, :2 * H], out=self.dH[0], splitk=self.dh_split, ws=self.gl_ws)
         if (not grouped or self.buckets) and not self.side:  # (bitwise the grouped launch's dW_lin at the same split)
             ops.gemm_bf16_gl(dPreb, self.outb[-1][:, :2 * H], transA=True, out=net.view("mix.Linear.weight", g),
                              beta=self._gbeta, splitk=2, ws=self.gl_ws)
@@ -786,9 +807,11 @@ class SepTrainer:
         for l in range(net.L - 1, -1, -1):
             dGb = self.dGb_l[l]
             dGhb = self.dGhb_l[l] if gru else dGb
+            # the top layer reads dH as the dH GEMM's split-K slabs (summed as it loads them)
+            slabs = self.dh_slabs if l == net.L - 1 else 1
             _lib.call("dl4ss_birnn_bwd_ex", cell, 1 | WS_ZEROED | (DEFER_BIAS if self.defer_bias else 0) |
-                      (DGH_PAD8 if gru else 0), B, T, H,
-                      _lib.ptr(dH),
+                      (DGH_PAD8 if gru else 0) | DOUT_SLABS(slabs), B, T, H,
+                      _lib.ptr(self.dh_ws) if slabs > 1 else _lib.ptr(dH),
                       _lib.ptr(self.dh_bcast) if (l == net.L - 1 and net.adjust) else None,
                       _lib.ptr(net.cat_view("weight_hh", l)), _lib.ptr(self.act[l]),
                       _lib.ptr(self.cs[l]) if self.cs else None, _lib.ptr(self.hprev[l]), None, None,

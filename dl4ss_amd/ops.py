@@ -104,6 +104,9 @@ def mix_sources(raw, gains, out_src=None, out_mix=None, stats_ws=None, lengths=N
 # ---------------------------------------------------------------------------
 PREC = {"fp32": 0, "bf16": 1}
 EPI_NONE, EPI_TANH, EPI_TANH_BF16 = 0, 1, 2  # 2: tanh written as bf16 (gemm_bf16_gl only)
+# gemm_bf16_gl split-K only: leave the fp32 slabs in ws for their consumer (no combine, out not written;
+# DL4SS_EPI_SPLIT_SLABS, include/dl4ss_hip.h)
+EPI_SPLIT_SLABS = 3
 
 
 def _mat(t, name):

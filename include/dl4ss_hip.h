@@ -78,7 +78,11 @@ int dl4ss_mix_sources_rot(const float* raw, const int* lengths, const int* shift
                           int N, float* stats_ws, float* out_src, float* out_mix, void* stream);
 
 /* ---- dense contractions (MFMA) ------------------------------------------ */
-enum { DL4SS_EPI_NONE = 0, DL4SS_EPI_TANH = 1, DL4SS_EPI_TANH_BF16 = 2 /* tanh, C written as bf16 */ };
+enum { DL4SS_EPI_NONE = 0, DL4SS_EPI_TANH = 1, DL4SS_EPI_TANH_BF16 = 2 /* tanh, C written as bf16 */,
+       DL4SS_EPI_SPLIT_SLABS = 3 /* dl4ss_gemm_bf16_gl split-K only: the S fp32 slabs stay in ws
+                                    ([S][batch][M][N], S = dl4ss_gemm_bf16_gl_ws_bytes / (batch M N 4)),
+                                    no combine, C not written: their consumer sums them (the
+                                    BPTT's DL4SS_RNN_DOUT_SLABS) */ };
 enum { DL4SS_PREC_F32 = 0, DL4SS_PREC_BF16 = 1 };
 /* C = op(A) op(B) (+ bias[N]) (tanh) (+ beta C); row-major, leading dims in elements.
  * transA: A stored K x M (else M x K); transB: B stored N x K (else K x N).
@@ -101,7 +105,8 @@ int dl4ss_f32_to_bf16(const float* x, void* y, long long n, void* stream);
  * to 8 with zeros in that padding; hipErrorInvalidValue otherwise. */
 long long dl4ss_gemm_bf16_gl_ws_bytes(int M, int N, int K, int splitk, int batch);
 /* Tuning knob: tile configuration of dl4ss_gemm_bf16_gl (0 = per shape, 1 = 128 x 128 double
- * buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages). */
+ * buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages, 4 / 5 = 256 x 256 ping-pong,
+ * 6 / 7 = 128 x 128 with five / four 32-deep k-tile stages). */
 int dl4ss_gemm_gl_set_config(int cfg);
 int dl4ss_gemm_bf16_gl(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
                        long long ldb, float* C, long long ldc, const float* bias, int epilogue, float beta,
@@ -175,6 +180,11 @@ enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
  * workspaces and bias gradient pointers as host arrays) into db_ih / db_hh in ONE launch, in the
  * same fixed row order (bitwise the per-launch reduce). */
 #define DL4SS_RNN_DEFER_BIAS 0x400
+/* precision field of dl4ss_birnn_bwd_ex (bits 12-13: S - 1): dOut is not one (B, T, 2H) array but the S
+ * (2..4) fp32 split-K slabs dl4ss_gemm_bf16_gl leaves with DL4SS_EPI_SPLIT_SLABS, slab z at dOut + z B T 2H;
+ * the BPTT sums them per element in slab order from zero (((0 + s0) + s1) + ...), bitwise the combine
+ * launch it replaces.  Packed bf16 BPTT at batch chunks >= 4 only (hipErrorInvalidValue otherwise). */
+#define DL4SS_RNN_DOUT_SLABS(S) ((((S) - 1) & 3) << 12)
 int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
                             float* const* db_hh, void* stream);
 /* dl4ss_birnn_bias_reduce with db = beta db + sums: beta 0 writes db_ih / db_hh without reading them
