@@ -58,7 +58,9 @@ struct Cfg {
   static constexpr int PPP = KT_ / 4;  // 1-KB DMA pieces per 128-row panel per k-tile
   static constexpr int CPW_A = BM_ / 128 * PPP / NW, CPW_B = BN / 128 * PPP / NW;  // 1-KB DMAs per wave per k-tile
   static constexpr int IMG_A = BM_ * KT_, IMG_B = BN * KT_, STAGE = IMG_A + IMG_B;
-  static constexpr int WPC = (NT == 256 && STG_ * STAGE * 2 <= 80 * 1024) ? 2 : 1;  // workgroups per CU
+  // LDS (bf16 elements): the stages, at least the epilogue's staging (NW waves x 32 rows x 68 fp32)
+  static constexpr int SMEM = STG_ * STAGE > NW * 32 * 68 * 2 ? STG_ * STAGE : NW * 32 * 68 * 2;
+  static constexpr int WPC = NT != 256 ? 1 : SMEM * 2 <= 40 * 1024 ? 4 : SMEM * 2 <= 80 * 1024 ? 2 : 1;  // per CU
   static_assert(CPW_A >= 1 && CPW_B >= 1, "at least one DMA per wave and operand");
 };
 enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2, EPI_SPLIT_SLABS = 3 };
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(CF::NT, CF::WPC) void gemm_gl_kernel(
     int grid_m, int grid_n, long long sa, long long sb, long long sc, float* __restrict__ part) {
   constexpr int BM = CF::BM;
   // one LDS array (a second __shared__ object can make hipcc drain vmcnt before every ds_read)
-  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::SMEM];
   // XCD-major order over the WHOLE grid (tiles x batch members x k-splits): workgroups are
   // dealt round-robin over the 8 XCDs in dispatch order (x fastest, then y, then z; speed
   // only, never correctness), so the dispatch index L is remapped bijectively to R, giving
@@ -752,7 +754,7 @@ __device__ __forceinline__ void grouped_tile(const GlProb p, int L, unsigned sho
 
 template <bool A_KC, bool B_KC, class CF, bool RS = false>
 __global__ __launch_bounds__(CF::NT, CF::WPC) void gemm_gl_grouped_kernel(GlGroup g) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::STG * CF::STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned short smem[CF::SMEM];
   // problems by DISPATCH order (so every problem's workgroups are dealt over all 8 XCDs: an
   // XCD-contiguous remap of the whole grid handed one XCD nearly all of dW_lin's long k-ranges,
   // 616 vs ~330 us), then the XCD-major remap inside the problem (L0 = its first dispatch index;
@@ -828,6 +830,7 @@ typedef Cfg<256, 3> C256;  // 256 x 128, three stages, one workgroup per CU
 typedef Cfg<128, 3> C128S3;  // 128 x 128, three stages (measured slower: A/B knob only)
 typedef Cfg<128, 5, 32> C128D5;  // 128 x 128, five 32-deep stages (80 KB), two per CU: the deep ring
 typedef Cfg<128, 4, 32> C128D4;  // the same with four stages (64 KB): three k-tiles in flight
+typedef Cfg<128, 2, 32> C128H2;  // 32-deep double buffer (32 KB): four workgroups per CU
 // tile configuration: 0 = per shape (gl_cfg_for), 1 = C128, 2 = C256, 3 = C128S3, 4 / 5 = 256 x 256
 // ping-pong with 8 / 10 half-tile slots
 int g_gl_cfg = 0;
@@ -931,6 +934,7 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
   if (cfg == 3) return launch_cfg<A_KC, B_KC, C128S3>(GGL_ARGS);
   if (cfg == 6) return launch_cfg<A_KC, B_KC, C128D5>(GGL_ARGS);
   if (cfg == 7) return launch_cfg<A_KC, B_KC, C128D4>(GGL_ARGS);
+  if (cfg == 8) return launch_cfg<A_KC, B_KC, C128H2>(GGL_ARGS);
   return launch_cfg<A_KC, B_KC, C128>(GGL_ARGS);
 #undef GGL_ARGS
 }
@@ -940,9 +944,10 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
 // Tuning knob (tools/gemm_gl_bench.py): tile configuration of gemm_gl (0 = per shape, 1 =
 // 128 x 128 double buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages, 4 = 256 x
 // 256 ping-pong, 128 KB LDS, 5 = the same with the whole 160 KB: six half-tiles in flight, 6 / 7 =
-// 128 x 128 deep ring: five / four 32-deep k-tile stages, four / three k-tiles in flight).
+// 128 x 128 deep ring: five / four 32-deep k-tile stages, four / three k-tiles in flight, 8 = 128 x 128
+// 32-deep double buffer, four workgroups per CU).
 DL4SS_API int dl4ss_gemm_gl_set_config(int cfg) {
-  DL4SS_REQUIRE(cfg >= 0 && cfg <= 7);
+  DL4SS_REQUIRE(cfg >= 0 && cfg <= 8);
   g_gl_cfg = cfg;
   return 0;
 }
