@@ -90,55 +90,91 @@ __global__ __launch_bounds__(64) void query_fwd_kernel(const float* __restrict__
   }
 }
 
-// Backward of the queries (thread per output, every sum over <= 64 terms, loads unrolled):
+// Backward of the queries (thread per output, every sum over <= 64 terms):
 //   dh_bcast[b][c] = sum_o W[o][c] u[b][o] / T,   u[b][o] = sum_k dq[b,k,o]   (c < D)
-//   dEmb[idx[b,k]][c] += dq[b,k,c] + sum_o W[o][D + c] dq[b,k,o]              (atomics)
+//   dEmb[idx[b,k]][c] += dq[b,k,c] + sum_o W[o][D + c] dq[b,k,o]
 //   dW_adj[o][c] += sum_b u[b][o] mean[b][c]  (c < D);  sum_{b,k} dq[b,k,o] Emb[idx[b,k]][c-D]
-// Every dh / dW_adj element has one owner thread and a fixed summation order; only the
-// embedding rows (speaker ids shared across the batch) use atomics.
-__device__ __forceinline__ void query_bwd_dh(int bx, int by, const float* __restrict__ dq,
+// Every element has one owner thread and a fixed summation order (no atomics).  Round 6: each role's
+// loads of a QCH-term chunk are issued together from clamped addresses and folded by selects (no
+// branches): the round-5 loops (five or eight loads at a time, predicated loads compiled to branches)
+// left four to ten dependent load rounds per role on this ~14 us launch.
+constexpr int QCH = 32;  // terms per load chunk (a multiple of 8: dW_adj's accumulator of term b is b & 7)
+__device__ __forceinline__ void query_bwd_dh(int bx, int by, float* su, const float* __restrict__ dq,
                                              const float* __restrict__ wadj, int T, int D, int K, int W,
                                              float* __restrict__ dh_bcast) {
   const int b = by, c = bx * 64 + threadIdx.x;
-  if (c >= D) return;
   const float* dqb = dq + (long long)b * K * W;
-  float g0 = 0.f, g1 = 0.f;
-#pragma unroll 5
-  for (int o = 0; o < W; ++o) {
+  for (int o = threadIdx.x; o < W; o += 64) {  // u[b][o], k in order from zero
     float u = 0.f;
     for (int k = 0; k < K; ++k) u += dqb[k * W + o];
-    const float t = wadj[(long long)o * (D + W) + c] * u;
-    if (o & 1) g1 += t; else g0 += t;
+    su[o] = u;
+  }
+  __syncthreads();
+  if (c >= D) return;
+  float g0 = 0.f, g1 = 0.f;
+  for (int o0 = 0; o0 < W; o0 += QCH) {
+    float wv[QCH];
+#pragma unroll
+    for (int i = 0; i < QCH; ++i) wv[i] = wadj[(long long)min(o0 + i, W - 1) * (D + W) + c];
+#pragma unroll
+    for (int i = 0; i < QCH; ++i) {
+      const int o = o0 + i;
+      const float t = wv[i] * su[min(o, W - 1)];
+      const bool in = o < W;
+      g0 = (in && !(o & 1)) ? g0 + t : g0;
+      g1 = (in && (o & 1)) ? g1 + t : g1;
+    }
   }
   dh_bcast[(long long)b * D + c] = (g0 + g1) / (float)T;
 }
 
 // d_emb[id] += sum over the rows bk with idx[bk] == id, in bk order: the block of the first
 // such row owns the label and sums every row of it (no atomics: a speaker drawn twice in a
-// batch gets the same bits on every run)
-__device__ __forceinline__ void query_bwd_emb(int bk, const float* __restrict__ dq, const int* __restrict__ idx,
-                                              int BK, const float* __restrict__ wadj, int D, int W,
+// batch gets the same bits on every run).  sidx: the batch's speaker ids staged in LDS by the block
+// (round 6: the ownership test and the row scan were serial scalar loads of idx); the matching rows
+// come from one ballot per 64 ids, visited in order.
+__device__ __forceinline__ void query_bwd_emb(int bk, const float* __restrict__ dq, const int* sidx, int BK,
+                                              const float* __restrict__ wadj, int D, int W,
                                               float* __restrict__ demb, float beta) {
-  const int id = idx[bk];
+  const int id = sidx[bk];
   if (id < 0) return;
-  for (int j = 0; j < bk; ++j)
-    if (idx[j] == id) return;  // an earlier row owns this label
-  for (int c = threadIdx.x; c < W; c += 64) {
+  for (int j0 = 0; j0 < bk; j0 += 64) {  // an earlier row owns this label
+    const int j = j0 + (int)threadIdx.x;
+    if (__any(j < bk && sidx[j] == id)) return;
+  }
+  for (int c0 = 0; c0 < W; c0 += 64) {  // every lane of the wave in each pass (the ballots are wave-wide)
+    const int c = c0 + (int)threadIdx.x, cc = min(c, W - 1);
     float acc = 0.f;
-    for (int r = bk; r < BK; ++r) {
-      if (idx[r] != id) continue;
-      const float* dqr = dq + (long long)r * W;
-      float g = dqr[c];
-      if (wadj) {
-        float g1 = 0.f;
-#pragma unroll 5
-        for (int o = 0; o < W; ++o) g1 = fmaf(wadj[(long long)o * (D + W) + D + c], dqr[o], g1);
-        g += g1;
+    for (int r0 = bk; r0 < BK; r0 += 64) {
+      const int rr = r0 + (int)threadIdx.x;
+      unsigned long long m = __ballot(rr < BK && sidx[rr] == id);
+      while (m) {  // wave-uniform: the rows of this label in order
+        const int r = r0 + __builtin_ctzll(m);
+        m &= m - 1;
+        const float* dqr = dq + (long long)r * W;
+        float g = dqr[cc];
+        if (wadj) {
+          float g1 = 0.f;
+          for (int o0 = 0; o0 < W; o0 += QCH) {
+            float wv[QCH], dv[QCH];
+#pragma unroll
+            for (int i = 0; i < QCH; ++i) {
+              const int o = min(o0 + i, W - 1);
+              wv[i] = wadj[(long long)o * (D + W) + D + cc];
+              dv[i] = dqr[o];
+            }
+#pragma unroll
+            for (int i = 0; i < QCH; ++i) g1 = o0 + i < W ? fmaf(wv[i], dv[i], g1) : g1;
+          }
+          g += g1;
+        }
+        acc += g;
       }
-      acc += g;
     }
-    float* o = demb + (long long)id * W + c;
-    *o = beta != 0.f ? acc + beta * *o : acc;  // beta 0: the row is written without being read
+    if (c < W) {
+      float* o = demb + (long long)id * W + c;
+      *o = beta != 0.f ? acc + beta * *o : acc;  // beta 0: the row is written without being read
+    }
   }
 }
 
@@ -147,7 +183,7 @@ __device__ __forceinline__ void query_bwd_w(int bx, int by, float* sm, const flo
                                             const float* __restrict__ mean, int B, int D, int K, int W,
                                             float* __restrict__ dwadj, float beta) {
   // block (column chunk, o): the o-th dq column (and its per-utterance sums u) and the
-  // speaker ids staged in LDS, then 8 independent loads in flight per thread
+  // speaker ids staged in LDS, then QCH loads in flight per thread
   float* sdq = sm;            // [B*K]  dq[bk][o]
   float* su = sdq + B * K;    // [B]    u[b][o]
   int* sid = reinterpret_cast<int*>(su + B);  // [B*K]
@@ -164,28 +200,29 @@ __device__ __forceinline__ void query_bwd_w(int bx, int by, float* sm, const flo
   }
   __syncthreads();
   if (c >= D + W) return;
+  // the sums over b (or b k) in eight interleaved accumulators, acc[j & 7] += term j in order
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < D) {
-    for (int b0 = 0; b0 < B; b0 += 8) {
-      float m[8];
+    for (int b0 = 0; b0 < B; b0 += QCH) {
+      float m[QCH];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = b0 + j < B ? mean[(long long)(b0 + j) * D + c] : 0.f;
+      for (int j = 0; j < QCH; ++j) m[j] = mean[(long long)min(b0 + j, B - 1) * D + c];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (b0 + j < B) acc[j] = fmaf(su[b0 + j], m[j], acc[j]);
+      for (int j = 0; j < QCH; ++j)
+        acc[j & 7] = b0 + j < B ? fmaf(su[min(b0 + j, B - 1)], m[j], acc[j & 7]) : acc[j & 7];
     }
   } else {
     const int ce = c - D;
-    for (int b0 = 0; b0 < B * K; b0 += 8) {
-      float e[8];
+    for (int b0 = 0; b0 < B * K; b0 += QCH) {
+      float e[QCH];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int id = b0 + j < B * K ? sid[b0 + j] : -1;
-        e[j] = id >= 0 ? emb[(long long)id * W + ce] : 0.f;
+      for (int j = 0; j < QCH; ++j) e[j] = emb[(long long)max(sid[min(b0 + j, B * K - 1)], 0) * W + ce];
+#pragma unroll
+      for (int j = 0; j < QCH; ++j) {
+        const int jj = min(b0 + j, B * K - 1);
+        const float ev = sid[jj] >= 0 ? e[j] : 0.f;
+        acc[j & 7] = b0 + j < B * K ? fmaf(sdq[jj], ev, acc[j & 7]) : acc[j & 7];
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (b0 + j < B * K) acc[j] = fmaf(sdq[b0 + j], e[j], acc[j]);
     }
   }
   const float sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
@@ -213,20 +250,26 @@ struct QbArgs {
 __global__ __launch_bounds__(64) void query_bwd_kernel(QbArgs a) {
   extern __shared__ float sm[];
   int blk = blockIdx.x;
-  if (blk < a.n_emb) {
-    query_bwd_emb(blk, a.dq, a.idx, a.B * a.K, a.wadj, a.D, a.W, a.demb, a.beta);
-    return;
-  }
-  blk -= a.n_emb;
-  if (blk < a.n_zero) {  // (beta 0) embedding row blk: zero unless a speaker of the batch owns it
-    for (int j = 0; j < a.B * a.K; ++j)
-      if (a.idx[j] == blk) return;
+  const int BK = a.B * a.K;
+  if (blk < a.n_emb + a.n_zero) {  // the embedding roles: the batch's speaker ids in LDS first
+    int* sidx = reinterpret_cast<int*>(sm);
+    for (int i = threadIdx.x; i < BK; i += 64) sidx[i] = a.idx[i];
+    __syncthreads();
+    if (blk < a.n_emb) {
+      query_bwd_emb(blk, a.dq, sidx, BK, a.wadj, a.D, a.W, a.demb, a.beta);
+      return;
+    }
+    blk -= a.n_emb;  // (beta 0) embedding row blk: zero unless a speaker of the batch owns it
+    for (int j0 = 0; j0 < BK; j0 += 64) {
+      const int j = j0 + (int)threadIdx.x;
+      if (__any(j < BK && sidx[j] == blk)) return;
+    }
     for (int c = threadIdx.x; c < a.W; c += 64) a.demb[(long long)blk * a.W + c] = 0.f;
     return;
   }
-  blk -= a.n_zero;
+  blk -= a.n_emb + a.n_zero;
   if (blk < a.n_dh) {
-    query_bwd_dh(blk % a.n_dh_x, blk / a.n_dh_x, a.dq, a.wadj, a.T, a.D, a.K, a.W, a.dh);
+    query_bwd_dh(blk % a.n_dh_x, blk / a.n_dh_x, sm, a.dq, a.wadj, a.T, a.D, a.K, a.W, a.dh);
     return;
   }
   blk -= a.n_dh;
@@ -383,11 +426,13 @@ DL4SS_API int dl4ss_query_bwd_ex(const float* dq, int B, int T, int D, const int
   a.n_dh = (w_adj && dh_bcast) ? a.n_dh_x * B : 0;
   a.n_w_x = (int)cdiv(D + W, 64);
   int n_w = 0;
-  size_t smem = 0;
+  size_t smem = a.n_emb + a.n_zero > 0 ? sizeof(int) * (size_t)B * K : 0;  // the embedding roles' staged ids
+  if (a.n_dh > 0 && sizeof(float) * (size_t)W > smem) smem = sizeof(float) * (size_t)W;  // dh: u[b][o]
   if (w_adj && d_wadj) {
     DL4SS_REQUIRE(mean && emb);
     n_w = a.n_w_x * W;
-    smem = sizeof(float) * (2 * (size_t)B * K + B);
+    const size_t sw = sizeof(float) * (2 * (size_t)B * K + B);
+    smem = sw > smem ? sw : smem;
   }
   const int nblk = a.n_emb + a.n_zero + a.n_dh + n_w;
   if (nblk == 0) return 0;
