@@ -56,11 +56,12 @@ template <int BM_, int STG_, int KT_ = 64>
 struct Cfg {
   static constexpr int BM = BM_, STG = STG_, KT = KT_, NT = 2 * BM_, NW = NT / 64;
   static constexpr int PPP = KT_ / 4;  // 1-KB DMA pieces per 128-row panel per k-tile
-  static constexpr int CPW_A = BM_ / 128 * PPP / NW, CPW_B = BN / 128 * PPP / NW;  // 1-KB DMAs per wave per k-tile
+  static constexpr int CPW_A = BM_ * KT_ / 512 / NW, CPW_B = BN * KT_ / 512 / NW;  // 1-KB DMAs per wave per k-tile
   static constexpr int IMG_A = BM_ * KT_, IMG_B = BN * KT_, STAGE = IMG_A + IMG_B;
   // LDS (bf16 elements): the stages, at least the epilogue's staging (NW waves x 32 rows x 68 fp32)
   static constexpr int SMEM = STG_ * STAGE > NW * 32 * 68 * 2 ? STG_ * STAGE : NW * 32 * 68 * 2;
-  static constexpr int WPC = NT != 256 ? 1 : SMEM * 2 <= 40 * 1024 ? 4 : SMEM * 2 <= 80 * 1024 ? 2 : 1;  // per CU
+  static constexpr int WPC = NT > 256 ? 1 : SMEM * 2 <= 40 * 1024 ? 4 : SMEM * 2 <= 53 * 1024 ? 3
+                             : SMEM * 2 <= 80 * 1024 ? 2 : 1;  // workgroups per CU
   static_assert(CPW_A >= 1 && CPW_B >= 1, "at least one DMA per wave and operand");
 };
 enum { EPI_NONE = 0, EPI_TANH = 1, EPI_TANH_BF16 = 2, EPI_SPLIT_SLABS = 3 };
@@ -831,6 +832,7 @@ typedef Cfg<128, 3> C128S3;  // 128 x 128, three stages (measured slower: A/B kn
 typedef Cfg<128, 5, 32> C128D5;  // 128 x 128, five 32-deep stages (80 KB), two per CU: the deep ring
 typedef Cfg<128, 4, 32> C128D4;  // the same with four stages (64 KB): three k-tiles in flight
 typedef Cfg<128, 2, 32> C128H2;  // 32-deep double buffer (32 KB): four workgroups per CU
+typedef Cfg<64, 2> C64;  // 64 x 128, two waves, double buffer (48 KB): three workgroups per CU
 // tile configuration: 0 = per shape (gl_cfg_for), 1 = C128, 2 = C256, 3 = C128S3, 4 / 5 = 256 x 256
 // ping-pong with 8 / 10 half-tile slots
 int g_gl_cfg = 0;
@@ -935,6 +937,8 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
   if (cfg == 6) return launch_cfg<A_KC, B_KC, C128D5>(GGL_ARGS);
   if (cfg == 7) return launch_cfg<A_KC, B_KC, C128D4>(GGL_ARGS);
   if (cfg == 8) return launch_cfg<A_KC, B_KC, C128H2>(GGL_ARGS);
+  // (64-row A images exist only in the k-contiguous layout: a k-major A runs the 128 x 128 tile)
+  if (cfg == 9) return A_KC ? launch_cfg<A_KC, B_KC, C64>(GGL_ARGS) : launch_cfg<A_KC, B_KC, C128>(GGL_ARGS);
   return launch_cfg<A_KC, B_KC, C128>(GGL_ARGS);
 #undef GGL_ARGS
 }
@@ -945,9 +949,9 @@ int launch(int M, int N, int K, const unsigned short* A, long long lda, const un
 // 128 x 128 double buffer, 2 = 256 x 128 three stages, 3 = 128 x 128 three stages, 4 = 256 x
 // 256 ping-pong, 128 KB LDS, 5 = the same with the whole 160 KB: six half-tiles in flight, 6 / 7 =
 // 128 x 128 deep ring: five / four 32-deep k-tile stages, four / three k-tiles in flight, 8 = 128 x 128
-// 32-deep double buffer, four workgroups per CU).
+// 32-deep double buffer, four workgroups per CU, 9 = 64 x 128 tiles, three workgroups per CU).
 DL4SS_API int dl4ss_gemm_gl_set_config(int cfg) {
-  DL4SS_REQUIRE(cfg >= 0 && cfg <= 8);
+  DL4SS_REQUIRE(cfg >= 0 && cfg <= 9);
   g_gl_cfg = cfg;
   return 0;
 }

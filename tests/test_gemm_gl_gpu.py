@@ -12,9 +12,9 @@ from dl4ss_amd import _lib, ops
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8], ids=["auto", "c128x128", "c256x128_3stage", "c128x128_3stage",
-                                                  "c256x256_pp8", "c256x256_pp10", "c128x128_deep5x32",
-                                                  "c128x128_deep4x32", "c128x128_2x32_4percu"],
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, 9], ids=["auto", "c128x128", "c256x128_3stage", "c128x128_3stage",
+                                                     "c256x256_pp8", "c256x256_pp10", "c128x128_deep5x32",
+                                                     "c128x128_deep4x32", "c128x128_2x32_4percu", "c64x128"],
                 autouse=True)
 def gl_config(request):
     """every tile configuration of gemm_gl.hip (forced through dl4ss_gemm_gl_set_config)"""
