@@ -909,6 +909,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_PUB_DPP
 #define FWD_PUB_DPP 1
 #endif
+#ifndef FWD_POLL3
+#define FWD_POLL3 0  // experiment: three granule sweeps in flight in the forward's polling waves (A/B)
+#endif
+#ifndef FWD_POLL_SLEEP
+#define FWD_POLL_SLEEP 0  // experiment: s_sleep (x 64 cycles) before a step's first granule sweep (A/B)
+#endif
+#ifndef BWD_POLL_SLEEP
+#define BWD_POLL_SLEEP 0
+#endif
   // FWD_STORE_WAVES (experiment, off): the saved-state stores of step s leave from waves 2-3
   // (matvec-only, idle after B2) during step s+1 instead of from the cell lanes after their publish:
   // the cell lanes stage {act, c, h_{t-1}, h} in LDS (double buffered by step parity), the last step
@@ -1157,6 +1166,51 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         // 13-16 % slower per step: DESIGN.md section 5).
         u32x4 v[GLK], qa[GLK], qb[GLK];
         unsigned done = 0;
+#if FWD_POLL_SLEEP
+        // (experiment) the first sweep of the step held back while this CU's own cell phase and publish
+        // run: no granule can land before the own publish, and the sweeps sit in the CU's memory queue
+        __builtin_amdgcn_s_sleep(FWD_POLL_SLEEP);
+#endif
+#if FWD_POLL3
+        // (experiment) three sweeps in flight: each merge samples a third of a round trip after the last
+        u32x4 qc[GLK];
+        auto fmerge = [&](const u32x4* q) __attribute__((always_inline)) {
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) {
+            const bool m = ((q[g].y >> 16) == tag) & ((q[g].w >> 16) == tag) & !((done >> g) & 1);
+            v[g] = m ? q[g] : v[g];
+            done |= (unsigned)m << g;
+          }
+        };
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int g = 0; g < GLK; ++g) qb[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+        unsigned spins = 0;
+        while (true) {
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) qc[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+          fmerge(qa);
+          if (done == (1u << GLK) - 1) break;
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+          fmerge(qb);
+          if (done == (1u << GLK) - 1) break;
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int g = 0; g < GLK; ++g) qb[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
+          fmerge(qc);
+          if (done == (1u << GLK) - 1) break;
+          if (++spins > a.spin_limit) {
+            atomicOr(a.status, 1);
+            return;
+          }
+        }
+#else
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + loff[g], 0, 16);
@@ -1190,6 +1244,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
             return;
           }
         }
+#endif
 #pragma unroll
         for (int g = 0; g < GLK; ++g) {
           const u32x4 x = v[g];
@@ -2027,6 +2082,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         const int sb = ((s - 1) & 1) * 2 * copy_g * 8;  // the slot's hand-off copy (bytes)
         u32x4 q[GLK], qa[GLK], qb[GLK];
         unsigned done = 0;
+#if BWD_POLL_SLEEP
+        __builtin_amdgcn_s_sleep(BWD_POLL_SLEEP);  // (experiment, as FWD_POLL_SLEEP)
+#endif
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int g = 0; g < GLK; ++g) qa[g] = __builtin_amdgcn_raw_buffer_load_b128(xr, sb + loff[g] * 8, 0, 16);
