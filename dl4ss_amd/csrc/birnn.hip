@@ -912,6 +912,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_POLL3
 #define FWD_POLL3 0  // experiment: three granule sweeps in flight in the forward's polling waves (A/B)
 #endif
+#ifndef FWD_GATE_LOADS_FIRST
+#define FWD_GATE_LOADS_FIRST 0  // experiment (A/B)
+#endif
 #ifndef FWD_POLL_SLEEP
 #define FWD_POLL_SLEEP 0  // experiment: s_sleep (x 64 cycles) before a step's first granule sweep (A/B)
 #endif
@@ -1365,9 +1368,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
         // whole-tile matvec's acc[0] + acc[1]; read unconditionally (a clamped address) and selected
         const int r3 = (NGATE - 1) * J + cu;
         const float x4 = sgx[cb * 16 + max(r3 - 64, 0)];
+        float mqs[NGATE];
+#pragma unroll
+        for (int q = 0; q < NGATE; ++q) mqs[q] = sgate[cb * SGS + q * J + cu];
+#if FWD_GATE_LOADS_FIRST
+        // every gate read issued before the first is used (hipcc placed the last gate's read after the
+        // first wait: a second LDS round trip on the output gate's chain)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int q = 0; q < NGATE; ++q) {
-          float mq = sgate[cb * SGS + q * J + cu];
+          float mq = mqs[q];
           if (q == NGATE - 1) mq = (t4h && r3 >= 64) ? mq + x4 : mq;
           hg[q] = bh[q] + mq;
           gx[q] = gxa[q];
