@@ -45,14 +45,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_TAG = "r06_prof_a"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
+PMC_TAG = "r06_prof_b"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
 PMC_FILE = f"profiles/{PMC_TAG}_pmc.json"
 MFMA_FILE = f"profiles/{PMC_TAG}_mfma.json"
 # the step's GEMM kernels as rocprofv3 names them (MFMA-busy counters are looked up by name): the
 # Linear + tanh -> bf16 V (the largest in-step dense contraction) and the input projection (a GEMM
 # only on the unfused path: the step forms it inside the recurrence, dl4ss_birnn_fwd_xw)
-GEMM_GL_LINEAR = "gemm_gl_kernel<true, true, 2, false, Cfg<128, 2> >"
-GEMM_GL_INPROJ = "gemm_gl_kernel<true, true, 0, false, Cfg<128, 2> >"
+GEMM_GL_LINEAR = "gemm_gl_kernel<true, true, 2, false, Cfg<128, 2, 64> >"
+GEMM_GL_INPROJ = "gemm_gl_kernel<true, true, 0, false, Cfg<128, 2, 64> >"
 BW_FILE = "profiles/r03_bw_probe.jsonl"  # tools/bw_probe.hip: plain streaming ceilings on MI355X
 
 
