@@ -688,6 +688,8 @@ __global__ __launch_bounds__(64) void pit_select_kernel(const float* __restrict_
   for (int k = 0; k < K; ++k) perm[b * K + k] = Perms<K>::P[best][k];
 }
 
+constexpr int FIN_CH = 8;      // finalize: loss items per thread loaded together
+constexpr int FIN_PMAX = 1024;  // finalize: permutation entries staged in LDS (B K <= this; else direct loads)
 // loss = s1 * sum_b sum_k C[b][k][perm k] + s2 * S ; also dq = sum_blk part_dq (fixed order)
 template <int K>
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int B, int nblk,
@@ -698,13 +700,34 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
   // block 0: loss, 256 fixed-stride fp64 partial sums + fixed-order tree (deterministic)
   if (blockIdx.x == 0) {
     __shared__ double r1[256], r2[256];
+    __shared__ int sperm[FIN_PMAX];
     double l1 = 0.0, l2 = 0.0;
-    for (int i = threadIdx.x; i < B * nblk; i += 256) {
-      const int b = i / nblk;
-      const float* p = part + (long long)i * (K * K + 1);
+    // the permutations staged in LDS first, then each thread's items loaded in chunks of FIN_CH
+    // before they are summed in item order (round 6: a perm load then the cost loads per item was
+    // two dependent rounds per item)
+    const bool lp = perm && B * K <= FIN_PMAX;
+    if (lp)
+      for (int i = threadIdx.x; i < B * K; i += 256) sperm[i] = perm[i];
+    __syncthreads();
+    for (int i0 = threadIdx.x; i0 < B * nblk; i0 += 256 * FIN_CH) {
+      float c[FIN_CH][K + 1];
 #pragma unroll
-      for (int k = 0; k < K; ++k) l1 += p[k * K + (perm ? perm[b * K + k] : k)];
-      l2 += p[K * K];
+      for (int u = 0; u < FIN_CH; ++u) {
+        const int i = min(i0 + 256 * u, B * nblk - 1), b = i / nblk;
+        const float* p = part + (long long)i * (K * K + 1);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          c[u][k] = p[k * K + (perm ? (lp ? sperm[b * K + k] : perm[b * K + k]) : k)];
+        c[u][K] = p[K * K];
+      }
+#pragma unroll
+      for (int u = 0; u < FIN_CH; ++u) {
+        if (i0 + 256 * u < B * nblk) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) l1 += c[u][k];
+          l2 += c[u][K];
+        }
+      }
     }
     r1[threadIdx.x] = l1;
     r2[threadIdx.x] = l2;
@@ -730,12 +753,18 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
       const int b = i / (K * qw), j = i % (K * qw);
       const float* pd = part_dq + (long long)b * nblk * K * qw + j;
       float a0 = 0.f, a1 = 0.f;
-      int blk = 0;
-      for (; blk + 1 < nblk; blk += 2) {
-        a0 += pd[(long long)blk * K * qw];
-        a1 += pd[(long long)(blk + 1) * K * qw];
+      // even blocks into a0, odd into a1, in block order; the loads of 32 blocks issued together
+      for (int b0 = 0; b0 < nblk; b0 += 32) {
+        float x[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) x[u] = pd[(long long)min(b0 + u, nblk - 1) * K * qw];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+          const bool in = b0 + u < nblk;
+          a0 = (in && !(u & 1)) ? a0 + x[u] : a0;
+          a1 = (in && (u & 1)) ? a1 + x[u] : a1;
+        }
       }
-      if (blk < nblk) a0 += pd[(long long)blk * K * qw];
       dq[i] = a0 + a1;
     }
   }
