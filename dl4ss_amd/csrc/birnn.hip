@@ -912,6 +912,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_POLL3
 #define FWD_POLL3 0  // experiment: three granule sweeps in flight in the forward's polling waves (A/B)
 #endif
+// The BPTT publish at batch chunks of 4: tiles 0-3's quads redistributed over the wave by DPP row shifts
+// into one full-wave 16-B store (round 6: bitwise the LDS-transposed form, -35 us per C2 step,
+// profiles/r06_bwd_pub_dpp_ab.txt); 0: the LDS transpose for every BC (A/B)
+#ifndef BWD_PUB_DPP
+#define BWD_PUB_DPP 1
+#endif
 #ifndef FWD_GATE_LOADS_FIRST
 #define FWD_GATE_LOADS_FIRST 0  // experiment (A/B)
 #endif
@@ -2326,8 +2332,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       store_dg();
       break;
     }
-    // ---- D[k][b] = sum_r W[r][k] dgh[b][r] per 16-unit tile, transposed through
-    //      wave-private LDS to [b][unit], packed four units per 16-B store
+    // ---- D[k][b] = sum_r W[r][k] dgh[b][r] per 16-unit tile, packed four units per 16-B store: at BC = 4
+    //      the quads are spread over the wave by DPP row shifts (BWD_PUB_DPP), otherwise transposed through
+    //      wave-private LDS to [b][unit].  (Round 4's register-direct form -- five 16-lane stores per wave --
+    //      lost to the transpose; the DPP form keeps the transpose's two full stores and drops its LDS trip.)
     {
       // rows >= BC of the dgh B image are zero: read row BC (broadcast, conflict-free B reads)
       const unsigned short* bp = sdgb + min(lane & 15, BC) * SDG + 8 * (lane >> 4);
@@ -2345,6 +2353,40 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 #pragma unroll
         for (int t2 = 0; t2 < MTWMAX; ++t2)
           acc[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t2][ks], bv[ks], acc[t2], 0, 0, 0);
+#if BWD_PUB_DPP
+      if constexpr (BC == 4 && MTWMAX == 5) {
+        // lane 16 g + b (b < 4) holds tile t's four units 16 t + 4 g .. + 3 of batch row b.  Tiles 0-3 go out
+        // in ONE full-wave 16-B store: lane 16 g + 4 t + b takes tile t's quad from lane 16 g + b by a DPP row
+        // shift of 4 t into bank t (no LDS transpose); tile 4 from its own 16 lanes
+        const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
+        f32x4 xq = acc[0];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int v = __float_as_int(xq[c]);
+          v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[1][c]), 0x114, 0xF, 0x2, false);  // row_shr:4
+          v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[2][c]), 0x118, 0xF, 0x4, false);  // row_shr:8
+          v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[3][c]), 0x11C, 0xF, 0x8, false);  // row_shr:12
+          xq[c] = __int_as_float(v);
+        }
+        const int bb = lane & 3, g = lane >> 4;
+        auto put = [&](const f32x4 v, int k) __attribute__((always_inline)) {
+          const unsigned r0 = pack24(v[0]), r1 = pack24(v[1]), r2 = pack24(v[2]), r3 = pack24(v[3]);
+          const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
+          const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules
+          if (wt)
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 16);  // sc1 write-through (group spans XCDs)
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);   // plain: stays in the group's L2
+        };
+        const int k0 = wv * WSPAN + 16 * ((lane >> 2) & 3) + 4 * g;
+        if (k0 < H) put(xq, k0);
+        const int k4 = wv * WSPAN + 64 + 4 * g;
+        if ((lane & 15) < 4 && k4 < H) put(acc[4], k4);
+        STAMP(4)
+        if (wv == 3) TRACE(0, s);
+      } else
+#endif
+      {
       if (col < BC) {
 #pragma unroll
         for (int t2 = 0; t2 < MTWMAX; ++t2)
@@ -2381,6 +2423,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         }
       }
       if (wv == 3) TRACE(0, s);
+      }
     }
     STAMP(5)
     // this step's dG / dGh, after the publish (off the critical path; issued after B1 of the next
