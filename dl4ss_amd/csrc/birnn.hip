@@ -2384,6 +2384,41 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         if ((lane & 15) < 4 && k4 < H) put(acc[4], k4);
         STAMP(4)
         if (wv == 3) TRACE(0, s);
+      } else if constexpr ((BC == 1 || BC == 2) && MTWMAX == 5) {
+        // BC <= 2: all five tiles fit one 16-lane row -- tile t's quad of row b into lane BC t + b by a
+        // row shift of BC t (bank mask of that lane group; tiles in increasing order, so a lane a shift
+        // filled with a neighbour's unused column is rewritten by the later tile that owns it), ONE store
+        const unsigned tag = (unsigned)(s + 1) & 0xFFFFu;
+        f32x4 xq = acc[0];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int v = __float_as_int(xq[c]);
+          if constexpr (BC == 2) {
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[1][c]), 0x112, 0xF, 0x1, false);  // row_shr:2
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[2][c]), 0x114, 0xF, 0x2, false);  // row_shr:4
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[3][c]), 0x116, 0xF, 0x2, false);  // row_shr:6
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[4][c]), 0x118, 0xF, 0x4, false);  // row_shr:8
+          } else {
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[1][c]), 0x111, 0xF, 0x1, false);  // row_shr:1
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[2][c]), 0x112, 0xF, 0x1, false);  // row_shr:2
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[3][c]), 0x113, 0xF, 0x1, false);  // row_shr:3
+            v = __builtin_amdgcn_update_dpp(v, __float_as_int(acc[4][c]), 0x114, 0xF, 0x2, false);  // row_shr:4
+          }
+          xq[c] = __int_as_float(v);
+        }
+        const int p = lane & 15, t = p / BC, bb = p % BC, g = lane >> 4;
+        const int k = wv * WSPAN + 16 * t + 4 * g;
+        if (p < 5 * BC && k < H) {
+          const unsigned r0 = pack24(xq[0]), r1 = pack24(xq[1]), r2 = pack24(xq[2]), r3 = pack24(xq[3]);
+          const u32x4 x = {r0 | (r1 << 24), (r1 >> 8) | (tag << 16), r2 | (r3 << 24), (r3 >> 8) | (tag << 16)};
+          const int off = (((s & 1) * 2 * NG + w) * BC + bb) * HG + (k >> 1);  // granules
+          if (wt)
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 16);  // sc1 write-through (group spans XCDs)
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(x, xr, off * 8, 0, 0);   // plain: stays in the group's L2
+        }
+        STAMP(4)
+        if (wv == 3) TRACE(0, s);
       } else
 #endif
       {

@@ -1,4 +1,4 @@
-"""Variant-library check: one eager + two graph C2 training steps (B = 32, BiLSTM-4L, PIT, bf16) from a
+"""Variant-library check: one eager + two graph training steps (default C2: B = 32, BiLSTM-4L, PIT, bf16) from a
 fixed seed with the library named by DL4SS_LIB (default: the shipped one); writes SHA-256 digests of the
 losses, the flat gradient and the updated parameters to argv[1] (JSON).  `--compare a b` reports whether two
 such records are bitwise equal."""
@@ -15,13 +15,15 @@ def run(out):
     from dl4ss_amd import engine, synth
 
     dev = torch.device("cuda")
-    B, K, N = 32, 2, 32000
+    # LIB_BW_CFG="B,cell,L" (default the C2 step: 32,lstm,4)
+    b_, cell, nl = os.environ.get("LIB_BW_CFG", "32,lstm,4").split(",")
+    B, K, N = int(b_), 2, 32000
     gen = synth.SyntheticMixtures(n_samples=N, k=K, seed=7)
     src, spk, u = gen.batch(B)
     batch = (torch.from_numpy(src.astype(np.float32)).to(dev),
              torch.from_numpy(synth.gains_for(u, K).astype(np.float32)).to(dev),
              torch.from_numpy(spk.astype(np.int32)).to(dev))
-    net = engine.SepNet(cell="lstm", num_layers=4, device=dev, seed=11)
+    net = engine.SepNet(cell=cell, num_layers=int(nl), adjust=cell == "lstm", device=dev, seed=11)
     tr = engine.SepTrainer(net, B, K, N, mode="pit", precision="bf16")
     losses = [tr.step(*batch).clone()] + [tr.step_graph(*batch).clone() for _ in range(2)]
     tr.check()
