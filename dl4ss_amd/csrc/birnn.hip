@@ -244,15 +244,17 @@ __device__ __forceinline__ void group_of(int bid, int NG, int ngroups, int& grou
 // p[q][(t + shift[q]) * stride[q]] (0 outside [0, T)), landing in LDS at dst[q].
 // Loads for step s+1 are issued during step s and committed to LDS at step s+1
 // (by then the granule poll has already waited past them).
-// NZ > 1 (the BPTT's dOut, DL4SS_RNN_DOUT_SLABS): an item with nz[q] > 1 is the sum of nz[q] split-K
+// NZ > 1 (the BPTT's dOut, DL4SS_RNN_DOUT_SLABS): an item with zq[q] set is the sum of NZ split-K
 // slabs zs floats apart, all loaded at issue and added at commit in slab order from zero -- bitwise the
-// gemm_gl split-K combine it replaces (((0 + s0) + s1) + ...).
+// gemm_gl split-K combine it replaces (((0 + s0) + s1) + ...).  NZ is the launch's exact slab count (a
+// kernel template argument): a runtime count per item (round 6's first form, NZ = 4 in every launch)
+// cost ~20 us per BPTT launch even at one slab (profiles/r06_nz_ab.txt).
 template <int NQ, int NZ = 1>
 struct StepLoader {
   const float* p[NQ];
   int stride[NQ], shift[NQ], dst[NQ];
   float v[NQ];
-  int nz[NQ];
+  bool zq[NQ];
   long long zs;
   float vz[NQ][NZ > 1 ? NZ - 1 : 1];
   __device__ __forceinline__ void issue(int t, int T) {
@@ -264,7 +266,7 @@ struct StepLoader {
       if constexpr (NZ > 1) {
 #pragma unroll
         for (int z = 1; z < NZ; ++z)
-          vz[q][z - 1] = (ok && z < nz[q]) ? p[q][(long long)tt * stride[q] + z * zs] : 0.0f;
+          vz[q][z - 1] = (ok && zq[q]) ? p[q][(long long)tt * stride[q] + z * zs] : 0.0f;
       }
     }
   }
@@ -274,11 +276,10 @@ struct StepLoader {
       if (dst[q] < 0) continue;
       float x = v[q];
       if constexpr (NZ > 1) {
-        if (nz[q] > 1) {
+        if (zq[q]) {
           x = 0.0f + v[q];
 #pragma unroll
-          for (int z = 1; z < NZ; ++z)
-            if (z < nz[q]) x += vz[q][z - 1];
+          for (int z = 1; z < NZ; ++z) x += vz[q][z - 1];
         }
       }
       lds[dst[q]] = x;
@@ -1869,7 +1870,7 @@ __device__ __forceinline__ unsigned pack24(float v) {
 }
 __device__ __forceinline__ float unpack24(unsigned r) { return __uint_as_float(r << 8); }
 
-template <int CELL, int BC>
+template <int CELL, int BC, int NZ = 1>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   constexpr int NGATE = CELL == CELL_LSTM ? 4 : 3;
   // partial-sum slots of the gather (polling waves): a lane group of BSL_Q lanes = every (b, quad)
@@ -1978,7 +1979,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   constexpr int NQA = PFF ? (CPWP + 63) / 64 : 1;
   const int ncell = BC * J, cpw = (ncell + 1) / 2, pwi = wv - WPF;
   float* sraw = sop + 2 * 2 * SOPP + (wv >= WPF ? pwi : 0) * NSL * CPWP;
-  StepLoader<NQ, 4> ld;  // dOut: up to 4 split-K slabs (DL4SS_RNN_DOUT_SLABS)
+  StepLoader<NQ, NZ> ld;  // dOut: NZ split-K slabs (DL4SS_RNN_DOUT_SLABS)
   ld.zs = a.dout_zs;
   const float4* ap[NQA];
   float4 av[NQA];
@@ -2046,7 +2047,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.stride[q] = stride;
     ld.shift[q] = shift;
     ld.dst[q] = !on ? -1 : PFF ? slot * CPWP + c : (slot >> 2) * SOPP + cell * 4 + (slot & 3);
-    ld.nz[q] = slot == 0 ? a.dout_ns : 1;
+    ld.zq[q] = slot == 0;
   }
   if (wv >= WPF) {
     ld.issue(d == 0 ? T - 1 : 0, T);
@@ -2671,6 +2672,13 @@ int launch_bwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStr
   bwd_dims(a.RPL, a.KGL, rpln, kgln);
 #ifdef RNN_EXP_MINIMAL
   if (BC != 4 || !mf || !pk) return (int)hipErrorNotSupported;
+#endif
+  if constexpr (BC == 4) {  // the dH GEMM's split-K slabs summed by the top layer (DL4SS_RNN_DOUT_SLABS)
+    if (mf && pk && a.dout_ns == 2) return launch_resident(rnn_bwd_pk_kernel<CELL, 4, 2>, grid, smem, st, a);
+    if (mf && pk && a.dout_ns == 3) return launch_resident(rnn_bwd_pk_kernel<CELL, 4, 3>, grid, smem, st, a);
+    if (mf && pk && a.dout_ns == 4) return launch_resident(rnn_bwd_pk_kernel<CELL, 4, 4>, grid, smem, st, a);
+  }
+#ifdef RNN_EXP_MINIMAL
   return launch_resident(rnn_bwd_pk_kernel<CELL, 4>, grid, smem, st, a);
 #else
   if (mf && pk)
@@ -3059,8 +3067,8 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   }
   // bf16 gradient copies, dropping the fp32 ones and the fused bias sums need the packed kernel
   DL4SS_REQUIRE(pk || (!dG_bf16 && !dGh_bf16 && !db_ih && !db_hh && dG && (cell == CELL_LSTM || dGh)));
-  // split-K dOut slabs: the packed BPTT's step-factor prefetch (batch chunks >= 4) sums them
-  DL4SS_REQUIRE(dout_ns == 1 || (pk && p.BC >= 4));
+  // split-K dOut slabs: the packed BPTT's step-factor prefetch at batch chunks of 4 sums them
+  DL4SS_REQUIRE(dout_ns == 1 || (pk && p.BC == 4));
   RnnArgs a{};
   fill_args(a, p, B, T, H);
   a.Whh = W_hh; a.act = const_cast<float*>(act); a.cs = const_cast<float*>(cs);

@@ -183,7 +183,7 @@ enum { DL4SS_CELL_LSTM = 0, DL4SS_CELL_GRU = 1 };
 /* precision field of dl4ss_birnn_bwd_ex (bits 12-13: S - 1): dOut is not one (B, T, 2H) array but the S
  * (2..4) fp32 split-K slabs dl4ss_gemm_bf16_gl leaves with DL4SS_EPI_SPLIT_SLABS, slab z at dOut + z B T 2H;
  * the BPTT sums them per element in slab order from zero (((0 + s0) + s1) + ...), bitwise the combine
- * launch it replaces.  Packed bf16 BPTT at batch chunks >= 4 only (hipErrorInvalidValue otherwise). */
+ * launch it replaces.  Packed bf16 BPTT at batch chunks of 4 only (hipErrorInvalidValue otherwise). */
 #define DL4SS_RNN_DOUT_SLABS(S) ((((S) - 1) & 3) << 12)
 int dl4ss_birnn_bias_reduce(int cell, int B, int H, int n, void* const* workspaces, float* const* db_ih,
                             float* const* db_hh, void* stream);
