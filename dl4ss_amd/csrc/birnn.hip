@@ -1861,6 +1861,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 #ifndef BWD_PF_LATE
 #define BWD_PF_LATE 1
 #endif
+// the packed BPTT's prefetch waves keep two steps' operand loads in flight (round 6); 0: one step ahead
+#ifndef BWD_PF2
+#define BWD_PF2 1
+#endif
 // the cell lanes' dG / dGh stores of step s-1 issued after B1 of step s (before the cell update)
 // instead of right after the publish: measured slower, 7994 vs 8085 mixtures/s
 // (profiles/r03_dglate.jsonl) -- their issue then sits on the cell phase's critical path
@@ -1983,6 +1987,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   ld.zs = a.dout_zs;
   const float4* ap[NQA];
   float4 av[NQA];
+#if BWD_PF2
+  StepLoader<NQ, NZ> ld2;  // odd steps' operands (BWD_PF2: two steps in flight)
+  float4 av2[NQA];
+#endif
   int ac[NQA];
 #pragma unroll
   for (int q = 0; q < NQA; ++q) {
@@ -1994,19 +2002,19 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ac[q] = ok ? c : -1;
     av[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  auto act_issue = [&](int t) {
+  auto act_issue = [&](float4* v, int t) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < NQA; ++q)
-      av[q] = ap[q] != nullptr ? ap[q][(long long)t * 2 * H] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[q] = ap[q] != nullptr ? ap[q][(long long)t * 2 * H] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  auto act_commit = [&]() {
+  auto act_commit = [&](const float4* v) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < NQA; ++q)
       if (ac[q] >= 0) {
-        sraw[1 * CPWP + ac[q]] = av[q].x;
-        sraw[2 * CPWP + ac[q]] = av[q].y;
-        sraw[3 * CPWP + ac[q]] = av[q].z;
-        sraw[4 * CPWP + ac[q]] = av[q].w;
+        sraw[1 * CPWP + ac[q]] = v[q].x;
+        sraw[2 * CPWP + ac[q]] = v[q].y;
+        sraw[3 * CPWP + ac[q]] = v[q].z;
+        sraw[4 * CPWP + ac[q]] = v[q].w;
       }
   };
 #pragma unroll
@@ -2049,9 +2057,19 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.dst[q] = !on ? -1 : PFF ? slot * CPWP + c : (slot >> 2) * SOPP + cell * 4 + (slot & 3);
     ld.zq[q] = slot == 0;
   }
+  auto tstep = [&](int s) { return d == 0 ? T - 1 - s : s; };  // time index of BPTT step s
+#if BWD_PF2
+  ld2 = ld;
+#endif
   if (wv >= WPF) {
-    ld.issue(d == 0 ? T - 1 : 0, T);
-    if constexpr (PFF) act_issue(d == 0 ? T - 1 : 0);
+    ld.issue(tstep(0), T);
+    if constexpr (PFF) act_issue(av, tstep(0));
+#if BWD_PF2
+    if (T > 1) {
+      ld2.issue(tstep(1), T);
+      if constexpr (PFF) act_issue(av2, tstep(1));
+    }
+#endif
     if constexpr (PFF && CELL == CELL_LSTM) {  // the first step's c (later steps reuse c_prev)
       const int t0 = d == 0 ? T - 1 : 0;
       for (int c = lane; c < cpw; c += 64) {
@@ -2163,9 +2181,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     // derivatives; GRU: the z / n / r products), into the record the cell lanes read after B1:
     //   LSTM {dOut, o (1 - tanh^2 c), g i (1 - i), c_prev f (1 - f)} {i (1 - g^2), tanh(c) o (1 - o), f, -}
     //   GRU  {dOut, (1-z)(1-n^2) hn r (1-r), (h_prev - n) z (1-z), (1-z)(1-n^2)} {(1-z)(1-n^2) r, z, -, -}
-    auto pf_factors = [&](int s) {
-      ld.commit(sraw);
-      act_commit();
+    auto pf_factors = [&](int s, const StepLoader<NQ, NZ>& L, const float4* A) __attribute__((always_inline)) {
+      L.commit(sraw);
+      act_commit(A);
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       // one lane per cell, in passes of 64: cpw = ceil(BC J / 2) is 80 at BC = 8, J = 20
@@ -2193,9 +2211,34 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         if constexpr (CELL == CELL_LSTM) sraw[5 * CPWP + c] = v[6];  // the next step's c
       }
     };
+#if BWD_PF2
+    // two steps in flight: step s's operands were issued in step s - 2 (ld for even s, ld2 for odd), so
+    // a load has a whole step more than the cell phase + hand-off window to land before the commit
+    // (round 6: with one step ahead the commit waited on them -- two more dOut loads per cell for the
+    // split-K slabs cost ~8 us per launch, profiles/r06_nz_ab.txt)
+    auto pf_step = [&](int s, StepLoader<NQ, NZ>& L, float4* A) __attribute__((always_inline)) {
+      if constexpr (PFF)
+        pf_factors(s, L, A);
+      else
+        L.commit(sop + (s & 1) * 2 * SOPP);
+      __syncthreads();  // B1
+      if (s + 2 < T) {
+        L.issue(tstep(s + 2), T);
+        if constexpr (PFF) act_issue(A, tstep(s + 2));
+      }
+      __syncthreads();  // B2
+    };
+    for (int s = 0; s < T; ++s) {
+      if (s & 1)
+        pf_step(s, ld2, av2);
+      else
+        pf_step(s, ld, av);
+      if (s + 1 == T) break;
+    }
+#else
     for (int s = 0; s < T; ++s) {
       if constexpr (PFF)
-        pf_factors(s);
+        pf_factors(s, ld, av);
       else
         ld.commit(sop + (s & 1) * 2 * SOPP);
 #if BWD_PF_LATE
@@ -2204,20 +2247,21 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       // in the consumer CU's queue); they still have the cell phase and the next poll window to land
       __syncthreads();  // B1
       if (s + 1 < T) {
-        ld.issue(d == 0 ? T - 2 - s : s + 1, T);
-        if constexpr (PFF) act_issue(d == 0 ? T - 2 - s : s + 1);
+        ld.issue(tstep(s + 1), T);
+        if constexpr (PFF) act_issue(av, tstep(s + 1));
       }
       __syncthreads();  // B2
 #else
       if (s + 1 < T) {
-        ld.issue(d == 0 ? T - 2 - s : s + 1, T);
-        if constexpr (PFF) act_issue(d == 0 ? T - 2 - s : s + 1);
+        ld.issue(tstep(s + 1), T);
+        if constexpr (PFF) act_issue(av, tstep(s + 1));
       }
       __syncthreads();  // B1
       __syncthreads();  // B2
 #endif
       if (s + 1 == T) break;
     }
+#endif
     return;
   }
 
