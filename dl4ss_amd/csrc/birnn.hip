@@ -905,6 +905,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #ifndef FWD_NT_HPREVB
 #define FWD_NT_HPREVB 1
 #endif
+#ifndef FWD_EXP_NOXDMA
+#define FWD_EXP_NOXDMA 0  // timing experiment only (results wrong): no x-row DMAs after the prologue
+#endif
 // The packed forward's publish gathers a granule pair's six bf16 h values by DPP wave shifts
 // (round 6); 0: through an LDS stage and read-back (the round-2..5 form, A/B)
 #ifndef FWD_PUB_DPP
@@ -1315,7 +1318,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_pk_kernel(RnnArgs a) {
 #if !FWD_XDMA_EARLY
         // step s + 3 SPB's rows into slot s % NSLOT, issued after B2 (off the matvec -> B2 path); that
         // slot held step s's rows, last read by the chain of block s / SPB, which ended before B1(s)
-        if (XW && s + NSLOT < T) xdma(s + NSLOT);
+        if (XW && !FWD_EXP_NOXDMA && s + NSLOT < T) xdma(s + NSLOT);
 #endif
         STAMP(4)
       }
@@ -1865,6 +1868,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 #ifndef BWD_PF2
 #define BWD_PF2 1
 #endif
+// timing experiment only (results wrong): 1 the prefetch waves issue no operand loads in the steps, 2 nor
+// form step factors.  Round 6: BPTT 331 -> 289 us per launch at 1 (the loads' price is paid in the
+// hand-off: they share the consumer CU's memory queue with the polls); non-temporal operand loads were
+// slower (376 us), the last forward layer's act / c saved with plain stores for the top BPTT no faster
+#ifndef BWD_EXP_PF
+#define BWD_EXP_PF 0
+#endif
 // the cell lanes' dG / dGh stores of step s-1 issued after B1 of step s (before the cell update)
 // instead of right after the publish: measured slower, 7994 vs 8085 mixtures/s
 // (profiles/r03_dglate.jsonl) -- their issue then sits on the cell phase's critical path
@@ -2217,12 +2227,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     // (round 6: with one step ahead the commit waited on them -- two more dOut loads per cell for the
     // split-K slabs cost ~8 us per launch, profiles/r06_nz_ab.txt)
     auto pf_step = [&](int s, StepLoader<NQ, NZ>& L, float4* A) __attribute__((always_inline)) {
+#if BWD_EXP_PF < 2
       if constexpr (PFF)
         pf_factors(s, L, A);
       else
         L.commit(sop + (s & 1) * 2 * SOPP);
+#endif
       __syncthreads();  // B1
-      if (s + 2 < T) {
+      if (BWD_EXP_PF == 0 && s + 2 < T) {
         L.issue(tstep(s + 2), T);
         if constexpr (PFF) act_issue(A, tstep(s + 2));
       }
@@ -2723,7 +2735,7 @@ int launch_bwd(const RnnArgs& a, bool mf, bool pk, int grid, size_t smem, hipStr
     if (mf && pk && a.dout_ns == 4) return launch_resident(rnn_bwd_pk_kernel<CELL, 4, 4>, grid, smem, st, a);
   }
 #ifdef RNN_EXP_MINIMAL
-  return launch_resident(rnn_bwd_pk_kernel<CELL, 4>, grid, smem, st, a);
+  return launch_resident(rnn_bwd_pk_kernel<CELL, 4, 1>, grid, smem, st, a);
 #else
   if (mf && pk)
     return launch_resident(rnn_bwd_pk_kernel<CELL, BC>, grid, smem, st, a);
