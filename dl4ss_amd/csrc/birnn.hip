@@ -1875,6 +1875,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 #ifndef BWD_EXP_PF
 #define BWD_EXP_PF 0
 #endif
+#if !defined(DL4SS_VARIANT_BUILD) && (BWD_EXP_PF || FWD_EXP_NOXDMA)
+#error "BWD_EXP_PF / FWD_EXP_NOXDMA are for tools/variant_lib.py builds only"
+#endif
 // the cell lanes' dG / dGh stores of step s-1 issued after B1 of step s (before the cell update)
 // instead of right after the publish: measured slower, 7994 vs 8085 mixtures/s
 // (profiles/r03_dglate.jsonl) -- their issue then sits on the cell phase's critical path
@@ -3131,6 +3134,9 @@ DL4SS_API int dl4ss_birnn_bwd_ex(int cell, int precision, int B, int T, int H, c
   a.hprev = const_cast<float*>(hprev); a.dOut = dOut; a.dOutB = dOut_bcast; a.dG = dG; a.dGh = dGh;
   a.dout_ns = dout_ns;
   a.dout_zs = (long long)B * T * 2 * H;
+#ifdef DL4SS_EXP_ZS_PAD
+  if (const char* e = getenv("DL4SS_EXP_ZS_PAD")) a.dout_zs += atoll(e);  // probe builds only
+#endif
   a.dGb = reinterpret_cast<unsigned short*>(dG_bf16); a.dGhb = reinterpret_cast<unsigned short*>(dGh_bf16);
   const int GHc = (cell == CELL_LSTM ? 4 : 3) * H;
   a.ghb = dgh_pad8 ? (GHc + 7) / 8 * 8 : GHc;

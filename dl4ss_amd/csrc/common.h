@@ -9,8 +9,8 @@
 // variant libraries tools/variant_lib.py builds (it defines DL4SS_VARIANT_BUILD): a stray -D in a
 // product build stops the compile instead of shipping a library that silently skips work.
 #if !defined(DL4SS_VARIANT_BUILD) && (defined(FWD_EXP_SKIP) || defined(BWD_EXP_NO_DG) || defined(GGL_NO_STORE) || \
-                                      defined(RNN_EXP_MINIMAL))
-#error "FWD_EXP_SKIP / BWD_EXP_NO_DG / GGL_NO_STORE / RNN_EXP_MINIMAL are for tools/variant_lib.py builds only"
+                                      defined(RNN_EXP_MINIMAL) || defined(DL4SS_EXP_ZS_PAD))
+#error "FWD_EXP_SKIP / BWD_EXP_NO_DG / GGL_NO_STORE / RNN_EXP_MINIMAL / DL4SS_EXP_ZS_PAD are for tools/variant_lib.py builds only"
 #endif
 
 #define DL4SS_CHECK_LAUNCH()                        \

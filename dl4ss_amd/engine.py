@@ -369,7 +369,9 @@ class SepTrainer:
             plan = ops.birnn_plan(net.cell, B, H) if dev.type == "cuda" else None
             nsl = _lib.query("dl4ss_gemm_bf16_gl_ws_bytes", BT, 2 * H, F * net.E, max(1, self.dh_split), 1) // \
                 (BT * 2 * H * 4)
-            if os.environ.get("DL4SS_DH_SLABS", "1") != "0" and plan is not None and plan["BC"] == 4 and 2 <= nsl <= 4:
+            # three slabs only: the BPTT's two- and four-slab instances measured 366 / 437 us per launch
+            # against 308 for one or three slabs (tools/slab_probe.py, profiles/r06_slab_probe.jsonl)
+            if os.environ.get("DL4SS_DH_SLABS", "1") != "0" and plan is not None and plan["BC"] == 4 and nsl == 3:
                 self.dh_slabs = int(nsl)
                 # the slabs' own workspace: other split-K GEMMs between dH and the BPTT (dW_lin off the side
                 # stream) must not overwrite them
