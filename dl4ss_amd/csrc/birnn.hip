@@ -1868,6 +1868,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_kernel(RnnArgs a) {
 #ifndef BWD_PF2
 #define BWD_PF2 1
 #endif
+// ... as straight-line even / odd pairs with the loads issued every step (round 6: hipcc's waitcnt pass
+// then keeps the newer step's loads in flight at each commit -- BPTT 331 -> 322 us per launch, bitwise,
+// profiles/r06_pf2_unroll_ab.txt); 0: the even / odd branch form
+#ifndef BWD_PF2_UNROLL
+#define BWD_PF2_UNROLL 1
+#endif
 // timing experiment only (results wrong): 1 the prefetch waves issue no operand loads in the steps, 2 nor
 // form step factors.  Round 6: BPTT 331 -> 289 us per launch at 1 (the loads' price is paid in the
 // hand-off: they share the consumer CU's memory queue with the polls); non-temporal operand loads were
@@ -2243,6 +2249,27 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       }
       __syncthreads();  // B2
     };
+#if BWD_PF2_UNROLL
+    // the even / odd pair as straight-line code, the loads issued every step (past the end the last
+    // step's again, unused): the same loads in flight at every commit, for hipcc's waitcnt pass
+    auto pf_step_u = [&](int s, StepLoader<NQ, NZ>& L, float4* A) __attribute__((always_inline)) {
+      if constexpr (PFF)
+        pf_factors(s, L, A);
+      else
+        L.commit(sop + (s & 1) * 2 * SOPP);
+      __syncthreads();  // B1
+      const int tn = tstep(min(s + 2, T - 1));
+      L.issue(tn, T);
+      if constexpr (PFF) act_issue(A, tn);
+      __syncthreads();  // B2
+    };
+    int s = 0;
+    for (; s + 1 < T; s += 2) {
+      pf_step_u(s, ld, av);
+      pf_step_u(s + 1, ld2, av2);
+    }
+    if (s < T) pf_step_u(s, ld, av);
+#else
     for (int s = 0; s < T; ++s) {
       if (s & 1)
         pf_step(s, ld2, av2);
@@ -2250,6 +2277,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         pf_step(s, ld, av);
       if (s + 1 == T) break;
     }
+#endif
 #else
     for (int s = 0; s < T; ++s) {
       if constexpr (PFF)
