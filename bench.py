@@ -45,7 +45,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK = {"fp32": 157.3, "bf16": 2500.0}  # dense TFLOP/s (F32 MFMA / BF16 MFMA)
 
 
-PMC_TAG = "r06_prof_d"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
+PMC_TAG = "r06_prof_e"  # tools/prof_round.sh + tools/summarize_prof.py session of this bench command
 PMC_FILE = f"profiles/{PMC_TAG}_pmc.json"
 MFMA_FILE = f"profiles/{PMC_TAG}_mfma.json"
 # the step's GEMM kernels as rocprofv3 names them (MFMA-busy counters are looked up by name): the
