@@ -2006,10 +2006,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
   ld.zs = a.dout_zs;
   const float4* ap[NQA];
   float4 av[NQA];
-#if BWD_PF2
-  StepLoader<NQ, NZ> ld2;  // odd steps' operands (BWD_PF2: two steps in flight)
+  // BWD_PF2 at batch chunks >= 4 (the step-factor prefetch): two steps in flight, ld2 / av2 the odd
+  // steps' operands.  At BC <= 2 (raw operands straight into the record) one step ahead stays: C1's
+  // B = 1 step measured 461 vs 468 mixtures/s with two (profiles/r06_cfg_pf2.txt)
+  constexpr bool PF2 = BWD_PF2 && PFF;
+  StepLoader<NQ, NZ> ld2;
   float4 av2[NQA];
-#endif
   int ac[NQA];
 #pragma unroll
   for (int q = 0; q < NQA; ++q) {
@@ -2077,18 +2079,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
     ld.zq[q] = slot == 0;
   }
   auto tstep = [&](int s) { return d == 0 ? T - 1 - s : s; };  // time index of BPTT step s
-#if BWD_PF2
-  ld2 = ld;
-#endif
+  if constexpr (PF2) ld2 = ld;
   if (wv >= WPF) {
     ld.issue(tstep(0), T);
     if constexpr (PFF) act_issue(av, tstep(0));
-#if BWD_PF2
-    if (T > 1) {
+    if (PF2 && T > 1) {
       ld2.issue(tstep(1), T);
       if constexpr (PFF) act_issue(av2, tstep(1));
     }
-#endif
     if constexpr (PFF && CELL == CELL_LSTM) {  // the first step's c (later steps reuse c_prev)
       const int t0 = d == 0 ? T - 1 : 0;
       for (int c = lane; c < cpw; c += 64) {
@@ -2230,7 +2228,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
         if constexpr (CELL == CELL_LSTM) sraw[5 * CPWP + c] = v[6];  // the next step's c
       }
     };
-#if BWD_PF2
+    if constexpr (PF2) {
     // two steps in flight: step s's operands were issued in step s - 2 (ld for even s, ld2 for odd), so
     // a load has a whole step more than the cell phase + hand-off window to land before the commit
     // (round 6: with one step ahead the commit waited on them -- two more dOut loads per cell for the
@@ -2278,7 +2276,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
       if (s + 1 == T) break;
     }
 #endif
-#else
+    } else {
     for (int s = 0; s < T; ++s) {
       if constexpr (PFF)
         pf_factors(s, ld, av);
@@ -2304,7 +2302,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_pk_kernel(RnnArgs a) {
 #endif
       if (s + 1 == T) break;
     }
-#endif
+    }
     return;
   }
 
