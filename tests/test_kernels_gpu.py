@@ -191,7 +191,10 @@ def _manual_birnn(cell, G, whh, bhh, H, bf16=False):
 
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("cell", ["lstm", "gru"])
-@pytest.mark.parametrize("B,T,H", [(1, 5, 300), (3, 8, 300), (2, 6, 40), (32, 12, 300)])
+# (32, T <= 3, 300): the packed BPTT at batch chunks of 4 with one, two, three steps -- the even / odd step
+# loaders of its two-step prefetch (BWD_PF2) at their edges
+@pytest.mark.parametrize("B,T,H", [(1, 5, 300), (3, 8, 300), (2, 6, 40), (32, 12, 300), (32, 1, 300), (32, 2, 300),
+                                   (32, 3, 300)])
 def test_birnn_bwd_dG_per_step(dev, cell, B, T, H, prec):
     """prec 0: exact fp32 recurrence vs fp64 (1e-5 abs on h, 1e-4 rel on dG).
     prec 1: bf16-operand MFMA recurrence vs an fp64 recurrence with the same operand
